@@ -1,0 +1,71 @@
+"""ORACLE (test infrastructure only) — ctypes binding of oracle/libcmpc_oracle.so,
+the plain-C condensed IPM restatement (cmpc_oracle.c).
+
+Problems are plain dicts of numpy arrays (batch-major):
+  nx nu N ns mc                 ints
+  Q (nx,nx) R (nu,nu) dR (nu,nu) Qs (ns,)  u_ub (nu,) u_lb (nu,)
+  row_slack (mc,) int (-1: none)   row_sign (mc,) int (+1/-1)
+  A (B,N,nx,nx) B (B,N,nx,nu) x0 (B,nx) u_prev (B,nu)
+  qlin (B,N+1,nx)   C (B,N,mc,nx)  h (B,N,mc)
+"""
+import ctypes as ct
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB = None
+
+
+def build():
+    subprocess.run(["make", "-s", "-C", _HERE], check=True)
+
+
+def lib():
+    global _LIB
+    if _LIB is None:
+        path = os.path.join(_HERE, "libcmpc_oracle.so")
+        if not os.path.exists(path):
+            build()
+        _LIB = ct.CDLL(path)
+        _LIB.cmpc_oracle_solve.restype = ct.c_int
+    return _LIB
+
+
+def _d(a):
+    a = np.ascontiguousarray(a, dtype=np.float64)
+    return a, a.ctypes.data_as(ct.POINTER(ct.c_double))
+
+
+def _i(a):
+    a = np.ascontiguousarray(a, dtype=np.int32)
+    return a, a.ctypes.data_as(ct.POINTER(ct.c_int))
+
+
+def nz_of(p):
+    return (p["nx"] + p["ns"]) * (p["N"] + 1) + 2 * p["nu"] * p["N"]
+
+
+def solve_batch(p, tol=1e-11, max_iter=60, nthreads=0):
+    nb = p["A"].shape[0]
+    keep = []
+    args = []
+    for k in ("Q", "R", "dR", "Qs", "u_ub", "u_lb"):
+        a, ptr = _d(p[k]); keep.append(a); args.append(ptr)
+    for k in ("row_slack", "row_sign"):
+        a, ptr = _i(p[k]); keep.append(a); args.append(ptr)
+    for k in ("A", "B", "x0", "u_prev", "qlin", "C", "h"):
+        a, ptr = _d(p[k]); keep.append(a); args.append(ptr)
+    z = np.zeros((nb, nz_of(p)))
+    kkt = np.zeros(nb)
+    iters = np.zeros(nb, np.int32)
+    status = np.zeros(nb, np.int32)
+    rc = lib().cmpc_oracle_solve(
+        ct.c_int(p["nx"]), ct.c_int(p["nu"]), ct.c_int(p["N"]), ct.c_int(p["ns"]), ct.c_int(p["mc"]),
+        ct.c_int(nb), *args, ct.c_double(tol), ct.c_int(max_iter), ct.c_int(nthreads),
+        z.ctypes.data_as(ct.POINTER(ct.c_double)), kkt.ctypes.data_as(ct.POINTER(ct.c_double)),
+        iters.ctypes.data_as(ct.POINTER(ct.c_int)), status.ctypes.data_as(ct.POINTER(ct.c_int)))
+    if rc != 0:
+        raise RuntimeError("cmpc_oracle_solve failed")
+    return z, kkt, iters, status
