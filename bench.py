@@ -1,0 +1,203 @@
+"""Benchmark: agent-QP solves/s for the whole node (BASELINE.json metric) on the
+per-control-step distributed QP loop, device-resident, one process per GPU.
+
+A step = one consensus round over every agent of every rank:
+  build (stage rows / costs from the exchanged trajectories, cmpc_di_build_dev)
+  -> batched condensed IPM, one wavefront per agent (cmpc_solve_mpc_batch_dev)
+  -> round advance (cmpc_di_advance_dev) -> RCCL all-gather of predicted positions.
+Workload (BASELINE.json configs[2], the config the metric is quoted on):
+1024 agents per GPU, N=30, 2-D double integrator (nx=4, nu=2), nb=2 neighbours,
+fp64 — weak scaling (1024 agents per rank; the 4096-agent cfg4 at 4 GPUs).
+
+Usage: python bench.py [--gpus N --steps K --warmup W]
+       (N>1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...)
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "colaborativempc-_amd"))
+sys.path.insert(0, ROOT)
+
+METRIC = "agent-QP solves/sec (whole node) at N=30, nx=4 nu=2; max KKT residual vs ref"
+FP64_PEAK_TFLOPS = 78.6   # MI355X dense FP64 (vector == matrix), spec
+HBM_PEAK_GBS = 8000.0
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--agents", type=int, default=1024, help="agents per GPU")
+    ap.add_argument("--horizon", type=int, default=30)
+    ap.add_argument("--nb", type=int, default=2)
+    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="target CPU-baseline sample time")
+    ap.add_argument("--no-cpu", action="store_true")
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    import cmpc
+    from cmpc import scenarios as S
+    from cmpc.rounds import DIRounds
+
+    n_total = args.agents * world
+    scen = S.make_di(n_total, args.horizon, args.nb, 2)
+    ctx = cmpc.Context(local)
+    R = DIRounds(scen, rank=rank, world=world, device=local, ctx=ctx)
+
+    def barrier():
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    for _ in range(args.warmup):
+        R.step()
+    barrier()
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    iters_sum = torch.zeros((), dtype=torch.float64, device=dev)
+    kkt_max = torch.zeros((), dtype=torch.float64, device=dev)
+    bad = torch.zeros((), dtype=torch.int64, device=dev)
+    barrier()
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        R.step(timer=ev[k])
+        iters_sum += R.iters.to(torch.float64).sum()
+        kkt_max = torch.maximum(kkt_max, R.kkt.max())
+        bad += (R.status != cmpc.CMPC_SOLVED).sum()
+    barrier()
+    elapsed = time.perf_counter() - t0
+    kern_ms = sum(a.elapsed_time(b) for a, b in ev) / args.steps
+
+    stats = torch.tensor([elapsed, kern_ms, kkt_max.item(), float(bad.item())], dtype=torch.float64, device=dev)
+    tot = torch.tensor([iters_sum.item()], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(stats, op=dist.ReduceOp.MAX)
+        dist.all_reduce(tot, op=dist.ReduceOp.SUM)
+    elapsed, kern_ms, kkt_all, bad_all = stats.tolist()
+    mean_iters = tot.item() / (n_total * args.steps)
+
+    value = n_total * args.steps / elapsed
+    sh = scen.shared
+    nx, nu, N, mc = sh["nx"], sh["nu"], sh["N"], sh["mc"]
+    m_rows = N * mc + 2 * nu * N
+    flops = S.alg_flops(nx, nu, N, m_rows, mean_iters)
+    achieved_tf = flops * args.agents / (kern_ms * 1e-3) / 1e12
+    alg_bytes = S.di_alg_bytes(nx, nu, N, args.nb)
+    traffic = None
+    pmc = os.path.join(ROOT, "profiles", "pmc_r01.json")
+    if os.path.exists(pmc):
+        try:
+            with open(pmc) as f:
+                traffic = json.load(f).get("mpc_ipm_kernel", {}).get("hbm_bytes_per_launch")
+        except Exception:
+            traffic = None
+
+    cpu = None
+    max_err = None
+    if rank == 0 and world == 1 and not args.no_cpu:
+        cpu, max_err = cpu_baseline(R, args.cpu_seconds)
+
+    if rank == 0:
+        out = {
+            "metric": METRIC,
+            "value": value,
+            "unit": "agent-QP/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": elapsed / args.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic (seeded double-integrator agent population, SURVEY.md §8d)",
+            "config": {
+                "workload": f"cfg3: {args.agents} agents/GPU, N={N}, 2-D double integrator nx={nx} nu={nu}, "
+                            f"nb={args.nb}, fp64 condensed IPM; step = build+solve+advance+all-gather",
+                "agents_total": n_total, "horizon": N, "nx": nx, "nu": nu, "neighbours": args.nb,
+                "parallelism": f"agents sharded over {world} GPU(s), RCCL all-gather per round",
+            },
+            "max_kkt": kkt_all,
+            "unsolved": int(bad_all),
+            "mean_ipm_iters": mean_iters,
+            "max_abs_err_vs_cpu": max_err,
+            "roofline": {
+                "kernel": "mpc_ipm_kernel",
+                "bound": "mfma",
+                "achieved": achieved_tf,
+                "peak": FP64_PEAK_TFLOPS,
+                "unit": "TFLOP/s",
+                "frac": achieved_tf / FP64_PEAK_TFLOPS,
+                "traffic": traffic,
+                "kernel_ms_per_launch": kern_ms,
+                "alg_flops_per_qp": flops,
+                "alg_bytes_per_qp": alg_bytes,
+                "hbm_alg_GBs": alg_bytes * args.agents / (kern_ms * 1e-3) / 1e9,
+                "hbm_frac": alg_bytes * args.agents / (kern_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+            },
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(out))
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def cpu_baseline(R, seconds):
+    """The oracle's plain-C restatement (oracle/cmpc_oracle.c, OpenMP) on a bounded
+    sample of the SAME round problem the GPU solves: build the current round on the
+    device, copy it to the host, time the CPU solve of the first S agents."""
+    import torch
+
+    from oracle import cmpc_oracle as CO
+
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
+    R.build()
+    prob = R.snapshot()
+    R.solve()
+    torch.cuda.synchronize()
+    zg = R.z.cpu().numpy()
+
+    def take(n):
+        p = dict(prob)
+        for k in ("A", "B", "x0", "u_prev", "qlin", "C", "h"):
+            p[k] = prob[k][:n]
+        return p
+
+    B = prob["A"].shape[0]
+    n0 = min(B, 4 * threads)
+    t = time.perf_counter()
+    CO.solve_batch(take(n0), nthreads=threads)
+    dt0 = time.perf_counter() - t
+    reps = max(1, int(seconds / max(dt0, 1e-6)))
+    # sample = `reps` passes over the first n0 agents (bounded CPU time), plus one full-batch check
+    t = time.perf_counter()
+    for _ in range(reps):
+        zc, _, _, _ = CO.solve_batch(take(n0), nthreads=threads)
+    el = time.perf_counter() - t
+    err = float(np.abs(zg[:n0] - zc).max())
+    return ({"value": reps * n0 / el, "unit": "agent-QP/s", "cores": threads, "kind": "port",
+             "sample": f"{reps} x {n0} agents of one cfg3 round (same device-built problems), "
+                       f"oracle/cmpc_oracle.c fp64, OpenMP {threads} threads, {el:.1f} s"}, err)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,119 @@
+"""Device-resident consensus-round driver (the collaborative loop of
+planner/scripts/LPV_HP_N_main.py:96-120, and of the one-process-per-agent ROS
+variant ROS/src/planner_experiments/src/LPV_ROS_main.py:124-150, re-designed as
+one process per GPU).
+
+Each round, on the GPU and on one stream:
+  1. build   — every local agent's stage rows / linear cost from the previous
+               round's exchanged trajectories            (cmpc_di_build_dev)
+  2. solve   — batched condensed IPM, one wavefront per agent  (cmpc_solve_mpc_batch_dev)
+  3. advance — x0 <- x_1, u_prev <- u_0, local trajectory <- predicted positions
+               (LPV_HP_N_main.py:106-117)                (cmpc_di_advance_dev)
+  4. exchange — all-gather of the (N+1) x 2 fp64 predicted positions of every
+               agent over RCCL (torch.distributed "nccl" backend) — the
+               replacement of the ROS topic exchange / np.swapaxes at :117.
+
+Agents are sharded contiguously across ranks (they are ordered along the road,
+so most neighbours are local); every rank holds the full gathered trajectory
+buffer, which is what a Jacobi round needs.
+"""
+from __future__ import annotations
+
+import ctypes as ct
+
+import numpy as np
+
+from . import _lib as L
+from .solver import _dims, _tptr, _weights, nz_of
+
+
+class DIRounds:
+    def __init__(self, scen, rank=0, world=1, device=None, ctx=None, tol=None, max_iter=None, group=None):
+        import torch
+
+        self.torch = torch
+        self.scen, self.rank, self.world, self.group = scen, rank, world, group
+        if scen.n_agents % world:
+            raise ValueError("n_agents must be divisible by the number of ranks")
+        self.dev = torch.device("cuda", torch.cuda.current_device() if device is None else device)
+        self.ctx = ctx or L.default_context(self.dev.index)
+        sl = scen.shard(rank, world)
+        self.off = sl.start
+        self.B = sl.stop - sl.start
+        self.N, self.nb = scen.N, scen.nb
+        sh = scen.shared
+        self.shared = sh
+        T = lambda a, dt=torch.float64: torch.as_tensor(np.ascontiguousarray(a), dtype=dt, device=self.dev)
+        self.A = T(scen.A[sl])
+        self.Bm = T(scen.B[sl])
+        self.x0 = T(scen.x0[sl])
+        self.u_prev = T(scen.u_prev[sl])
+        self.lane = T(scen.lane[sl])
+        self.nbr = T(scen.nbr[sl], torch.int32)
+        self.traj_all = T(scen.traj)
+        self.traj_local = torch.empty((self.B, self.N + 1, 2), dtype=torch.float64, device=self.dev)
+        nx, mc = sh["nx"], sh["mc"]
+        self.qlin = torch.empty((self.B, self.N + 1, nx), dtype=torch.float64, device=self.dev)
+        self.C = torch.empty((self.B, self.N, mc, nx), dtype=torch.float64, device=self.dev)
+        self.h = torch.empty((self.B, self.N, mc), dtype=torch.float64, device=self.dev)
+        self.z = torch.empty((self.B, nz_of(sh)), dtype=torch.float64, device=self.dev)
+        self.kkt = torch.empty(self.B, dtype=torch.float64, device=self.dev)
+        self.iters = torch.empty(self.B, dtype=torch.int32, device=self.dev)
+        self.status = torch.empty(self.B, dtype=torch.int32, device=self.dev)
+        p = scen.params
+        self.dprm = L.cmpc_di_params(int(p["dim"]), *(float(p[k]) for k in ("v_ref", "q_v", "q_lane", "hw",
+                                                                              "min_vel", "max_vel", "min_dist",
+                                                                              "wq")))
+        self.ddims = L.cmpc_di_dims(self.B, self.N, self.nb, self.off)
+        self.mdims = _dims(sh, self.B)
+        self.w, self._wkeep = _weights(sh)
+        self.opts = L.opts(tol, max_iter)
+        self.data = L.cmpc_mpc_data(*[_tptr(t) for t in (self.A, self.Bm, self.x0, self.u_prev, self.qlin,
+                                                          self.C, self.h)])
+        self.out = L.cmpc_mpc_out(_tptr(self.z), _tptr(self.kkt), _tptr(self.iters), _tptr(self.status))
+
+    def _stream(self):
+        return ct.c_void_p(self.torch.cuda.current_stream(self.dev).cuda_stream)
+
+    def build(self):
+        lib = self.ctx.lib
+        self.ctx.check(lib.cmpc_di_build_dev(self.ctx.h, ct.byref(self.dprm), ct.byref(self.ddims), _tptr(self.nbr),
+                                             _tptr(self.lane), _tptr(self.traj_all), _tptr(self.qlin),
+                                             _tptr(self.C), _tptr(self.h), self._stream()))
+
+    def solve(self):
+        self.ctx.check(self.ctx.lib.cmpc_solve_mpc_batch_dev(self.ctx.h, ct.byref(self.mdims), ct.byref(self.w),
+                                                             ct.byref(self.data), ct.byref(self.out),
+                                                             ct.byref(self.opts), self._stream()))
+
+    def advance(self):
+        self.ctx.check(self.ctx.lib.cmpc_di_advance_dev(self.ctx.h, ct.byref(self.dprm), ct.byref(self.ddims),
+                                                        _tptr(self.z), _tptr(self.x0), _tptr(self.u_prev),
+                                                        _tptr(self.traj_local), self._stream()))
+
+    def exchange(self):
+        if self.world == 1:
+            self.traj_all.copy_(self.traj_local)
+        else:
+            import torch.distributed as dist
+
+            dist.all_gather_into_tensor(self.traj_all, self.traj_local, group=self.group)
+
+    def step(self, timer=None):
+        """One consensus round.  `timer` (start, stop) events bracket the solve launch."""
+        self.build()
+        if timer is not None:
+            timer[0].record()
+        self.solve()
+        if timer is not None:
+            timer[1].record()
+        self.advance()
+        self.exchange()
+
+    def snapshot(self):
+        """Host copy of this rank's current structured problem (for checkers)."""
+        p = dict(self.shared)
+        for k, t in (("A", self.A), ("B", self.Bm), ("x0", self.x0), ("u_prev", self.u_prev), ("qlin", self.qlin),
+                     ("C", self.C), ("h", self.h)):
+            p[k] = t.detach().cpu().numpy().copy()
+        return p

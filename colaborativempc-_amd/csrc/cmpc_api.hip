@@ -1,0 +1,337 @@
+// C ABI of libcmpc (include/cmpc.h): context management, host<->device staging
+// and dispatch of the batched kernels.  No CPU solver exists behind this ABI:
+// without a gfx950 device every entry point fails with CMPC_ERR_DEVICE.
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+
+#include "internal.h"
+
+struct cmpc_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;  // private stream for the host-pointer entry points
+    char* ws = nullptr;            // device arena
+    size_t ws_bytes = 0;
+    std::string err;
+};
+
+namespace {
+
+int fail(cmpc_ctx* c, int code, const std::string& msg) {
+    if (c) c->err = msg;
+    return code;
+}
+
+int hip_fail(cmpc_ctx* c, hipError_t e, const char* where) {
+    return fail(c, CMPC_ERR_DEVICE, std::string(where) + ": " + hipGetErrorString(e));
+}
+
+#define HIP_TRY(expr)                                    \
+    do {                                                 \
+        hipError_t e_ = (expr);                          \
+        if (e_ != hipSuccess) return hip_fail(ctx, e_, #expr); \
+    } while (0)
+
+// Ensure the device arena holds `bytes`; returns base pointer or nullptr.
+char* arena(cmpc_ctx* ctx, size_t bytes) {
+    if (ctx->ws_bytes >= bytes) return ctx->ws;
+    if (ctx->ws) {
+        (void)hipStreamSynchronize(ctx->stream);
+        (void)hipFree(ctx->ws);
+        ctx->ws = nullptr;
+        ctx->ws_bytes = 0;
+    }
+    size_t want = bytes + bytes / 4 + (1 << 20);
+    if (hipMalloc(&ctx->ws, want) != hipSuccess) return nullptr;
+    ctx->ws_bytes = want;
+    return ctx->ws;
+}
+
+struct Carve {
+    char* base;
+    size_t off = 0;
+    template <class T>
+    T* take(size_t count) {
+        off = (off + 255) & ~size_t(255);
+        T* p = reinterpret_cast<T*>(base + off);
+        off += count * sizeof(T);
+        return p;
+    }
+};
+
+size_t mpc_nz(const cmpc_mpc_dims& d) { return (size_t)(d.nx + d.ns) * (d.N + 1) + 2 * (size_t)d.nu * d.N; }
+
+int set_device(cmpc_ctx* ctx) {
+    hipError_t e = hipSetDevice(ctx->device);
+    return e == hipSuccess ? CMPC_OK : hip_fail(ctx, e, "hipSetDevice");
+}
+
+int build_lpv_const(cmpc_ctx* ctx, const cmpc_lpv_params* prm, const cmpc_track* tr, const cmpc_lpv_dims* d,
+                    cmpc::LpvConst* c) {
+    if (!prm || !tr || !d) return fail(ctx, CMPC_ERR_ARG, "null argument");
+    if (tr->nseg < 1 || tr->nseg > CMPC_MAX_SEG) return fail(ctx, CMPC_ERR_UNSUPPORTED, "track has 1..32 segments");
+    if (d->N < 1 || d->nb < 0 || 4 + d->nb > CMPC_MAX_MC || (d->last_rows != d->N && d->last_rows != d->N + 1) ||
+        d->batch < 0)
+        return fail(ctx, CMPC_ERR_ARG, "bad LPV dimensions (last_rows must be N or N+1, nb <= 12)");
+    *c = cmpc::LpvConst{};
+    c->N = d->N;
+    c->nb = d->nb;
+    c->last_rows = d->last_rows;
+    c->nseg = tr->nseg;
+    c->mc = 4 + d->nb;
+    c->lf = prm->lf; c->lr = prm->lr; c->m = prm->m; c->I = prm->I;
+    c->Cf = prm->Cf; c->Cr = prm->Cr; c->mu = prm->mu;
+    c->vx_ref = prm->vx_ref; c->min_dist = prm->min_dist; c->max_vel = prm->max_vel; c->min_vel = prm->min_vel;
+    c->max_rs = prm->max_rs; c->max_ls = prm->max_ls; c->max_ac = prm->max_ac; c->max_dc = prm->max_dc;
+    c->dt = prm->dt; c->wq = prm->wq; c->Q00 = prm->Q[0];
+    for (int i = 0; i < tr->nseg; ++i) {
+        c->s0[i] = tr->s0[i];
+        c->len[i] = tr->len[i];
+        c->curv[i] = tr->curv[i];
+        c->hw[i] = tr->half_width[i];
+    }
+    // TrackLength = PointAndTangent[-1, 3] + PointAndTangent[-1, 4]  (utilities/misc.py:85)
+    c->track_len = tr->s0[tr->nseg - 1] + tr->len[tr->nseg - 1];
+    return CMPC_OK;
+}
+
+int lpv_solver_const(cmpc_ctx* ctx, const cmpc_lpv_params* prm, const cmpc_lpv_dims* d, const cmpc_opts* o,
+                     cmpc::MpcConst* mc) {
+    cmpc_mpc_dims md{9, 2, d->N, 3, 4 + d->nb, d->batch};
+    int slack[CMPC_MAX_MC], sign[CMPC_MAX_MC];
+    const int base_slack[4] = {-1, 0, 1, 1};
+    for (int r = 0; r < md.mc; ++r) {
+        slack[r] = r < 4 ? base_slack[r] : 2;
+        sign[r] = r < 4 ? 1 : -1;
+    }
+    double Qsd[3] = {prm->Qs[0], prm->Qs[1], prm->Qs[2]};
+    // input rows [delta <= max_rs; -delta <= max_ls; a <= max_ac; -a <= max_dc]  (LPV_Planner.py:331-339)
+    double ub[2] = {prm->max_rs, prm->max_ac}, lb[2] = {-prm->max_ls, -prm->max_dc};
+    cmpc_mpc_weights w{prm->Q, prm->R, prm->dR, Qsd, ub, lb, slack, sign};
+    const char* msg = nullptr;
+    int rc = cmpc::mpc_prepare(&md, &w, o, mc, &msg);
+    return rc == CMPC_OK ? rc : fail(ctx, rc, msg);
+}
+
+}  // namespace
+
+extern "C" {
+
+int cmpc_abi_version(void) { return CMPC_ABI_VERSION; }
+
+int cmpc_create(cmpc_ctx** out, int device) {
+    if (!out) return CMPC_ERR_ARG;
+    *out = nullptr;
+    int count = 0;
+    if (hipGetDeviceCount(&count) != hipSuccess || count <= 0) return CMPC_ERR_DEVICE;
+    if (device < 0 || device >= count) return CMPC_ERR_ARG;
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, device) != hipSuccess) return CMPC_ERR_DEVICE;
+    if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0) return CMPC_ERR_DEVICE;
+    auto* c = new cmpc_ctx();
+    c->device = device;
+    if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+        delete c;
+        return CMPC_ERR_DEVICE;
+    }
+    *out = c;
+    return CMPC_OK;
+}
+
+int cmpc_destroy(cmpc_ctx* ctx) {
+    if (!ctx) return CMPC_OK;
+    (void)hipSetDevice(ctx->device);
+    if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+    if (ctx->ws) (void)hipFree(ctx->ws);
+    if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
+    delete ctx;
+    return CMPC_OK;
+}
+
+const char* cmpc_last_error(const cmpc_ctx* ctx) { return ctx ? ctx->err.c_str() : "null context"; }
+
+int cmpc_solve_mpc_batch_dev(cmpc_ctx* ctx, const cmpc_mpc_dims* dims, const cmpc_mpc_weights* w,
+                             const cmpc_mpc_data* in, const cmpc_mpc_out* out, const cmpc_opts* opts,
+                             void* stream) {
+    if (!ctx) return CMPC_ERR_ARG;
+    if (!in || !out || !out->z) return fail(ctx, CMPC_ERR_ARG, "null data / output");
+    cmpc::MpcConst c;
+    const char* msg = nullptr;
+    int rc = cmpc::mpc_prepare(dims, w, opts, &c, &msg);
+    if (rc != CMPC_OK) return fail(ctx, rc, msg);
+    if ((rc = set_device(ctx)) != CMPC_OK) return rc;
+    cmpc::MpcPtrs p{in->A, in->B, in->x0, in->u_prev, in->qlin, in->C, in->h, out->z, out->kkt, out->iters, out->status};
+    HIP_TRY(cmpc::mpc_launch(c, p, dims->batch, (hipStream_t)stream));
+    return CMPC_OK;
+}
+
+int cmpc_solve_mpc_batch(cmpc_ctx* ctx, const cmpc_mpc_dims* d, const cmpc_mpc_weights* w,
+                         const cmpc_mpc_data* in, const cmpc_mpc_out* out, const cmpc_opts* opts) {
+    if (!ctx) return CMPC_ERR_ARG;
+    if (!d || !in || !out || !out->z) return fail(ctx, CMPC_ERR_ARG, "null argument");
+    cmpc::MpcConst c;
+    const char* msg = nullptr;
+    int rc = cmpc::mpc_prepare(d, w, opts, &c, &msg);
+    if (rc != CMPC_OK) return fail(ctx, rc, msg);
+    if ((rc = set_device(ctx)) != CMPC_OK) return rc;
+    const size_t B = d->batch, N = d->N, nx = d->nx, nu = d->nu, mc = d->mc;
+    const size_t sA = B * N * nx * nx, sB = B * N * nx * nu, sx = B * nx, su = B * nu, sp = B * (N + 1) * nx,
+                 sC = B * N * mc * nx, sh = B * N * mc, sz = B * mpc_nz(*d);
+    const size_t bytes = 8 * (sA + sB + sx + su + sp + sC + sh + sz + B) + 8 * B + 16 * 256;
+    char* base = arena(ctx, bytes);
+    if (!base) return fail(ctx, CMPC_ERR_NOMEM, "device arena allocation failed");
+    Carve cv{base};
+    double *dA = cv.take<double>(sA), *dB = cv.take<double>(sB), *dx0 = cv.take<double>(sx),
+           *du = cv.take<double>(su), *dp = cv.take<double>(sp), *dC = cv.take<double>(sC),
+           *dh = cv.take<double>(sh), *dz = cv.take<double>(sz), *dk = cv.take<double>(B);
+    int *di = cv.take<int>(B), *ds = cv.take<int>(B);
+    hipStream_t s = ctx->stream;
+    HIP_TRY(hipMemcpyAsync(dA, in->A, 8 * sA, hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemcpyAsync(dB, in->B, 8 * sB, hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemcpyAsync(dx0, in->x0, 8 * sx, hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemcpyAsync(du, in->u_prev, 8 * su, hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemcpyAsync(dp, in->qlin, 8 * sp, hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemcpyAsync(dC, in->C, 8 * sC, hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemcpyAsync(dh, in->h, 8 * sh, hipMemcpyHostToDevice, s));
+    cmpc::MpcPtrs p{dA, dB, dx0, du, dp, dC, dh, dz, dk, di, ds};
+    HIP_TRY(cmpc::mpc_launch(c, p, d->batch, s));
+    HIP_TRY(hipMemcpyAsync(out->z, dz, 8 * sz, hipMemcpyDeviceToHost, s));
+    if (out->kkt) HIP_TRY(hipMemcpyAsync(out->kkt, dk, 8 * B, hipMemcpyDeviceToHost, s));
+    if (out->iters) HIP_TRY(hipMemcpyAsync(out->iters, di, 4 * B, hipMemcpyDeviceToHost, s));
+    if (out->status) HIP_TRY(hipMemcpyAsync(out->status, ds, 4 * B, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    return CMPC_OK;
+}
+
+// Workspace layout of the LPV path (device): structured problem + error flags.
+static size_t lpv_ws_bytes(const cmpc_lpv_dims* d) {
+    const size_t B = d->batch, N = d->N, mc = 4 + d->nb;
+    return 8 * (B * N * 81 + B * N * 18 + B * (N + 1) * 9 + B * N * mc * 9 + B * N * mc) + 4 * B + 8 * 256;
+}
+
+static int lpv_run(cmpc_ctx* ctx, const cmpc_lpv_params* prm, const cmpc_track* tr, const cmpc_lpv_dims* d,
+                   const cmpc_lpv_data* in, const cmpc_lpv_out* out, const cmpc_opts* opts, hipStream_t s,
+                   Carve& cv) {
+    cmpc::LpvConst lc;
+    int rc = build_lpv_const(ctx, prm, tr, d, &lc);
+    if (rc != CMPC_OK) return rc;
+    cmpc::MpcConst mc;
+    if ((rc = lpv_solver_const(ctx, prm, d, opts, &mc)) != CMPC_OK) return rc;
+    const size_t B = d->batch, N = d->N, m = 4 + d->nb;
+    double *A = cv.take<double>(B * N * 81), *Bm = cv.take<double>(B * N * 18), *p = cv.take<double>(B * (N + 1) * 9),
+           *C = cv.take<double>(B * N * m * 9), *h = cv.take<double>(B * N * m);
+    int* err = cv.take<int>(B);
+    HIP_TRY(hipMemsetAsync(err, 0, 4 * B, s));
+    cmpc::LpvPtrs lp{in->x_last, in->u_last, in->x_agents, in->pose, A, Bm, p, C, h, out->planes, err};
+    HIP_TRY(cmpc::lpv_build_launch(lc, lp, d->batch, s));
+    cmpc::MpcPtrs mp{A, Bm, in->x0, in->u_old, p, C, h, out->z, out->kkt, out->iters, out->status};
+    HIP_TRY(cmpc::mpc_launch(mc, mp, d->batch, s));
+    if (out->status) HIP_TRY(cmpc::lpv_mark_launch(err, out->status, d->batch, s));
+    return CMPC_OK;
+}
+
+int cmpc_solve_lpv_batch_dev(cmpc_ctx* ctx, const cmpc_lpv_params* prm, const cmpc_track* tr, const cmpc_lpv_dims* d,
+                             const cmpc_lpv_data* in, const cmpc_lpv_out* out, const cmpc_opts* opts, void* stream) {
+    if (!ctx) return CMPC_ERR_ARG;
+    if (!d || !in || !out || !out->z || !in->x0 || !in->x_last || !in->u_last || !in->u_old || !in->pose)
+        return fail(ctx, CMPC_ERR_ARG, "null argument");
+    int rc = set_device(ctx);
+    if (rc != CMPC_OK) return rc;
+    char* base = arena(ctx, lpv_ws_bytes(d));
+    if (!base) return fail(ctx, CMPC_ERR_NOMEM, "device arena allocation failed");
+    Carve cv{base};
+    return lpv_run(ctx, prm, tr, d, in, out, opts, (hipStream_t)stream, cv);
+}
+
+int cmpc_solve_lpv_batch(cmpc_ctx* ctx, const cmpc_lpv_params* prm, const cmpc_track* tr, const cmpc_lpv_dims* d,
+                         const cmpc_lpv_data* in, const cmpc_lpv_out* out, const cmpc_opts* opts) {
+    if (!ctx) return CMPC_ERR_ARG;
+    if (!d || !in || !out || !out->z || !in->x0 || !in->x_last || !in->u_last || !in->u_old || !in->pose)
+        return fail(ctx, CMPC_ERR_ARG, "null argument");
+    int rc = set_device(ctx);
+    if (rc != CMPC_OK) return rc;
+    const size_t B = d->batch, N = d->N, nb = d->nb, nz = 12 * (N + 1) + 4 * N;
+    const size_t sx0 = B * 9, sxl = B * d->last_rows * 9, sul = B * N * 2, suo = B * 2,
+                 sxa = in->x_agents ? B * (N + 1) * nb * 2 : 0, spo = B * (N + 1) * 2, sz = B * nz,
+                 spl = out->planes ? B * N * 3 * nb : 0;
+    const size_t bytes = lpv_ws_bytes(d) + 8 * (sx0 + sxl + sul + suo + sxa + spo + sz + spl + B) + 8 * B + 16 * 256;
+    char* base = arena(ctx, bytes);
+    if (!base) return fail(ctx, CMPC_ERR_NOMEM, "device arena allocation failed");
+    Carve cv{base};
+    double *x0 = cv.take<double>(sx0), *xl = cv.take<double>(sxl), *ul = cv.take<double>(sul),
+           *uo = cv.take<double>(suo), *xa = sxa ? cv.take<double>(sxa) : nullptr, *po = cv.take<double>(spo),
+           *z = cv.take<double>(sz), *pl = spl ? cv.take<double>(spl) : nullptr, *kk = cv.take<double>(B);
+    int *it = cv.take<int>(B), *st = cv.take<int>(B);
+    hipStream_t s = ctx->stream;
+    HIP_TRY(hipMemcpyAsync(x0, in->x0, 8 * sx0, hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemcpyAsync(xl, in->x_last, 8 * sxl, hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemcpyAsync(ul, in->u_last, 8 * sul, hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemcpyAsync(uo, in->u_old, 8 * suo, hipMemcpyHostToDevice, s));
+    if (sxa) HIP_TRY(hipMemcpyAsync(xa, in->x_agents, 8 * sxa, hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemcpyAsync(po, in->pose, 8 * spo, hipMemcpyHostToDevice, s));
+    cmpc_lpv_data din{x0, xl, ul, uo, xa, po};
+    cmpc_lpv_out dout{z, pl, kk, it, st};
+    rc = lpv_run(ctx, prm, tr, d, &din, &dout, opts, s, cv);
+    if (rc != CMPC_OK) return rc;
+    HIP_TRY(hipMemcpyAsync(out->z, z, 8 * sz, hipMemcpyDeviceToHost, s));
+    if (out->planes) HIP_TRY(hipMemcpyAsync(out->planes, pl, 8 * spl, hipMemcpyDeviceToHost, s));
+    if (out->kkt) HIP_TRY(hipMemcpyAsync(out->kkt, kk, 8 * B, hipMemcpyDeviceToHost, s));
+    if (out->iters) HIP_TRY(hipMemcpyAsync(out->iters, it, 4 * B, hipMemcpyDeviceToHost, s));
+    if (out->status) HIP_TRY(hipMemcpyAsync(out->status, st, 4 * B, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    return CMPC_OK;
+}
+
+static int di_const(cmpc_ctx* ctx, const cmpc_di_params* prm, const cmpc_di_dims* d, cmpc::DiConst* c) {
+    if (!prm || !d) return fail(ctx, CMPC_ERR_ARG, "null argument");
+    if ((prm->dim != 2 && prm->dim != 3) || d->N < 1 || d->nb < 0 || 4 + d->nb > CMPC_MAX_MC || d->batch < 0 ||
+        d->self_offset < 0)
+        return fail(ctx, CMPC_ERR_ARG, "bad double-integrator dimensions");
+    *c = cmpc::DiConst{d->N, d->nb, 2 * prm->dim, prm->dim, 3, prm->dim, d->self_offset, prm->v_ref, prm->q_v,
+                       prm->q_lane, prm->hw, prm->min_vel, prm->max_vel, prm->min_dist, prm->wq};
+    return set_device(ctx);
+}
+
+int cmpc_di_build_dev(cmpc_ctx* ctx, const cmpc_di_params* prm, const cmpc_di_dims* d, const int* nbr,
+                      const double* lane, const double* traj_all, double* qlin, double* C, double* h, void* stream) {
+    if (!ctx) return CMPC_ERR_ARG;
+    if (!lane || !traj_all || !qlin || !C || !h || (d && d->nb > 0 && !nbr))
+        return fail(ctx, CMPC_ERR_ARG, "null argument");
+    cmpc::DiConst c;
+    int rc = di_const(ctx, prm, d, &c);
+    if (rc != CMPC_OK) return rc;
+    cmpc::DiPtrs p{nbr, lane, traj_all, qlin, C, h};
+    HIP_TRY(cmpc::di_build_launch(c, p, d->batch, (hipStream_t)stream));
+    return CMPC_OK;
+}
+
+int cmpc_di_advance_dev(cmpc_ctx* ctx, const cmpc_di_params* prm, const cmpc_di_dims* d, const double* z,
+                        double* x0, double* u_prev, double* traj_local, void* stream) {
+    if (!ctx) return CMPC_ERR_ARG;
+    if (!z || !x0 || !u_prev || !traj_local) return fail(ctx, CMPC_ERR_ARG, "null argument");
+    cmpc::DiConst c;
+    int rc = di_const(ctx, prm, d, &c);
+    if (rc != CMPC_OK) return rc;
+    HIP_TRY(cmpc::di_advance_launch(c, z, x0, u_prev, traj_local, d->batch, (hipStream_t)stream));
+    return CMPC_OK;
+}
+
+int cmpc_selftest_mfma(cmpc_ctx* ctx, const double* A, const double* B, double* D) {
+    if (!ctx || !A || !B || !D) return CMPC_ERR_ARG;
+    int rc = set_device(ctx);
+    if (rc != CMPC_OK) return rc;
+    char* base = arena(ctx, 8 * (64 + 64 + 256) + 1024);
+    if (!base) return fail(ctx, CMPC_ERR_NOMEM, "arena");
+    Carve cv{base};
+    double *dA = cv.take<double>(64), *dB = cv.take<double>(64), *dD = cv.take<double>(256);
+    hipStream_t s = ctx->stream;
+    HIP_TRY(hipMemcpyAsync(dA, A, 8 * 64, hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemcpyAsync(dB, B, 8 * 64, hipMemcpyHostToDevice, s));
+    HIP_TRY(cmpc::selftest_mfma_launch(dA, dB, dD, s));
+    HIP_TRY(hipMemcpyAsync(D, dD, 8 * 256, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    return CMPC_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,106 @@
+// Internal declarations shared by the HIP translation units of libcmpc.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstddef>
+
+#include "cmpc.h"
+
+namespace cmpc {
+
+constexpr int kWave = 64;
+
+// Batch-shared constants of the structured agent QP.  Passed BY VALUE as a
+// kernel argument (lands in the scalar constant path; no per-call memcpy, so a
+// launch is graph-capturable).
+struct MpcConst {
+    int nx, nu, N, ns, mc;
+    int n;      // condensed variables N*nu
+    int ms;     // state rows N*mc
+    int m;      // all rows ms + 2*nu*N
+    int nxp;    // nx rounded up to the MFMA K granularity (4)
+    int npad;   // n rounded up to 16 (MFMA tile)
+    int ldk;    // leading dimension of the LDS Hessian (odd)
+    int max_iter;
+    double tol;
+    double qs_max;  // max(1, 2*max(Qs)) — slack residual scale
+    double Q[CMPC_MAX_NX * CMPC_MAX_NX];
+    double R[CMPC_MAX_NU * CMPC_MAX_NU];
+    double dR[CMPC_MAX_NU * CMPC_MAX_NU];
+    double Qs[CMPC_MAX_NS];
+    double u_ub[CMPC_MAX_NU];
+    double u_lb[CMPC_MAX_NU];
+    int row_slack[CMPC_MAX_MC];
+    int row_sign[CMPC_MAX_MC];
+};
+
+struct MpcPtrs {
+    const double* A;
+    const double* B;
+    const double* x0;
+    const double* up;
+    const double* p;
+    const double* C;
+    const double* h;
+    double* z;
+    double* kkt;
+    int* iters;
+    int* status;
+};
+
+// Fills the derived fields of MpcConst; returns CMPC_OK or an error code with msg.
+int mpc_prepare(const cmpc_mpc_dims* d, const cmpc_mpc_weights* w, const cmpc_opts* o,
+                MpcConst* c, const char** msg);
+size_t mpc_lds_bytes(const MpcConst& c);
+hipError_t mpc_launch(const MpcConst& c, const MpcPtrs& p, int batch, hipStream_t s);
+
+// LPV reference-semantics builder (scheduling + planes + weights + rows).
+struct LpvConst {
+    int N, nb, last_rows, nseg, mc;
+    double lf, lr, m, I, Cf, Cr, mu;
+    double vx_ref, min_dist, max_vel, min_vel, max_rs, max_ls, max_ac, max_dc;
+    double dt, wq, Q00;
+    double s0[CMPC_MAX_SEG], len[CMPC_MAX_SEG], curv[CMPC_MAX_SEG], hw[CMPC_MAX_SEG];
+    double track_len;
+};
+
+struct LpvPtrs {
+    const double* x_last;
+    const double* u_last;
+    const double* x_agents;
+    const double* pose;
+    double* A;
+    double* B;
+    double* p;
+    double* C;
+    double* h;
+    double* planes;
+    int* err;  // per agent: 0 ok, 1 track lookup failed (reference raises)
+};
+
+hipError_t lpv_build_launch(const LpvConst& c, const LpvPtrs& p, int batch, hipStream_t s);
+// status[b] = CMPC_UNSOLVED where the builder flagged agent b (track lookup failed).
+hipError_t lpv_mark_launch(const int* err, int* status, int batch, hipStream_t s);
+
+// Synthetic double-integrator family (bench workload).
+struct DiConst {
+    int N, nb, nx, nu, ns, dim, self_offset;
+    double v_ref, q_v, q_lane, hw, min_vel, max_vel, min_dist, wq;
+};
+
+struct DiPtrs {
+    const int* nbr;
+    const double* lane;
+    const double* traj_all;
+    double* qlin;
+    double* C;
+    double* h;
+};
+
+hipError_t di_build_launch(const DiConst& c, const DiPtrs& p, int batch, hipStream_t s);
+hipError_t di_advance_launch(const DiConst& c, const double* z, double* x0, double* up, double* traj, int batch,
+                             hipStream_t s);
+
+hipError_t selftest_mfma_launch(const double* A, const double* B, double* D, hipStream_t s);
+
+}  // namespace cmpc

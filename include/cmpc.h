@@ -1,0 +1,231 @@
+/* cmpc.h — C ABI of the MI355X-native collaborative-MPC QP solver (libcmpc.so).
+ *
+ * Drop-in boundary for the reference's per-control-step distributed QP path
+ * (MarcFacerias/ColaborativeMPC-; paths relative to planner/lib/plan_lib/):
+ *
+ *   reference call site                                  replaced by
+ *   ---------------------------------------------------  ---------------------------------
+ *   PlannerLPV.solve (distributedPlanner/                cmpc_solve_lpv_batch[_dev]
+ *     LPV_Planner.py:115-182): _EstimateABC :477-591,     (LPV scheduling + hyperplanes +
+ *     compute_hyperplane planes/compute_plane.py:41-68,   weights + QP build fused on the
+ *     compute_weights utilities/misc.py:10-18, builders   GPU, then the batched condensed
+ *     :251-475, osqp_solve_qp :192-249                     IPM; one call = every agent)
+ *   osqp_solve_qp(P,q,G,h,A,b) (LPV_Planner.py:192-249)   cmpc_solve_mpc_batch[_dev] for the
+ *     on the structured LTV QP                            structured form (any nx, nu, N)
+ *   quadprog(H,f,A,b,Aeq,beq,lb,ub) reached through       cmpc_solve_qp_batch (dense
+ *     YALMIP callquadprog.m:63-69                         standard form, quadprog semantics)
+ *     (Matlab-tests/yalmip/.../solvers/callquadprog.m)
+ *   ROS topic exchange of predicted trajectories          caller-side RCCL all-gather (see
+ *     (ROS/src/planner_experiments/src/LPV_ROS_main.py     INTEGRATION.md); the solver reads
+ *     :66-77,124-150) / LPV_HP_N_main.py:117              neighbour rows from device memory
+ *
+ * Conventions
+ *  - All floating point is IEEE fp64, row-major, batch-major (agent b's block is
+ *    contiguous).  No torch / C++ types cross this boundary.
+ *  - Plain entry points take HOST pointers (the library stages them through
+ *    device memory); *_dev entry points take DEVICE pointers plus a hipStream_t
+ *    passed as void* (0 = default stream) and never synchronise the host.
+ *  - Return value: CMPC_OK (0) or a negative CMPC_ERR_* code (API error);
+ *    cmpc_last_error() gives the message.  Numerical outcome is reported per
+ *    problem in status[] with OSQP's status_val codes so the reference's
+ *    feasibility rule (status in {1, 2, -2}, LPV_Planner.py:246-248) applies
+ *    unchanged.
+ *  - A context is bound to one device and is not re-entrant: one context per
+ *    host thread / stream.  One process per GPU for multi-GPU.
+ *  - There is no CPU fallback: without a usable gfx950 device every solve
+ *    returns CMPC_ERR_DEVICE.
+ */
+#ifndef CMPC_H
+#define CMPC_H
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define CMPC_ABI_VERSION 1
+
+/* API error codes */
+#define CMPC_OK 0
+#define CMPC_ERR_ARG (-1)
+#define CMPC_ERR_DEVICE (-2)
+#define CMPC_ERR_UNSUPPORTED (-3)
+#define CMPC_ERR_NOMEM (-4)
+
+/* Per-problem status (OSQP status_val values, LPV_Planner.py:243-249) */
+#define CMPC_SOLVED 1
+#define CMPC_SOLVED_INACCURATE 2
+#define CMPC_MAX_ITER_REACHED (-2)
+#define CMPC_PRIMAL_INFEASIBLE (-3)
+#define CMPC_UNSOLVED (-10)
+
+/* Size limits of the one-wavefront-per-agent solver (n = N*nu condensed variables). */
+#define CMPC_MAX_NX 12
+#define CMPC_MAX_NU 4
+#define CMPC_MAX_NS 4
+#define CMPC_MAX_MC 16
+#define CMPC_MAX_NCOND 64
+
+typedef struct cmpc_ctx cmpc_ctx;
+
+typedef struct {
+    double tol;    /* relative KKT tolerance; <= 0 selects 1e-11 */
+    int max_iter;  /* interior-point iteration cap; <= 0 selects 60 */
+    int flags;     /* reserved, 0 */
+} cmpc_opts;
+
+int cmpc_abi_version(void);
+/* Create a context on HIP device `device` (ordinal among visible devices). */
+int cmpc_create(cmpc_ctx** ctx, int device);
+int cmpc_destroy(cmpc_ctx* ctx);
+const char* cmpc_last_error(const cmpc_ctx* ctx);
+
+/* ------------------------------------------------------------------------
+ * Structured LTV agent-QP batch (the hot path).  For every agent b:
+ *
+ *   z = [xi_0 .. xi_N | u_0 .. u_{N-1} | du_0 .. du_{N-1}],  xi_k = [x_k (nx) | s_k (ns)]
+ *   min  1/2 z'Pz + q'z  with  P = 2 blkdiag((Q (+) diag(Qs))^(N+1), R^N, dR^N),
+ *                              q = 2 [qlin_0 .. qlin_N (state part), 0, 0]
+ *   s.t. x_0 = x0,  x_{k+1} = A_k x_k + B_k u_k,  du_0 = u_0 - u_prev,  du_k = u_k - u_{k-1}
+ *        C_{k,r} . x_k + sign_r * s_k[slack_r] <= h_{k,r}   (k = 1..N, r < mc; slack_r = -1: none)
+ *        u_lb <= u_k <= u_ub   (rows ordered [u_i <= ub_i; -u_i <= -lb_i] per input, per stage)
+ *
+ * which is exactly the reference-form QP of PlannerLPV (LPV_Planner.py:279-475) for
+ * nx=9, ns=3, nu=2 (cost :382-427, equalities :429-475, rows :251-380).  Rows with an
+ * infinite bound are inactive.  Solved in condensed form (x eliminated; H = G'WG built
+ * on MFMA) by a Mehrotra interior-point method, one wavefront per agent.
+ * ---------------------------------------------------------------------- */
+typedef struct {
+    int nx, nu, N, ns, mc; /* state, input, horizon, slacks per stage, state rows per stage */
+    int batch;             /* number of agents */
+} cmpc_mpc_dims;
+
+typedef struct { /* batch-shared (always HOST pointers; copied into the launch) */
+    const double* Q;      /* nx*nx */
+    const double* R;      /* nu*nu */
+    const double* dR;     /* nu*nu */
+    const double* Qs;     /* ns (diagonal slack weights, > 0) */
+    const double* u_ub;   /* nu (+inf allowed) */
+    const double* u_lb;   /* nu (-inf allowed) */
+    const int* row_slack; /* mc: slack index used by row r, or -1 */
+    const int* row_sign;  /* mc: +1 / -1 coefficient of that slack */
+} cmpc_mpc_weights;
+
+typedef struct { /* per-agent, batch-major */
+    const double* A;      /* batch x N x nx x nx */
+    const double* B;      /* batch x N x nx x nu */
+    const double* x0;     /* batch x nx */
+    const double* u_prev; /* batch x nu */
+    const double* qlin;   /* batch x (N+1) x nx */
+    const double* C;      /* batch x N x mc x nx   (stage k = 1..N) */
+    const double* h;      /* batch x N x mc */
+} cmpc_mpc_data;
+
+typedef struct {
+    double* z;    /* batch x nz,  nz = (nx+ns)(N+1) + 2 nu N  (reference layout) */
+    double* kkt;  /* batch: final scaled KKT residual (may be NULL) */
+    int* iters;   /* batch (may be NULL) */
+    int* status;  /* batch: CMPC_SOLVED ... (may be NULL) */
+} cmpc_mpc_out;
+
+int cmpc_solve_mpc_batch(cmpc_ctx* ctx, const cmpc_mpc_dims* dims, const cmpc_mpc_weights* w,
+                         const cmpc_mpc_data* host_in, const cmpc_mpc_out* host_out,
+                         const cmpc_opts* opts);
+int cmpc_solve_mpc_batch_dev(cmpc_ctx* ctx, const cmpc_mpc_dims* dims, const cmpc_mpc_weights* w,
+                             const cmpc_mpc_data* dev_in, const cmpc_mpc_out* dev_out,
+                             const cmpc_opts* opts, void* hip_stream);
+
+/* ------------------------------------------------------------------------
+ * Reference-semantics LPV batch: one call = PlannerLPV.solve for every agent
+ * (LPV_Planner.py:115-182) with the reference's exact quirks (lagged plane and
+ * weight indexing, u not shifted, ey half-width from the previous prediction's s,
+ * vx < 0.2 branch).  n_s = 9 states [vx vy wz ey epsi theta s X Y], 3 slacks,
+ * 2 inputs [delta a].
+ * ---------------------------------------------------------------------- */
+#define CMPC_MAX_SEG 32
+
+typedef struct {
+    double lf, lr, m, I, Cf, Cr, mu;                   /* model_param (config/base_class.py:20-28) */
+    double vx_ref, min_dist, max_vel, min_vel;         /* sys_lim (config/base_class.py:30-41) */
+    double max_rs, max_ls, max_ac, max_dc;
+    double dt, wq;                                     /* sample time, coverage weight */
+    double Q[81], Qs[3], R[4], dR[4];                  /* gains (scripts/config_files/config_LPV.py:6-11) */
+} cmpc_lpv_params;
+
+typedef struct {     /* one lane of Map.PointAndTangent (track_initialization.py:220-300) */
+    int nseg;        /* rows */
+    const double* s0;         /* nseg: cumulative s at segment start (column 3) */
+    const double* len;        /* nseg: segment length (column 4) */
+    const double* curv;       /* nseg: signed curvature (column 5) */
+    const double* half_width; /* nseg: Map.halfWidth */
+} cmpc_track;
+
+typedef struct {
+    int batch, N, nb;  /* agents, horizon, neighbours per agent (same for all agents) */
+    int last_rows;     /* rows of Last_xPredicted: N+1 at the first step, N afterwards */
+} cmpc_lpv_dims;
+
+typedef struct {   /* per-agent, batch-major */
+    const double* x0;       /* batch x 9 */
+    const double* x_last;   /* batch x last_rows x 9   (Last_xPredicted) */
+    const double* u_last;   /* batch x N x 2           (uPred, not shifted) */
+    const double* u_old;    /* batch x 2               ([OldSteering, OldAccelera]) */
+    const double* x_agents; /* batch x (N+1) x nb x 2  (neighbour X,Y; NULL => planes 0, weights 1) */
+    const double* pose;     /* batch x (N+1) x 2       (own previous X,Y) */
+} cmpc_lpv_data;
+
+typedef struct {
+    double* z;       /* batch x nz (nz = 12(N+1) + 4N) */
+    double* planes;  /* batch x N x 3 x nb (may be NULL) — compute_plane.py layout */
+    double* kkt;     /* may be NULL */
+    int* iters;      /* may be NULL */
+    int* status;     /* may be NULL */
+} cmpc_lpv_out;
+
+int cmpc_solve_lpv_batch(cmpc_ctx* ctx, const cmpc_lpv_params* prm, const cmpc_track* track,
+                         const cmpc_lpv_dims* dims, const cmpc_lpv_data* host_in,
+                         const cmpc_lpv_out* host_out, const cmpc_opts* opts);
+int cmpc_solve_lpv_batch_dev(cmpc_ctx* ctx, const cmpc_lpv_params* prm, const cmpc_track* track,
+                             const cmpc_lpv_dims* dims, const cmpc_lpv_data* dev_in,
+                             const cmpc_lpv_out* dev_out, const cmpc_opts* opts, void* hip_stream);
+
+/* ------------------------------------------------------------------------
+ * Synthetic agent family of BASELINE.json configs 1-5 (no reference counterpart:
+ * the reference's model is the 9-state LPV bicycle; BASELINE fixes a double
+ * integrator).  State [p (dim) | v (dim)], input a (dim), dim = 2 (nx=4, nu=2) or
+ * 3 (nx=6, nu=3); 3 slacks; rows per stage mirror PlannerLPV's
+ * (LPV_Planner.py:279-380) with v_x for vx, p_y - lane for ey and (p_x, p_y) for
+ * (X, Y).  Per consensus round: _build rebuilds C, h, qlin of every local agent
+ * from the previous round's exchanged trajectories (DEVICE pointers); _advance
+ * applies the round update of LPV_HP_N_main.py:106-117 (x0 <- x_1,
+ * u_prev <- u_0, trajectory <- predicted positions) and writes this rank's rows
+ * of the exchange buffer.
+ * ---------------------------------------------------------------------- */
+typedef struct {
+    int dim;                                   /* 2 or 3 */
+    double v_ref, q_v, q_lane, hw, min_vel, max_vel, min_dist, wq;
+} cmpc_di_params;
+
+typedef struct {
+    int batch, N, nb;   /* local agents, horizon, neighbours per agent */
+    int self_offset;    /* global index of local agent 0 in traj_all */
+} cmpc_di_dims;
+
+int cmpc_di_build_dev(cmpc_ctx* ctx, const cmpc_di_params* prm, const cmpc_di_dims* dims,
+                      const int* nbr /* batch x nb, global agent indices */,
+                      const double* lane /* batch */,
+                      const double* traj_all /* n_total x (N+1) x 2 */,
+                      double* qlin /* batch x (N+1) x nx */, double* C /* batch x N x (4+nb) x nx */,
+                      double* h /* batch x N x (4+nb) */, void* hip_stream);
+int cmpc_di_advance_dev(cmpc_ctx* ctx, const cmpc_di_params* prm, const cmpc_di_dims* dims,
+                        const double* z /* batch x nz */, double* x0 /* batch x nx */,
+                        double* u_prev /* batch x nu */, double* traj_local /* batch x (N+1) x 2 */,
+                        void* hip_stream);
+
+/* Device self-test of the f64 MFMA fragment mapping used by the solver
+ * (D = A*B for one 16x16x4 tile, A,B host 16x4 / 4x16 row-major, D host 16x16). */
+int cmpc_selftest_mfma(cmpc_ctx* ctx, const double* A, const double* B, double* D);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* CMPC_H */

@@ -114,7 +114,7 @@ static double max_step(const double* v, const double* dv, const unsigned char* a
 
 typedef struct {
     double *Gam, *K, *X, *dX, *U, *dU, *sig, *dsig, *Dsig, *rsig, *t, *lam, *th, *rho, *rt, *rp, *w,
-        *dt_a, *dl_a, *dtv, *dlv, *GdU, *ybar, *gU, *rd, *rhs, *psi, *tmp, *W;
+        *dt_a, *dl_a, *dtv, *dlv, *GdU, *ybar, *gU, *rd, *rhs, *psi, *tmp, *W, *Yk;
     unsigned char* act;
 } work_t;
 
@@ -288,14 +288,18 @@ static int solve_one(const shared_t* S, const agent_t* a, double tol, int max_it
                 }
             }
             const double* G = Gam + (size_t)(k + 1) * nx * n;
-            for (int c1 = 0; c1 < n; ++c1)
+            const int ncol = (k + 1) * nu; /* Gamma_{k+1} is zero beyond column (k+1)nu */
+            double* Yk = wk->Yk;
+            for (int s = 0; s < nx; ++s)
+                for (int c2 = 0; c2 < ncol; ++c2) {
+                    double v = 0.0;
+                    for (int u = 0; u < nx; ++u) v += W[s * nx + u] * G[u * n + c2];
+                    Yk[s * n + c2] = v;
+                }
+            for (int c1 = 0; c1 < ncol; ++c1)
                 for (int c2 = 0; c2 <= c1; ++c2) {
                     double v = 0.0;
-                    for (int s = 0; s < nx; ++s) {
-                        double ws = 0.0;
-                        for (int u = 0; u < nx; ++u) ws += W[s * nx + u] * G[u * n + c2];
-                        v += G[s * n + c1] * ws;
-                    }
+                    for (int s = 0; s < nx; ++s) v += G[s * n + c1] * Yk[s * n + c2];
                     K[IDX2(c1, c2, n)] += v;
                 }
         }
@@ -437,7 +441,7 @@ int cmpc_oracle_solve(int nx, int nu, int N, int ns, int mc, int batch,
     {
         work_t wk;
         size_t need = (size_t)(N + 1) * nx * n + (size_t)n * n + 4 * (size_t)(N + 1) * nx + 4 * (size_t)n +
-                      4 * (size_t)N * ns + 11 * (size_t)m + 2 * (size_t)nx + (size_t)nx * nx + (size_t)n * 3;
+                      4 * (size_t)N * ns + 12 * (size_t)m + 2 * (size_t)nx + (size_t)nx * nx + (size_t)n * 3 + (size_t)nx * n;
         double* buf = (double*)calloc(need, sizeof(double));
         unsigned char* act = (unsigned char*)calloc(m, 1);
         if (!buf || !act) {
@@ -452,7 +456,7 @@ int cmpc_oracle_solve(int nx, int nu, int N, int ns, int mc, int batch,
             TAKE(sig, N * ns); TAKE(dsig, N * ns); TAKE(Dsig, N * ns); TAKE(rsig, N * ns);
             TAKE(t, m); TAKE(lam, m); TAKE(th, m); TAKE(rho, m); TAKE(rt, m); TAKE(rp, m); TAKE(w, m);
             TAKE(dt_a, m); TAKE(dl_a, m); TAKE(dtv, m); TAKE(dlv, m); TAKE(GdU, m);
-            TAKE(psi, nx); TAKE(tmp, nx);
+            TAKE(psi, nx); TAKE(tmp, nx); TAKE(Yk, (size_t)nx * n);
 #undef TAKE
             wk.act = act;
 #pragma omp for schedule(dynamic, 4)

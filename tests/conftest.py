@@ -1,0 +1,48 @@
+import os
+import sys
+
+import numpy as np
+import pytest
+import scipy.sparse as sp
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PKG = os.path.join(ROOT, "colaborativempc-_amd")
+GOLDEN = os.path.join(ROOT, "tests", "golden")
+for p in (ROOT, PKG):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an MI355X (gfx950) device and the built libcmpc.so")
+
+
+def golden(name):
+    return np.load(os.path.join(GOLDEN, name + ".npz"), allow_pickle=False)
+
+
+def golden_matrix(d, nm, j):
+    shp = tuple(int(v) for v in d[f"{nm}_{j}_shape"])
+    return sp.coo_matrix((d[f"{nm}_{j}_data"], (d[f"{nm}_{j}_row"], d[f"{nm}_{j}_col"])), shape=shp).toarray()
+
+
+LPV_CASES = ["lpv_n10_a2", "lpv_n30_a3", "lpv_n10_lowspeed", "lpv_n10_a1", "lpv_n20_a4"]
+
+
+def lpv_qps(name):
+    """Yield (index, dict) for every captured reference QP of a golden file."""
+    d = golden(name)
+    for j in range(len(d["step"])):
+        yield j, dict(N=int(d["N"]), step=int(d["step"][j]), agent=int(d["agent"][j]), x0=d["x0"][j],
+                      x_last=d[f"x_last_{j}"], u_last=d[f"u_last_{j}"], u_old=d["u_old"][j],
+                      x_agents=d["x_agents"][j], pose=d["pose"][j], z=d["z"][j], y=d["y"][j],
+                      planes=d["planes"][j], P=golden_matrix(d, "P", j), A=golden_matrix(d, "A", j),
+                      q=d["q"][j], l=d["l"][j], u=d["u"][j], dt=float(d["dt"]), vx_ref=float(d["vx_ref"]),
+                      map_name=str(d["map_name"]))
+
+
+@pytest.fixture(scope="session")
+def gpu_ctx():
+    import cmpc
+
+    return cmpc.default_context(0)

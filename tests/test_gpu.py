@@ -1,0 +1,224 @@
+"""GPU parity tests: libcmpc's HIP path (through the C ABI) against the oracle.
+
+Bars: solutions within 1e-6 (max abs, fp64) of the KKT-certified
+reference optimum / the C restatement; builder outputs to fp64 rounding.
+"""
+import numpy as np
+import pytest
+
+from conftest import LPV_CASES, golden, lpv_qps
+
+pytestmark = pytest.mark.gpu
+
+Z_TOL = 1e-6
+
+
+def _gains():
+    from oracle import lpv_ref as L
+
+    return L.paper_gains(), L.SCALED_CAR_MODEL
+
+
+def test_mfma_fragment_map(gpu_ctx):
+    import cmpc
+
+    for seed in range(3):
+        D, ref = cmpc.selftest_mfma(gpu_ctx, seed)
+        assert np.array_equal(D, ref)
+
+
+@pytest.mark.parametrize("name", LPV_CASES)
+def test_lpv_batch_matches_reference_optimum(gpu_ctx, name):
+    import cmpc
+    from oracle import lpv_ref as L
+
+    g, model = _gains()
+    tr = L.Track.build("Highway")
+    groups = {}
+    for j, c in lpv_qps(name):
+        groups.setdefault(c["x_last"].shape[0], []).append(c)
+    N = None
+    for rows, cs in groups.items():
+        N = cs[0]["N"]
+        lim = L.scaled_car_limits(cs[0]["vx_ref"])
+        bp = cmpc.PlannerLPVBatch(g["Q"], g["Qs"], g["R"], g["dR"], N, cs[0]["dt"], tr, g["wq"], model, lim,
+                                  ctx=gpu_ctx)
+        xa = np.stack([c["x_agents"] for c in cs])
+        res = bp.solve(np.stack([c["x0"] for c in cs]), np.stack([c["x_last"] for c in cs]),
+                       np.stack([c["u_last"] for c in cs]), np.stack([c["u_old"] for c in cs]),
+                       xa if xa.shape[2] else None, np.stack([c["pose"] for c in cs]))
+        assert (res["status"] == cmpc.CMPC_SOLVED).all(), res["status"]
+        zref = np.stack([c["z"] for c in cs])
+        assert np.abs(res["z"] - zref).max() < Z_TOL
+        if xa.shape[2]:
+            np.testing.assert_allclose(res["planes"], np.stack([c["planes"] for c in cs]), rtol=0, atol=1e-14)
+
+
+def test_planner_lpv_dropin_closed_loop(gpu_ctx):
+    """The reference-interface PlannerLPV driven by the reference loop semantics
+    (LPV_HP_N_main.py:96-117) reproduces the captured trajectory."""
+    import cmpc
+    from oracle import lpv_ref as L
+
+    d = golden("lpv_n10_a2")
+    N, n, steps = int(d["N"]), int(d["n_agents"]), int(d["steps"])
+    g, model = _gains()
+    tr = L.Track.build("Highway")
+    lim = L.scaled_car_limits(float(d["vx_ref"]))
+    agents, x_old, u_old = L.initialise_agents(L.X0_DATABASE[:n], N, 0.025, tr)
+    ns = L.neighbour_lists(n)
+    rs = [cmpc.PlannerLPV(g["Q"], g["Qs"], g["R"], g["dR"], N, 0.025, tr, i, g["wq"], model, lim, ctx=gpu_ctx)
+          for i in range(n)]
+    x0 = [x_old[i][0].copy() for i in range(n)]
+    j = 0
+    for step in range(steps):
+        xp, up = [None] * n, [None] * n
+        for i, r in enumerate(rs):
+            feas, sol, planes = r.solve(x0[i], x_old[i], u_old[i], agents[:, ns[i], :], ns[i], agents[:, i, :])
+            assert feas == 1
+            assert np.abs(sol - d["z"][j]).max() < Z_TOL
+            assert np.abs(r.xPred - d["xPred"][j]).max() < Z_TOL
+            assert np.abs(r.uPred - d["uPred"][j]).max() < Z_TOL
+            xp[i], up[i] = r.xPred, r.uPred
+            x0[i] = xp[i][1].copy()
+            j += 1
+        u_old = up
+        x_old = [xp[i][1:] for i in range(n)]
+        agents = np.swapaxes(np.asarray(xp)[:, :, -2:], 0, 1)
+
+
+@pytest.mark.parametrize("n,N,nb,dim", [(2, 10, 1, 2), (64, 20, 2, 2), (1024, 30, 2, 2), (16, 10, 2, 3)])
+def test_synthetic_batch_vs_c_oracle(gpu_ctx, n, N, nb, dim):
+    import cmpc
+    from cmpc import scenarios as S
+    from oracle import cmpc_oracle as CO
+    from oracle import synth
+
+    sc = S.make_di(n, N, nb, dim)
+    P = synth.structured(sc.shared, sc.params, sc.A, sc.B, sc.x0, sc.u_prev, sc.lane, sc.nbr, sc.traj,
+                         np.arange(n))
+    z, kkt, it, st = cmpc.solve_mpc(P, gpu_ctx)
+    zc, kc, ic, sc_ = CO.solve_batch(P)
+    assert (st == cmpc.CMPC_SOLVED).all()
+    assert (sc_ == 1).all()
+    assert np.abs(z - zc).max() < Z_TOL
+    assert kkt.max() < 1e-10
+
+
+def test_synthetic_small_vs_reference_form(gpu_ctx):
+    import cmpc
+    from cmpc import scenarios as S
+    from oracle import qp_ipm, synth
+
+    sc = S.make_di(3, 10, 2, 2)
+    P = synth.structured(sc.shared, sc.params, sc.A, sc.B, sc.x0, sc.u_prev, sc.lane, sc.nbr, sc.traj, np.arange(3))
+    z, kkt, it, st = cmpc.solve_mpc(P, gpu_ctx)
+    for a in range(3):
+        r = qp_ipm.solve_qp(*synth.reference_form(P, a))
+        assert np.abs(z[a] - r.x).max() < Z_TOL
+
+
+def test_gpu_builder_matches_oracle_and_rounds(gpu_ctx):
+    """cmpc_di_build_dev == oracle builder; three device-resident rounds == the
+    same rounds replayed on the host with the C oracle."""
+    import torch
+    from cmpc import scenarios as S
+    from cmpc.rounds import DIRounds
+    from oracle import cmpc_oracle as CO
+    from oracle import synth
+
+    sc = S.make_di(96, 20, 2, 2)
+    R = DIRounds(sc, ctx=gpu_ctx)
+    traj = sc.traj.copy()
+    x0, up = sc.x0.copy(), sc.u_prev.copy()
+    for rnd in range(3):
+        R.build()
+        snap = R.snapshot()
+        ref = synth.structured(sc.shared, sc.params, sc.A, sc.B, x0, up, sc.lane, sc.nbr, traj, np.arange(96))
+        for k in ("qlin", "C", "h"):
+            np.testing.assert_allclose(snap[k], ref[k], rtol=0, atol=1e-14)
+        R.solve()
+        torch.cuda.synchronize()
+        zc, kc, ic, stc = CO.solve_batch(ref)
+        zg = R.z.cpu().numpy()
+        assert np.abs(zg - zc).max() < Z_TOL
+        R.advance()
+        R.exchange()
+        torch.cuda.synchronize()
+        nx, ne = 4, 7
+        traj = np.stack([zc[:, [k * ne for k in range(21)]], zc[:, [k * ne + 1 for k in range(21)]]], -1)
+        x0 = zc[:, ne:ne + nx].copy()
+        up = zc[:, ne * 21:ne * 21 + 2].copy()
+        assert np.abs(R.traj_all.cpu().numpy() - traj).max() < Z_TOL
+
+
+def test_deterministic_and_permutation_invariant(gpu_ctx):
+    import cmpc
+    from cmpc import scenarios as S
+    from oracle import synth
+
+    sc = S.make_di(128, 30, 2, 2)
+    P = synth.structured(sc.shared, sc.params, sc.A, sc.B, sc.x0, sc.u_prev, sc.lane, sc.nbr, sc.traj,
+                         np.arange(128))
+    z1 = cmpc.solve_mpc(P, gpu_ctx)[0]
+    z2 = cmpc.solve_mpc(P, gpu_ctx)[0]
+    assert np.array_equal(z1, z2)
+    perm = np.random.default_rng(3).permutation(128)
+    Pp = dict(P)
+    for k in ("A", "B", "x0", "u_prev", "qlin", "C", "h"):
+        Pp[k] = P[k][perm]
+    zp = cmpc.solve_mpc(Pp, gpu_ctx)[0]
+    assert np.array_equal(zp, z1[perm])
+
+
+def test_edge_cases(gpu_ctx):
+    import cmpc
+    from cmpc import scenarios as S
+    from oracle import cmpc_oracle as CO
+    from oracle import synth
+
+    sc = S.make_di(8, 10, 2, 2)
+    P = synth.structured(sc.shared, sc.params, sc.A, sc.B, sc.x0, sc.u_prev, sc.lane, sc.nbr, sc.traj, np.arange(8))
+    # empty batch is a no-op
+    E = dict(P)
+    for k in ("A", "B", "x0", "u_prev", "qlin", "C", "h"):
+        E[k] = P[k][:0]
+    z, kkt, it, st = cmpc.solve_mpc(E, gpu_ctx)
+    assert z.shape == (0, cmpc.nz_of(P))
+    # infinite bounds -> inactive rows (inputs unbounded, speed cap removed)
+    F = dict(P)
+    F["u_ub"] = np.full(2, np.inf)
+    F["u_lb"] = np.full(2, -np.inf)
+    F["h"] = P["h"].copy()
+    F["h"][:, :, 1] = np.inf
+    z, kkt, it, st = cmpc.solve_mpc(F, gpu_ctx)
+    zc, _, _, stc = CO.solve_batch(F)
+    assert (st == 1).all() and np.abs(z - zc).max() < Z_TOL
+    # no neighbour rows
+    G = synth.structured(S.di_shared(2, 10, 0), sc.params, sc.A, sc.B, sc.x0, sc.u_prev, sc.lane,
+                         np.zeros((8, 0), np.int32), sc.traj, np.arange(8))
+    z, kkt, it, st = cmpc.solve_mpc(G, gpu_ctx)
+    zc, _, _, _ = CO.solve_batch(G)
+    assert (st == 1).all() and np.abs(z - zc).max() < Z_TOL
+    # a hard-infeasible agent (min speed above the reachable range) and a NaN agent:
+    # both report a non-solved status, the other agents are unaffected
+    H = dict(P)
+    H["h"] = P["h"].copy()
+    H["h"][0, :, 0] = -50.0
+    H["x0"] = P["x0"].copy()
+    H["x0"][1, 0] = np.nan
+    z, kkt, it, st = cmpc.solve_mpc(H, gpu_ctx, max_iter=40)
+    assert st[0] != cmpc.CMPC_SOLVED and st[1] != cmpc.CMPC_SOLVED
+    zc, _, _, _ = CO.solve_batch(P)
+    assert (st[2:] == 1).all() and np.abs(z[2:] - zc[2:]).max() < Z_TOL
+
+
+def test_unsupported_sizes_are_rejected(gpu_ctx):
+    import cmpc
+    from cmpc import scenarios as S
+    from oracle import synth
+
+    sc = S.make_di(2, 40, 1, 2)   # N*nu = 80 > 64
+    P = synth.structured(sc.shared, sc.params, sc.A, sc.B, sc.x0, sc.u_prev, sc.lane, sc.nbr, sc.traj, np.arange(2))
+    with pytest.raises(cmpc.CmpcError):
+        cmpc.solve_mpc(P, gpu_ctx)
