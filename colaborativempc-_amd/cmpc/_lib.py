@@ -129,6 +129,14 @@ def load():
         if not os.path.exists(LIB_PATH):
             raise FileNotFoundError(f"{LIB_PATH} not built: run __graft_entry__.build() "
                                     f"or make -C colaborativempc-_amd/csrc")
+        # One HIP runtime per process: PyTorch-ROCm ships its own libamdhip64 (SONAME
+        # libamdhip64.so.7) and loads it by the unversioned name.  Loading torch first
+        # makes libcmpc's NEEDED libamdhip64.so.7 bind to that same runtime; loading
+        # libcmpc first would give the process two runtimes and torch would see no GPU.
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
         lib = ct.CDLL(LIB_PATH)
         for name, (res, args) in SIGNATURES.items():
             fn = getattr(lib, name)

@@ -79,9 +79,12 @@ __device__ __forceinline__ double readlane_d(double v, int lane) {
     return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
 }
 
+// NaN-propagating max: a NaN residual must never look converged (fmax drops NaNs).
+__device__ __forceinline__ double nmax(double a, double b) { return (a > b || a != a) ? a : b; }
+
 __device__ __forceinline__ double wave_max(double v) {
 #pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o));
+    for (int o = 32; o > 0; o >>= 1) v = nmax(v, __shfl_xor(v, o));
     return v;
 }
 __device__ __forceinline__ double wave_min(double v) {
@@ -298,7 +301,7 @@ __global__ __launch_bounds__(kWave) void mpc_ipm_kernel(const MpcConst c, const 
         double gs_l = 1.0;
         for (int i = l; i < n; i += kWave) {
             gU[i] += rdr_grad(c, U, up, i);
-            gs_l = fmax(gs_l, fabs(gU[i]));
+            gs_l = nmax(gs_l, fabs(gU[i]));
         }
         const double gscale = wave_max(gs_l);
         for (int i = l; i < N * nx; i += kWave) {  // + C' lambda on stages 1..N
@@ -313,7 +316,7 @@ __global__ __launch_bounds__(kWave) void mpc_ipm_kernel(const MpcConst c, const 
         for (int i = l; i < n; i += kWave) {
             const int r = ms + 2 * i;
             rd[i] += rdr_grad(c, U, up, i) + lam[r] - lam[r + 1];
-            nrd_l = fmax(nrd_l, fabs(rd[i]));
+            nrd_l = nmax(nrd_l, fabs(rd[i]));
         }
         for (int i = l; i < N * ns; i += kWave) {
             const int k = i / ns, j = i - k * ns;
@@ -321,21 +324,21 @@ __global__ __launch_bounds__(kWave) void mpc_ipm_kernel(const MpcConst c, const 
             for (int r = 0; r < mc; ++r)
                 if (c.row_slack[r] == j) v += c.row_sign[r] * lam[k * mc + r];
             rsig[i] = v;
-            nrs_l = fmax(nrs_l, fabs(v));
+            nrs_l = nmax(nrs_l, fabs(v));
         }
         for (int r = l; r < m; r += kWave) {
             if (isfinite(w[r])) {
                 const double v = row_value(c, C, r, X, U, sig) + t[r] - w[r];
                 rp[r] = v;
-                nrp_l = fmax(nrp_l, fabs(v));
+                nrp_l = nmax(nrp_l, fabs(v));
                 mu_l += t[r] * lam[r];
             } else {
                 rp[r] = 0.0;
             }
         }
         const double mu = wave_sum(mu_l) / mact;
-        kkt = fmax(fmax(wave_max(nrd_l) / gscale, wave_max(nrs_l) / c.qs_max),
-                   fmax(wave_max(nrp_l) / scale_p, mu));
+        kkt = nmax(nmax(wave_max(nrd_l) / gscale, wave_max(nrs_l) / c.qs_max),
+                   nmax(wave_max(nrp_l) / scale_p, mu));
         if (kkt < c.tol) {
             status = CMPC_SOLVED;
             break;

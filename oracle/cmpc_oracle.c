@@ -73,6 +73,9 @@ static void adjoint(const shared_t* S, const agent_t* a, const double* ybar, dou
     }
 }
 
+/* NaN-propagating max (fmax would drop a NaN residual and report convergence) */
+static double nmax(double a, double b) { return (a > b || a != a) ? a : b; }
+
 static int chol(double* K, int n) {
     for (int j = 0; j < n; ++j) {
         double d = K[IDX2(j, j, n)];
@@ -213,7 +216,7 @@ static int solve_one(const shared_t* S, const agent_t* a, double tol, int max_it
                 }
                 wk->gU[k * nu + i] += v;
             }
-        for (int c = 0; c < n; ++c) if (fabs(wk->gU[c]) > gscale) gscale = fabs(wk->gU[c]);
+        for (int c = 0; c < n; ++c) gscale = nmax(gscale, fabs(wk->gU[c]));
         for (int k = 0; k < N; ++k)
             for (int r = 0; r < mc; ++r) {
                 const double* c_ = a->C + ((size_t)k * mc + r) * nx;
@@ -243,13 +246,13 @@ static int solve_one(const shared_t* S, const agent_t* a, double tol, int max_it
             if (!wk->act[r]) { wk->rp[r] = 0.0; continue; }
             double g; ROWVAL(X, U, sig, r, g);
             wk->rp[r] = g + t[r] - wk->w[r];
-            if (fabs(wk->rp[r]) > nrp) nrp = fabs(wk->rp[r]);
+            nrp = nmax(nrp, fabs(wk->rp[r]));
             mu += t[r] * lam[r];
         }
         mu = mact ? mu / mact : 0.0;
-        for (int c = 0; c < n; ++c) if (fabs(wk->rd[c]) > nrd) nrd = fabs(wk->rd[c]);
-        for (int q = 0; q < N * ns; ++q) if (fabs(wk->rsig[q]) > nrs) nrs = fabs(wk->rsig[q]);
-        kkt = fmax(fmax(nrd / gscale, nrs / qs_max), fmax(nrp / scale_p, mu));
+        for (int c = 0; c < n; ++c) nrd = nmax(nrd, fabs(wk->rd[c]));
+        for (int q = 0; q < N * ns; ++q) nrs = nmax(nrs, fabs(wk->rsig[q]));
+        kkt = nmax(nmax(nrd / gscale, nrs / qs_max), nmax(nrp / scale_p, mu));
         if (kkt < tol) { status = 1; break; }
         if (!isfinite(kkt)) { status = -3; break; }
 
