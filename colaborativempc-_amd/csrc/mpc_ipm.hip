@@ -337,9 +337,11 @@ __global__ __launch_bounds__(kWave) void mpc_ipm_kernel(const MpcConst c, const 
             }
         }
         const double mu = wave_sum(mu_l) / mact;
-        kkt = nmax(nmax(wave_max(nrd_l) / gscale, wave_max(nrs_l) / c.qs_max),
-                   nmax(wave_max(nrp_l) / scale_p, mu));
-        if (kkt < c.tol) {
+        // stationarity / feasibility relative; complementarity absolute and 1e4 tighter
+        // (degenerate rows sit at t, lambda ~ sqrt(mu): primal accuracy needs tiny mu)
+        const double res = nmax(nmax(wave_max(nrd_l) / gscale, wave_max(nrs_l) / c.qs_max), wave_max(nrp_l) / scale_p);
+        kkt = nmax(res, mu);
+        if (res < c.tol && mu < 1e-4 * c.tol) {
             status = CMPC_SOLVED;
             break;
         }
@@ -459,8 +461,8 @@ __global__ __launch_bounds__(kWave) void mpc_ipm_kernel(const MpcConst c, const 
             else if (l > j && l < n) K[l * ldk + j] = v / d;
             bar();
         }
-        if (!chol_ok) {
-            status = CMPC_UNSOLVED;
+        if (!chol_ok) {  // factorisation broke down: keep the current iterate
+            status = (kkt < 1e3 * c.tol) ? CMPC_SOLVED_INACCURATE : CMPC_UNSOLVED;
             break;
         }
 
@@ -582,7 +584,10 @@ __global__ __launch_bounds__(kWave) void mpc_ipm_kernel(const MpcConst c, const 
             }
         bar();
     }
-    if (it > c.max_iter) it = c.max_iter;
+    if (it > c.max_iter) {
+        it = c.max_iter;
+        if (kkt < 1e3 * c.tol) status = CMPC_SOLVED_INACCURATE;
+    }
     bar();
 
     // ---- output in the reference layout ----
@@ -633,7 +638,7 @@ int mpc_prepare(const cmpc_mpc_dims* d, const cmpc_mpc_weights* wt, const cmpc_o
     c->nxp = (d->nx + 3) & ~3;
     c->npad = (c->n + 15) & ~15;
     c->ldk = (c->n & 1) ? c->n : c->n + 1;
-    c->tol = (o && o->tol > 0) ? o->tol : 1e-11;
+    c->tol = (o && o->tol > 0) ? o->tol : 1e-9;
     c->max_iter = (o && o->max_iter > 0) ? o->max_iter : 60;
     double qs = 1.0;
     for (int i = 0; i < d->nx * d->nx; ++i) c->Q[i] = wt->Q[i];

@@ -68,7 +68,7 @@ extern "C" {
 typedef struct cmpc_ctx cmpc_ctx;
 
 typedef struct {
-    double tol;    /* relative KKT tolerance; <= 0 selects 1e-11 */
+    double tol;    /* relative stationarity/feasibility tolerance (complementarity: 1e-4*tol); <= 0 selects 1e-9 */
     int max_iter;  /* interior-point iteration cap; <= 0 selects 60 */
     int flags;     /* reserved, 0 */
 } cmpc_opts;

@@ -121,7 +121,7 @@ typedef struct {
     unsigned char* act;
 } work_t;
 
-/* Solve one agent.  Returns status: 1 solved, -2 max_iter, -3 numerical failure. */
+/* Solve one agent.  Returns OSQP-style status: 1 solved, 2 solved inaccurate, -2 max_iter, -10 unsolved. */
 static int solve_one(const shared_t* S, const agent_t* a, double tol, int max_iter, work_t* wk,
                      double* z, double* kkt_out, int* iters_out) {
     const int nx = S->nx, nu = S->nu, N = S->N, ns = S->ns, mc = S->mc;
@@ -252,9 +252,12 @@ static int solve_one(const shared_t* S, const agent_t* a, double tol, int max_it
         mu = mact ? mu / mact : 0.0;
         for (int c = 0; c < n; ++c) nrd = nmax(nrd, fabs(wk->rd[c]));
         for (int q = 0; q < N * ns; ++q) nrs = nmax(nrs, fabs(wk->rsig[q]));
-        kkt = nmax(nmax(nrd / gscale, nrs / qs_max), nmax(nrp / scale_p, mu));
-        if (kkt < tol) { status = 1; break; }
-        if (!isfinite(kkt)) { status = -3; break; }
+        /* stationarity / feasibility relative; complementarity absolute and 1e4 tighter
+           (degenerate rows sit at t, lambda ~ sqrt(mu): primal accuracy needs tiny mu) */
+        double res = nmax(nmax(nrd / gscale, nrs / qs_max), nrp / scale_p);
+        kkt = nmax(res, mu);
+        if (res < tol && mu < 1e-4 * tol) { status = 1; break; }
+        if (!isfinite(kkt)) { status = -10; break; }
 
         /* ---- Newton matrix ---- */
         for (int r = 0; r < m; ++r) wk->th[r] = wk->act[r] ? lam[r] / t[r] : 0.0;
@@ -319,7 +322,7 @@ static int solve_one(const shared_t* S, const agent_t* a, double tol, int max_it
                 int r = ms + (k * nu + i) * 2;
                 K[IDX2(k * nu + i, k * nu + i, n)] += wk->th[r] + wk->th[r + 1];
             }
-        if (chol(K, n)) { status = -3; break; }
+        if (chol(K, n)) { status = (kkt < 1e3 * tol) ? 2 : -10; break; }
 
         /* ---- predictor / corrector ---- */
         double sig_c = 0.0, mu_aff = 0.0;
@@ -404,7 +407,10 @@ static int solve_one(const shared_t* S, const agent_t* a, double tol, int max_it
             }
         }
     }
-    if (it > max_iter) it = max_iter;
+    if (it > max_iter) {
+        it = max_iter;
+        if (kkt < 1e3 * tol) status = 2;
+    }
     /* exact re-simulation for the output trajectory */
     fwd_sim(S, a, a->x0, U, X);
     const int nxe = nx + ns;

@@ -47,7 +47,7 @@ def nz_of(p):
     return (p["nx"] + p["ns"]) * (p["N"] + 1) + 2 * p["nu"] * p["N"]
 
 
-def solve_batch(p, tol=1e-11, max_iter=60, nthreads=0):
+def solve_batch(p, tol=1e-9, max_iter=60, nthreads=0):
     nb = p["A"].shape[0]
     keep = []
     args = []
