@@ -36,8 +36,11 @@ _DP = ct.POINTER(ct.c_double)
 _IP = ct.POINTER(ct.c_int)
 
 
+CMPC_FLAG_GENERIC = 1
+
+
 class cmpc_opts(ct.Structure):
-    _fields_ = [("tol", ct.c_double), ("max_iter", ct.c_int), ("flags", ct.c_int)]
+    _fields_ = [("tol", ct.c_double), ("max_iter", ct.c_int), ("flags", ct.c_int), ("stamps", ct.c_void_p)]
 
 
 class cmpc_mpc_dims(ct.Structure):
@@ -162,8 +165,8 @@ def i32(a):
     return np.ascontiguousarray(a, dtype=np.int32)
 
 
-def opts(tol=None, max_iter=None):
-    return cmpc_opts(float(tol or 0.0), int(max_iter or 0), 0)
+def opts(tol=None, max_iter=None, flags=0, stamps=None):
+    return cmpc_opts(float(tol or 0.0), int(max_iter or 0), int(flags), stamps)
 
 
 class Context:

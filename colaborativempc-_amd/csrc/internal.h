@@ -22,6 +22,7 @@ struct MpcConst {
     int npad;   // n rounded up to 16 (MFMA tile)
     int ldk;    // leading dimension of the LDS Hessian (odd)
     int max_iter;
+    int debug;  // CMPC_FLAG_DEBUG: dump the first Newton matrix into opts->stamps
     double tol;
     double qs_max;  // max(1, 2*max(Qs)) — slack residual scale
     double Q[CMPC_MAX_NX * CMPC_MAX_NX];
@@ -46,13 +47,16 @@ struct MpcPtrs {
     double* kkt;
     int* iters;
     int* status;
+    unsigned long long* stamps;  // optional: batch x 8 per-phase s_memtime counts (v2 kernel)
 };
 
 // Fills the derived fields of MpcConst; returns CMPC_OK or an error code with msg.
 int mpc_prepare(const cmpc_mpc_dims* d, const cmpc_mpc_weights* w, const cmpc_opts* o,
                 MpcConst* c, const char** msg);
 size_t mpc_lds_bytes(const MpcConst& c);
-hipError_t mpc_launch(const MpcConst& c, const MpcPtrs& p, int batch, hipStream_t s);
+hipError_t mpc_launch(const MpcConst& c, const MpcPtrs& p, int batch, hipStream_t s, bool force_generic = false);
+// Specialised (NX, NU, MC) kernels of mpc_ipm2.hip; false when no instantiation covers the problem.
+bool mpc2_try_launch(const MpcConst& c, const MpcPtrs& p, int batch, hipStream_t s, hipError_t* err);
 
 // LPV reference-semantics builder (scheduling + planes + weights + rows).
 struct LpvConst {

@@ -441,6 +441,13 @@ __global__ __launch_bounds__(kWave) void mpc_ipm_kernel(const MpcConst c, const 
         }
         bar();
 
+        if (c.debug && it == 1 && P.stamps) {  // diagnostic: dump K (lower, npad x npad) to the stamps buffer
+            double* dk = reinterpret_cast<double*>(P.stamps) + (size_t)b * npad * npad;
+            for (int i = l; i < n * n; i += kWave) {
+                const int r = i / n, cc = i - r * n;
+                dk[r * npad + cc] = (cc <= r) ? K[r * ldk + cc] : 0.0;
+            }
+        }
         // ================= Cholesky K = L L' (lane i owns row i) =================
         bool chol_ok = true;
         for (int j = 0; j < n; ++j) {
@@ -640,6 +647,7 @@ int mpc_prepare(const cmpc_mpc_dims* d, const cmpc_mpc_weights* wt, const cmpc_o
     c->ldk = (c->n & 1) ? c->n : c->n + 1;
     c->tol = (o && o->tol > 0) ? o->tol : 1e-9;
     c->max_iter = (o && o->max_iter > 0) ? o->max_iter : 60;
+    c->debug = (o && (o->flags & 2)) ? 1 : 0;
     double qs = 1.0;
     for (int i = 0; i < d->nx * d->nx; ++i) c->Q[i] = wt->Q[i];
     for (int i = 0; i < d->nu * d->nu; ++i) {
@@ -680,8 +688,10 @@ static hipError_t launch_t(const MpcConst& c, const MpcPtrs& p, int batch, hipSt
     return hipGetLastError();
 }
 
-hipError_t mpc_launch(const MpcConst& c, const MpcPtrs& p, int batch, hipStream_t s) {
+hipError_t mpc_launch(const MpcConst& c, const MpcPtrs& p, int batch, hipStream_t s, bool force_generic) {
     if (batch == 0) return hipSuccess;
+    hipError_t e2;
+    if (!force_generic && mpc2_try_launch(c, p, batch, s, &e2)) return e2;
     switch (c.npad / 16) {
         case 1: return launch_t<1>(c, p, batch, s);
         case 2: return launch_t<2>(c, p, batch, s);

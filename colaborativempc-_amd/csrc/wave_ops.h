@@ -1,0 +1,52 @@
+// Wave-level helpers shared by the solver kernels (one 64-lane wavefront = one agent).
+#pragma once
+#include <hip/hip_runtime.h>
+
+namespace cmpc {
+
+typedef double v4d __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ void bar() { __syncthreads(); }
+
+// Broadcast lane `lane` (must be wave-uniform) of a double to every lane (two v_readlane_b32).
+__device__ __forceinline__ double readlane_d(double v, int lane) {
+    long long i = __double_as_longlong(v);
+    int lo = __builtin_amdgcn_readlane((int)(i & 0xffffffffll), lane);
+    int hi = __builtin_amdgcn_readlane((int)(i >> 32), lane);
+    return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+
+// NaN-propagating max: a NaN residual must never look converged (fmax drops NaNs).
+__device__ __forceinline__ double nmax(double a, double b) { return (a > b || a != a) ? a : b; }
+
+__device__ __forceinline__ double wave_max(double v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = nmax(v, __shfl_xor(v, o));
+    return v;
+}
+__device__ __forceinline__ double wave_min(double v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = fmin(v, __shfl_xor(v, o));
+    return v;
+}
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    return v;
+}
+// sum over the 16 lanes that share (lane >> 4)
+__device__ __forceinline__ double sum16(double v) {
+#pragma unroll
+    for (int o = 8; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    return v;
+}
+// sum over the 4 lanes that share (lane & 15)
+__device__ __forceinline__ double sum_groups(double v) {
+    v += __shfl_xor(v, 16);
+    v += __shfl_xor(v, 32);
+    return v;
+}
+
+__device__ __forceinline__ unsigned long long clock64_() { return __builtin_amdgcn_s_memtime(); }
+
+}  // namespace cmpc

@@ -67,10 +67,14 @@ extern "C" {
 
 typedef struct cmpc_ctx cmpc_ctx;
 
+#define CMPC_FLAG_GENERIC 1  /* force the generic (runtime-dimension) kernel */
+
 typedef struct {
     double tol;    /* relative stationarity/feasibility tolerance (complementarity: 1e-4*tol); <= 0 selects 1e-9 */
     int max_iter;  /* interior-point iteration cap; <= 0 selects 60 */
-    int flags;     /* reserved, 0 */
+    int flags;     /* CMPC_FLAG_* */
+    void* stamps;  /* optional DEVICE buffer, batch x 8 uint64: per-phase shader-clock counts of the
+                      specialised kernel (diagnostic; NULL in production) */
 } cmpc_opts;
 
 int cmpc_abi_version(void);

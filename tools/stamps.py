@@ -1,0 +1,47 @@
+"""Diagnostic: per-phase shader-clock breakdown of the specialised solver kernel
+(cfg3 round 0 problem).  Usage: python tools/stamps.py [agents] [N]"""
+import ctypes as ct
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "colaborativempc-_amd"))
+sys.path.insert(0, ROOT)
+import torch  # noqa: E402
+
+import cmpc  # noqa: E402
+from cmpc import _lib as L  # noqa: E402
+from cmpc import scenarios as S  # noqa: E402
+from cmpc.rounds import DIRounds  # noqa: E402
+
+n = int(sys.argv[1]) if len(sys.argv) > 1 else 1024
+N = int(sys.argv[2]) if len(sys.argv) > 2 else 30
+sc = S.make_di(n, N, 2, 2)
+R = DIRounds(sc)
+R.build()
+st = torch.zeros((n, 8), dtype=torch.int64, device="cuda")
+R.opts = L.opts(stamps=st.data_ptr())
+for _ in range(3):
+    R.solve()
+torch.cuda.synchronize()
+ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+ev[0].record()
+R.solve()
+ev[1].record()
+torch.cuda.synchronize()
+a = st.cpu().numpy().astype(np.float64)
+names = ["setup+residuals", "W+K build", "cholesky", "predictor", "corrector", "update"]
+it = a[:, 6]
+tot = a[:, :6].sum(1)
+print(f"agents {n} N {N}: kernel {ev[0].elapsed_time(ev[1]):.3f} ms (with stamps); iters mean {it.mean():.2f} max {it.max():.0f}")
+for i, nm in enumerate(names):
+    print(f"  {nm:16s} {a[:, i].mean() / it.mean():10.0f} clk/iter   {100 * a[:, i].sum() / tot.sum():5.1f} %")
+print(f"  total            {tot.mean() / it.mean():10.0f} clk/iter ; slowest agent {tot.max():.0f} clk")
+R.opts = L.opts()
+ev[0].record()
+R.solve()
+ev[1].record()
+torch.cuda.synchronize()
+print(f"kernel without stamps {ev[0].elapsed_time(ev[1]):.3f} ms; status {np.unique(R.status.cpu().numpy(), return_counts=True)}")
