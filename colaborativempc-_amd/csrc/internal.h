@@ -50,6 +50,23 @@ struct MpcPtrs {
     unsigned long long* stamps;  // optional: batch x 8 per-phase s_memtime counts (v2 kernel)
 };
 
+// Interior-point safeguards shared by both solver kernels and the C oracle (oracle/cmpc_oracle.c).
+//  * kNbhdGamma: after each step every active pair keeps t_r lam_r >= gamma * mu (wide
+//    neighbourhood, step backtracked by 0.8).  Without it Mehrotra's corrector can cycle on
+//    degenerate collision rows: two rows alternately block the step and mu stalls near 1e-5.
+//  * kStallIters: once the merit max(res, 1e4 mu) is below 1e3 tol, that many iterations
+//    without a new best stop the solve (rounding floor); the best iterate is returned.
+constexpr double kNbhdGamma = 0.01;
+constexpr int kMaxBacktrack = 30;
+constexpr int kStallIters = 3;
+enum { kStopMaxIter = 0, kStopConverged = 1, kStopBreakdown = 2, kStopStalled = 3, kStopNonFinite = 4 };
+
+// Per-agent status of a solve that ended without meeting the tolerance (best merit best_m).
+__host__ __device__ inline int stop_status(int stop, double best_m, double tol) {
+    if (best_m < 1e3 * tol) return CMPC_SOLVED_INACCURATE;
+    return stop == kStopMaxIter ? CMPC_MAX_ITER_REACHED : CMPC_UNSOLVED;
+}
+
 // Fills the derived fields of MpcConst; returns CMPC_OK or an error code with msg.
 int mpc_prepare(const cmpc_mpc_dims* d, const cmpc_mpc_weights* w, const cmpc_opts* o,
                 MpcConst* c, const char** msg);

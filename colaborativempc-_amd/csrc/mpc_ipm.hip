@@ -24,7 +24,7 @@ typedef double v4d __attribute__((ext_vector_type(4)));
 
 struct Lds {
     int K, G0, G1, Y, W, X, dX, yb, psi, U, dU, rd, gU, sig, dsig, Dsig, rsig;
-    int t, lam, th, rho, rt, rp, w, dta, dla, GdU, red, total;
+    int t, lam, th, rho, rt, rp, w, dta, dla, GdU, bU, bsig, red, total;
 };
 
 __host__ __device__ inline int lds_take(int& o, int cnt) {
@@ -63,6 +63,8 @@ __host__ __device__ inline Lds lds_layout(const MpcConst& c) {
     L.dta = lds_take(o, c.m);
     L.dla = lds_take(o, c.m);
     L.GdU = lds_take(o, c.m);
+    L.bU = lds_take(o, c.npad);
+    L.bsig = lds_take(o, c.N * c.ns);
     L.red = lds_take(o, kWave);
     L.total = o;
     return L;
@@ -251,6 +253,8 @@ __global__ __launch_bounds__(kWave) void mpc_ipm_kernel(const MpcConst c, const 
     double* dta = sm + L.dta;
     double* dla = sm + L.dla;
     double* GdU = sm + L.GdU;
+    double* bU = sm + L.bU;
+    double* bsig = sm + L.bsig;
 
     for (int i = l; i < L.total; i += kWave) sm[i] = 0.0;
     bar();
@@ -286,7 +290,10 @@ __global__ __launch_bounds__(kWave) void mpc_ipm_kernel(const MpcConst c, const 
     const double scale_p = wave_max(sp_l);
     bar();
 
-    int status = CMPC_MAX_ITER_REACHED, it;
+    // best iterate by merit max(res, 1e4 mu) (< tol <=> converged), returned when the method
+    // stops short of convergence (iteration cap, factorisation breakdown, stagnation)
+    double best_m = INFINITY, best_kkt = INFINITY;
+    int best_it = 0, stop = kStopMaxIter, it;
     double kkt = INFINITY;
     for (it = 1; it <= c.max_iter; ++it) {
         // ================= residuals =================
@@ -341,12 +348,24 @@ __global__ __launch_bounds__(kWave) void mpc_ipm_kernel(const MpcConst c, const 
         // (degenerate rows sit at t, lambda ~ sqrt(mu): primal accuracy needs tiny mu)
         const double res = nmax(nmax(wave_max(nrd_l) / gscale, wave_max(nrs_l) / c.qs_max), wave_max(nrp_l) / scale_p);
         kkt = nmax(res, mu);
-        if (res < c.tol && mu < 1e-4 * c.tol) {
-            status = CMPC_SOLVED;
+        const double merit = nmax(res, 1e4 * mu);
+        if (!isfinite(merit)) {
+            stop = kStopNonFinite;
             break;
         }
-        if (!isfinite(kkt)) {
-            status = CMPC_UNSOLVED;
+        if (merit < best_m) {
+            best_m = merit;
+            best_kkt = kkt;
+            best_it = it;
+            for (int i = l; i < n; i += kWave) bU[i] = U[i];
+            for (int i = l; i < N * ns; i += kWave) bsig[i] = sig[i];
+        }
+        if (merit < c.tol) {
+            stop = kStopConverged;
+            break;
+        }
+        if (best_m < 1e3 * c.tol && it - best_it >= kStallIters) {
+            stop = kStopStalled;
             break;
         }
         bar();
@@ -468,8 +487,8 @@ __global__ __launch_bounds__(kWave) void mpc_ipm_kernel(const MpcConst c, const 
             else if (l > j && l < n) K[l * ldk + j] = v / d;
             bar();
         }
-        if (!chol_ok) {  // factorisation broke down: keep the current iterate
-            status = (kkt < 1e3 * c.tol) ? CMPC_SOLVED_INACCURATE : CMPC_UNSOLVED;
+        if (!chol_ok) {
+            stop = kStopBreakdown;
             break;
         }
 
@@ -578,6 +597,18 @@ __global__ __launch_bounds__(kWave) void mpc_ipm_kernel(const MpcConst c, const 
                 sig_c = ratio * ratio * ratio;
             } else {
                 alpha = fmin(1.0, 0.995 * amax);
+                // stay in the wide neighbourhood t_r lam_r >= gamma mu(alpha) (see kNbhdGamma)
+                for (int bt = 0; bt < kMaxBacktrack; ++bt) {
+                    double mn_l = 0.0, pm_l = INFINITY;
+                    for (int r = l; r < m; r += kWave)
+                        if (isfinite(w[r])) {
+                            const double pr = (t[r] + alpha * rho[r]) * (lam[r] + alpha * rt[r]);
+                            mn_l += pr;
+                            pm_l = fmin(pm_l, pr);
+                        }
+                    if (wave_min(pm_l) >= kNbhdGamma * (wave_sum(mn_l) / mact)) break;
+                    alpha *= 0.8;
+                }
             }
         }
         // ---- update (corrector direction: dU, dX, dsig, (rho, rt) = (dt, dl)) ----
@@ -591,9 +622,16 @@ __global__ __launch_bounds__(kWave) void mpc_ipm_kernel(const MpcConst c, const 
             }
         bar();
     }
-    if (it > c.max_iter) {
-        it = c.max_iter;
-        if (kkt < 1e3 * c.tol) status = CMPC_SOLVED_INACCURATE;
+    if (it > c.max_iter) it = c.max_iter;
+    bar();
+    int status = CMPC_SOLVED;
+    if (stop != kStopConverged) {
+        if (best_it > 0) {  // restore the best iterate
+            for (int i = l; i < n; i += kWave) U[i] = bU[i];
+            for (int i = l; i < N * ns; i += kWave) sig[i] = bsig[i];
+            kkt = best_kkt;
+        }
+        status = stop_status(stop, best_m, c.tol);
     }
     bar();
 

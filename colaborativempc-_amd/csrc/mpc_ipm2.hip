@@ -23,7 +23,7 @@
 namespace cmpc {
 
 struct Lds2 {
-    int A, B, C, H, Pq, x0, up, W, X, dX, yb0, U, dU, rd, gU, vb, thin, G0, G1, Y, S0, SP, red, total;
+    int A, B, C, H, Pq, x0, up, W, X, dX, yb0, U, dU, rd, gU, vb, thin, bU, G0, G1, Y, S0, SP, red, total;
 };
 
 template <int T, int NX, int NU, int MC>
@@ -53,6 +53,7 @@ __host__ __device__ inline Lds2 lds2_layout(int N) {
     L.gU = take(NP);
     L.vb = take(NP);
     L.thin = take(NP);
+    L.bU = take(NP);
     L.G0 = take(NXP * NP);
     L.G1 = take(NXP * NP);
     L.Y = take(NXP * NP);
@@ -139,6 +140,7 @@ __global__ __launch_bounds__(64, 1) void mpc_ipm2_kernel(const MpcConst c, const
     double* gU = sm + L.gU;
     double* vb = sm + L.vb;
     double* thin = sm + L.thin;
+    double* bU = sm + L.bU;
     double* S0 = sm + L.S0;
     double* SP = sm + L.SP;
     double* red = sm + L.red;
@@ -229,7 +231,10 @@ __global__ __launch_bounds__(64, 1) void mpc_ipm2_kernel(const MpcConst c, const
     const double scale_p = wave_max(sp_l);
     STAMP(0);
 
-    int status = CMPC_MAX_ITER_REACHED, it;
+    // best iterate by merit max(res, 1e4 mu) (< tol <=> converged), returned when the method
+    // stops short of convergence (iteration cap, factorisation breakdown, stagnation)
+    double best_m = INFINITY, best_kkt = INFINITY, bsg[NS] = {0.0, 0.0, 0.0};
+    int best_it = 0, stop = kStopMaxIter, it;
     double kkt = INFINITY;
     double th[RX], Dsig[NS], rsig[NS];
     v4d acc[NT];
@@ -302,12 +307,25 @@ __global__ __launch_bounds__(64, 1) void mpc_ipm2_kernel(const MpcConst c, const
                                 wave_max(nrp_l) / scale_p);
         kkt = nmax(res, mu);
         STAMP(0);
-        if (res < c.tol && mu < 1e-4 * c.tol) {
-            status = CMPC_SOLVED;
+        const double merit = nmax(res, 1e4 * mu);
+        if (!isfinite(merit)) {
+            stop = kStopNonFinite;
             break;
         }
-        if (!isfinite(kkt)) {
-            status = CMPC_UNSOLVED;
+        if (merit < best_m) {
+            best_m = merit;
+            best_kkt = kkt;
+            best_it = it;
+            for (int i = l; i < NP; i += 64) bU[i] = U[i];
+#pragma unroll
+            for (int j = 0; j < NS; ++j) bsg[j] = sg[j];
+        }
+        if (merit < c.tol) {
+            stop = kStopConverged;
+            break;
+        }
+        if (best_m < 1e3 * c.tol && it - best_it >= kStallIters) {
+            stop = kStopStalled;
             break;
         }
 
@@ -516,8 +534,8 @@ __global__ __launch_bounds__(64, 1) void mpc_ipm2_kernel(const MpcConst c, const
             }
         }
         STAMP(2);
-        if (!chol_ok) {  // factorisation broke down: keep the current iterate
-            status = (kkt < 1e3 * c.tol) ? CMPC_SOLVED_INACCURATE : CMPC_UNSOLVED;
+        if (!chol_ok) {
+            stop = kStopBreakdown;
             break;
         }
         // inverse diagonal of the owning block row, for the in-block substitutions
@@ -683,6 +701,21 @@ __global__ __launch_bounds__(64, 1) void mpc_ipm2_kernel(const MpcConst c, const
                 STAMP(3);
             } else {
                 alpha = fmin(1.0, 0.995 * amax);
+                // stay in the wide neighbourhood t_r lam_r >= gamma mu(alpha) (see kNbhdGamma)
+                for (int bt = 0; bt < kMaxBacktrack; ++bt) {
+                    double mn_l = 0.0, pm_l = INFINITY;
+#pragma unroll
+                    for (int r = 0; r < RX; ++r)
+                        if (ACT(r)) {
+                            const double sd = sdr(r);
+                            const double pr = (t[r] + alpha * (-rp[r] - gdu[r] - sd)) *
+                                              (lam[r] + alpha * (rho[r] + th[r] * (gdu[r] + sd)));
+                            mn_l += pr;
+                            pm_l = fmin(pm_l, pr);
+                        }
+                    if (wave_min(pm_l) >= kNbhdGamma * (wave_sum(mn_l) / mact)) break;
+                    alpha *= 0.8;
+                }
 #pragma unroll
                 for (int r = 0; r < RX; ++r)
                     if (ACT(r)) {
@@ -700,9 +733,17 @@ __global__ __launch_bounds__(64, 1) void mpc_ipm2_kernel(const MpcConst c, const
         bar();
         STAMP(5);
     }
-    if (it > c.max_iter) {
-        it = c.max_iter;
-        if (kkt < 1e3 * c.tol) status = CMPC_SOLVED_INACCURATE;
+    if (it > c.max_iter) it = c.max_iter;
+    bar();
+    int status = CMPC_SOLVED;
+    if (stop != kStopConverged) {
+        if (best_it > 0) {  // restore the best iterate
+            for (int i = l; i < NP; i += 64) U[i] = bU[i];
+#pragma unroll
+            for (int j = 0; j < NS; ++j) sg[j] = bsg[j];
+            kkt = best_kkt;
+        }
+        status = stop_status(stop, best_m, c.tol);
     }
     bar();
 

@@ -76,6 +76,11 @@ static void adjoint(const shared_t* S, const agent_t* a, const double* ybar, dou
 /* NaN-propagating max (fmax would drop a NaN residual and report convergence) */
 static double nmax(double a, double b) { return (a > b || a != a) ? a : b; }
 
+#ifndef NBHD_GAMMA
+#define NBHD_GAMMA 0.01 /* wide-neighbourhood floor: t_r lambda_r >= gamma mu after a step */
+#endif
+#define STALL_ITERS 3   /* near-converged iterations without merit progress before stopping */
+
 static int chol(double* K, int n) {
     for (int j = 0; j < n; ++j) {
         double d = K[IDX2(j, j, n)];
@@ -116,7 +121,7 @@ static double max_step(const double* v, const double* dv, const unsigned char* a
 }
 
 typedef struct {
-    double *Gam, *K, *X, *dX, *U, *dU, *sig, *dsig, *Dsig, *rsig, *t, *lam, *th, *rho, *rt, *rp, *w,
+    double *bU, *bsig, *Gam, *K, *X, *dX, *U, *dU, *sig, *dsig, *Dsig, *rsig, *t, *lam, *th, *rho, *rt, *rp, *w,
         *dt_a, *dl_a, *dtv, *dlv, *GdU, *ybar, *gU, *rd, *rhs, *psi, *tmp, *W, *Yk;
     unsigned char* act;
 } work_t;
@@ -192,7 +197,12 @@ static int solve_one(const shared_t* S, const agent_t* a, double tol, int max_it
     double qs_max = 1.0;
     for (int j = 0; j < ns; ++j) if (2 * S->Qs[j] > qs_max) qs_max = 2 * S->Qs[j];
 
-    int status = -2, it;
+    /* best iterate by merit max(res, 1e4 mu) (< tol <=> converged): returned when the
+       method stops short of convergence (max_iter, factorisation breakdown, stagnation) */
+    double best_m = INFINITY, best_kkt = INFINITY;
+    int best_it = 0, stop = 0; /* stop: 0 max_iter, 1 converged, 2 breakdown, 3 stagnation, 4 non-finite */
+    double *bU = wk->bU, *bsig = wk->bsig;
+    int it;
     double kkt = INFINITY;
     for (it = 1; it <= max_iter; ++it) {
         /* ---- residuals ---- */
@@ -256,8 +266,18 @@ static int solve_one(const shared_t* S, const agent_t* a, double tol, int max_it
            (degenerate rows sit at t, lambda ~ sqrt(mu): primal accuracy needs tiny mu) */
         double res = nmax(nmax(nrd / gscale, nrs / qs_max), nrp / scale_p);
         kkt = nmax(res, mu);
-        if (res < tol && mu < 1e-4 * tol) { status = 1; break; }
-        if (!isfinite(kkt)) { status = -10; break; }
+        const double merit = nmax(res, 1e4 * mu);
+        if (!isfinite(merit)) { stop = 4; break; }
+        if (merit < best_m) {
+            best_m = merit;
+            best_kkt = kkt;
+            best_it = it;
+            memcpy(bU, U, sizeof(double) * n);
+            memcpy(bsig, sig, sizeof(double) * N * ns);
+        }
+        if (merit < tol) { stop = 1; break; }
+        /* near-converged but no progress for STALL_ITERS iterations: rounding floor reached */
+        if (best_m < 1e3 * tol && it - best_it >= STALL_ITERS) { stop = 3; break; }
 
         /* ---- Newton matrix ---- */
         for (int r = 0; r < m; ++r) wk->th[r] = wk->act[r] ? lam[r] / t[r] : 0.0;
@@ -322,7 +342,7 @@ static int solve_one(const shared_t* S, const agent_t* a, double tol, int max_it
                 int r = ms + (k * nu + i) * 2;
                 K[IDX2(k * nu + i, k * nu + i, n)] += wk->th[r] + wk->th[r + 1];
             }
-        if (chol(K, n)) { status = (kkt < 1e3 * tol) ? 2 : -10; break; }
+        if (chol(K, n)) { stop = 2; break; }
 
         /* ---- predictor / corrector ---- */
         double sig_c = 0.0, mu_aff = 0.0;
@@ -399,6 +419,20 @@ static int solve_one(const shared_t* S, const agent_t* a, double tol, int max_it
             } else {
                 al = 0.995 * al;
                 if (al > 1.0) al = 1.0;
+                /* keep the iterate in the wide neighbourhood t_r lambda_r >= gamma mu(al):
+                   without it Mehrotra's corrector can cycle on degenerate collision rows
+                   (two rows alternately blocking the step, mu stalled near 1e-5) */
+                for (int bt = 0; bt < 30 && mact; ++bt) {
+                    double mn = 0.0, pmin = INFINITY;
+                    for (int r = 0; r < m; ++r)
+                        if (wk->act[r]) {
+                            double pr = (t[r] + al * dt[r]) * (lam[r] + al * dl[r]);
+                            mn += pr;
+                            if (pr < pmin) pmin = pr;
+                        }
+                    if (pmin >= NBHD_GAMMA * (mn / mact)) break;
+                    al *= 0.8;
+                }
                 for (int c = 0; c < n; ++c) U[c] += al * wk->dU[c];
                 for (int q = 0; q < N * ns; ++q) sig[q] += al * wk->dsig[q];
                 for (int r = 0; r < m; ++r)
@@ -407,9 +441,17 @@ static int solve_one(const shared_t* S, const agent_t* a, double tol, int max_it
             }
         }
     }
-    if (it > max_iter) {
-        it = max_iter;
-        if (kkt < 1e3 * tol) status = 2;
+    if (it > max_iter) it = max_iter;
+    int status;
+    if (stop == 1) {
+        status = 1;
+    } else {
+        if (best_it > 0) { /* restore the best iterate */
+            memcpy(U, bU, sizeof(double) * n);
+            memcpy(sig, bsig, sizeof(double) * N * ns);
+            kkt = best_kkt;
+        }
+        status = best_m < 1e3 * tol ? 2 : (stop == 0 ? -2 : -10);
     }
     /* exact re-simulation for the output trajectory */
     fwd_sim(S, a, a->x0, U, X);
@@ -449,7 +491,7 @@ int cmpc_oracle_solve(int nx, int nu, int N, int ns, int mc, int batch,
 #pragma omp parallel
     {
         work_t wk;
-        size_t need = (size_t)(N + 1) * nx * n + (size_t)n * n + 4 * (size_t)(N + 1) * nx + 4 * (size_t)n +
+        size_t need = (size_t)n + (size_t)N * ns + (size_t)(N + 1) * nx * n + (size_t)n * n + 4 * (size_t)(N + 1) * nx + 4 * (size_t)n +
                       4 * (size_t)N * ns + 12 * (size_t)m + 2 * (size_t)nx + (size_t)nx * nx + (size_t)n * 3 + (size_t)nx * n;
         double* buf = (double*)calloc(need, sizeof(double));
         unsigned char* act = (unsigned char*)calloc(m, 1);
@@ -459,6 +501,7 @@ int cmpc_oracle_solve(int nx, int nu, int N, int ns, int mc, int batch,
         } else {
             double* p = buf;
 #define TAKE(f, cnt) do { wk.f = p; p += (cnt); } while (0)
+            TAKE(bU, n); TAKE(bsig, N * ns);
             TAKE(Gam, (size_t)(N + 1) * nx * n); TAKE(K, (size_t)n * n);
             TAKE(X, (N + 1) * nx); TAKE(dX, (N + 1) * nx); TAKE(ybar, (N + 1) * nx); TAKE(W, nx * nx);
             TAKE(U, n); TAKE(dU, n); TAKE(gU, n); TAKE(rd, n); TAKE(rhs, n);

@@ -102,7 +102,7 @@ def test_synthetic_batch_vs_c_oracle(gpu_ctx, n, N, nb, dim):
     assert (st == cmpc.CMPC_SOLVED).all()
     assert (sc_ == 1).all()
     assert np.abs(z - zc).max() < Z_TOL
-    assert kkt.max() < 1e-10
+    assert kkt.max() < 1e-9   # solved <=> scaled residuals < tol (1e-9), mu < 1e-4 tol
 
 
 def test_synthetic_small_vs_reference_form(gpu_ctx):
