@@ -27,6 +27,22 @@ from . import _lib as L
 from .solver import _dims, _tptr, _weights, nz_of
 
 
+def exchange_positions(traj_all, traj_local, world=1, group=None):
+    """The per-round exchange of predicted positions (the np.swapaxes "exchange" of
+    LPV_HP_N_main.py:117, and the ROS topic publish/subscribe of LPV_ROS_main.py:66-77):
+    every rank's contiguous block `traj_local` (B, N+1, 2) is gathered, in rank order,
+    into the node-global `traj_all` (world*B, N+1, 2).  One all-gather per round;
+    over RCCL/xGMI with the "nccl" backend, gloo on CPU tensors."""
+    if world == 1:
+        traj_all.copy_(traj_local)
+        return
+    import torch.distributed as dist
+
+    if traj_all.shape[0] != world * traj_local.shape[0]:
+        raise ValueError("traj_all must hold world x local agents")
+    dist.all_gather_into_tensor(traj_all, traj_local.contiguous(), group=group)
+
+
 class DIRounds:
     def __init__(self, scen, rank=0, world=1, device=None, ctx=None, tol=None, max_iter=None, group=None):
         import torch
@@ -92,12 +108,7 @@ class DIRounds:
                                                         _tptr(self.traj_local), self._stream()))
 
     def exchange(self):
-        if self.world == 1:
-            self.traj_all.copy_(self.traj_local)
-        else:
-            import torch.distributed as dist
-
-            dist.all_gather_into_tensor(self.traj_all, self.traj_local, group=self.group)
+        exchange_positions(self.traj_all, self.traj_local, self.world, self.group)
 
     def step(self, timer=None):
         """One consensus round.  `timer` (start, stop) events bracket the solve launch."""
