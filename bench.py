@@ -154,7 +154,7 @@ def main():
             "mean_ipm_iters": mean_iters,
             "max_abs_err_vs_cpu": max_err,
             "roofline": {
-                "kernel": "mpc_ipm_kernel",
+                "kernel": "mpc_ipm3_kernel<4,4,2,2>",
                 "bound": "mfma",
                 "achieved": achieved_tf,
                 "peak": FP64_PEAK_TFLOPS,

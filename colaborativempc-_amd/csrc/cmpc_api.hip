@@ -163,7 +163,7 @@ int cmpc_solve_mpc_batch_dev(cmpc_ctx* ctx, const cmpc_mpc_dims* dims, const cmp
     if ((rc = set_device(ctx)) != CMPC_OK) return rc;
     cmpc::MpcPtrs p{in->A, in->B, in->x0, in->u_prev, in->qlin, in->C, in->h, out->z, out->kkt, out->iters, out->status,
                     opts ? (unsigned long long*)opts->stamps : nullptr};
-    HIP_TRY(cmpc::mpc_launch(c, p, dims->batch, (hipStream_t)stream, opts && (opts->flags & CMPC_FLAG_GENERIC)));
+    HIP_TRY(cmpc::mpc_launch(c, p, dims->batch, (hipStream_t)stream, opts ? opts->flags : 0));
     return CMPC_OK;
 }
 
@@ -197,7 +197,7 @@ int cmpc_solve_mpc_batch(cmpc_ctx* ctx, const cmpc_mpc_dims* d, const cmpc_mpc_w
     HIP_TRY(hipMemcpyAsync(dh, in->h, 8 * sh, hipMemcpyHostToDevice, s));
     cmpc::MpcPtrs p{dA, dB, dx0, du, dp, dC, dh, dz, dk, di, ds,
                     opts ? (unsigned long long*)opts->stamps : nullptr};  // stamps: device memory
-    HIP_TRY(cmpc::mpc_launch(c, p, d->batch, s, opts && (opts->flags & CMPC_FLAG_GENERIC)));
+    HIP_TRY(cmpc::mpc_launch(c, p, d->batch, s, opts ? opts->flags : 0));
     HIP_TRY(hipMemcpyAsync(out->z, dz, 8 * sz, hipMemcpyDeviceToHost, s));
     if (out->kkt) HIP_TRY(hipMemcpyAsync(out->kkt, dk, 8 * B, hipMemcpyDeviceToHost, s));
     if (out->iters) HIP_TRY(hipMemcpyAsync(out->iters, di, 4 * B, hipMemcpyDeviceToHost, s));
@@ -228,7 +228,7 @@ static int lpv_run(cmpc_ctx* ctx, const cmpc_lpv_params* prm, const cmpc_track* 
     cmpc::LpvPtrs lp{in->x_last, in->u_last, in->x_agents, in->pose, A, Bm, p, C, h, out->planes, err};
     HIP_TRY(cmpc::lpv_build_launch(lc, lp, d->batch, s));
     cmpc::MpcPtrs mp{A, Bm, in->x0, in->u_old, p, C, h, out->z, out->kkt, out->iters, out->status, nullptr};
-    HIP_TRY(cmpc::mpc_launch(mc, mp, d->batch, s, opts && (opts->flags & CMPC_FLAG_GENERIC)));
+    HIP_TRY(cmpc::mpc_launch(mc, mp, d->batch, s, opts ? opts->flags : 0));
     if (out->status) HIP_TRY(cmpc::lpv_mark_launch(err, out->status, d->batch, s));
     return CMPC_OK;
 }

@@ -47,7 +47,7 @@ struct MpcPtrs {
     double* kkt;
     int* iters;
     int* status;
-    unsigned long long* stamps;  // optional: batch x 8 per-phase s_memtime counts (v2 kernel)
+    unsigned long long* stamps;  // optional: batch x kStampSlots per-section s_memtime counts (v3 kernel)
 };
 
 // Interior-point safeguards shared by both solver kernels and the C oracle (oracle/cmpc_oracle.c).
@@ -56,6 +56,8 @@ struct MpcPtrs {
 //    degenerate collision rows: two rows alternately block the step and mu stalls near 1e-5.
 //  * kStallIters: once the merit max(res, 1e4 mu) is below 1e3 tol, that many iterations
 //    without a new best stop the solve (rounding floor); the best iterate is returned.
+// diagnostic stamps of the v3 kernel: batch x kStampSlots uint64 (last slot = iterations)
+constexpr int kStampSlots = 16;
 constexpr double kNbhdGamma = 0.01;
 constexpr int kMaxBacktrack = 30;
 constexpr int kStallIters = 3;
@@ -71,9 +73,10 @@ __host__ __device__ inline int stop_status(int stop, double best_m, double tol) 
 int mpc_prepare(const cmpc_mpc_dims* d, const cmpc_mpc_weights* w, const cmpc_opts* o,
                 MpcConst* c, const char** msg);
 size_t mpc_lds_bytes(const MpcConst& c);
-hipError_t mpc_launch(const MpcConst& c, const MpcPtrs& p, int batch, hipStream_t s, bool force_generic = false);
-// Specialised (NX, NU, MC) kernels of mpc_ipm2.hip; false when no instantiation covers the problem.
-bool mpc2_try_launch(const MpcConst& c, const MpcPtrs& p, int batch, hipStream_t s, hipError_t* err);
+// flags: CMPC_FLAG_GENERIC forces the generic kernel (diagnostics)
+hipError_t mpc_launch(const MpcConst& c, const MpcPtrs& p, int batch, hipStream_t s, int flags = 0);
+// v3 kernels of mpc_ipm3.hip (PlannerLPV row pattern, N <= 32); false when none covers the problem.
+bool mpc3_try_launch(const MpcConst& c, const MpcPtrs& p, int batch, hipStream_t s, hipError_t* err);
 
 // LPV reference-semantics builder (scheduling + planes + weights + rows).
 struct LpvConst {

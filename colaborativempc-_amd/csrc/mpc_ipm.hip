@@ -726,10 +726,10 @@ static hipError_t launch_t(const MpcConst& c, const MpcPtrs& p, int batch, hipSt
     return hipGetLastError();
 }
 
-hipError_t mpc_launch(const MpcConst& c, const MpcPtrs& p, int batch, hipStream_t s, bool force_generic) {
+hipError_t mpc_launch(const MpcConst& c, const MpcPtrs& p, int batch, hipStream_t s, int flags) {
     if (batch == 0) return hipSuccess;
     hipError_t e2;
-    if (!force_generic && mpc2_try_launch(c, p, batch, s, &e2)) return e2;
+    if (!(flags & CMPC_FLAG_GENERIC) && mpc3_try_launch(c, p, batch, s, &e2)) return e2;
     switch (c.npad / 16) {
         case 1: return launch_t<1>(c, p, batch, s);
         case 2: return launch_t<2>(c, p, batch, s);

@@ -1,0 +1,951 @@
+// Batched condensed IPM, v3: the production solver for the PlannerLPV row pattern
+// (stage rows [v <= ; v + s0 <= ; e + s1 <= ; -e + s1 <= ; planes - s2 <=], reference
+// planner/lib/plan_lib/distributedPlanner/LPV_Planner.py:251-380) with N <= 32.
+// Same QP, same interior-point method, same safeguards and termination as the generic
+// kernel (mpc_ipm.hip) and the C oracle (oracle/cmpc_oracle.c).
+//
+// Laid out so that nothing spills (the v2 kernel needed 512 registers and spilled
+// 0.9 KB/lane to scratch on its latency-critical chains):
+//  * one 64-lane wavefront per agent, one wavefront per workgroup.  LDS operations of
+//    one wave execute in order, so intra-wave LDS hand-offs need only a compiler fence
+//    (wsync), never s_barrier or a full lgkmcnt drain;
+//  * lanes 0..31 own the constraint rows of stage k+1 (k = lane), lanes 32..63 the input
+//    rows of u_k: RX = max(MC, 2 NU) register rows per lane; the slack groups of a stage
+//    stay lane-local;
+//  * batch-shared weights live in LDS, not in kernel-argument SGPRs;
+//  * K = sum_k Gamma_{k+1}' W_{k+1} Gamma_{k+1}: lane c carries column c of Gamma_k in
+//    registers through the recursion Gamma_{k+1} = A_k Gamma_k + [0 .. B_k], forms
+//    W Gamma in registers, hands both to the MFMA fragment layout through LDS and
+//    accumulates with V_MFMA_F64_16X16X4_F64 only on the tiles that are nonzero for the
+//    stage (static per horizon segment: no data-dependent branch around an MFMA);
+//  * K is factored in the accumulators (blocked right-looking Cholesky: 16x16 diagonal
+//    factor, panel substitution, trailing SYRK on MFMA); the diagonal factors L_JJ are
+//    kept in LDS for the triangular solves.
+#include <cmath>
+
+#include "internal.h"
+#include "wave_ops.h"
+
+namespace cmpc {
+
+namespace {
+
+// Intra-wave LDS ordering: the hardware keeps one wave's LDS operations in order; this
+// only stops the compiler from moving LDS accesses across the hand-off point.
+__device__ __forceinline__ void wsync() {
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    asm volatile("" ::: "memory");
+}
+
+// PlannerLPV row pattern: row 0 no slack; 1 -> s0 (+); 2,3 -> s1 (+); 4.. -> s2 (-)
+__host__ __device__ constexpr int slk(int r) { return r == 0 ? -1 : (r == 1 ? 0 : (r < 4 ? 1 : 2)); }
+__host__ __device__ constexpr double sgn(int r) { return r < 4 ? 1.0 : -1.0; }
+
+struct Lds3 {
+    int cst, A, B, C, H, Pq, x0, up, W, Gb, Yb, X, dX, yb, U, dU, rd, gU, vb, thin, bU, Ld, red, stamps, total;
+};
+
+template <int T, int NX, int NU, int NB>
+__host__ __device__ inline Lds3 lds3_layout(int N) {
+    constexpr int NP = 16 * T, NXP = (NX + 3) & ~3, MC = 4 + NB;
+    Lds3 L;
+    int o = 0;
+    auto take = [&](int cnt) {
+        int r = o;
+        o += (cnt + 1) & ~1;
+        return r;
+    };
+    L.cst = take(NX * NX + 2 * NU * NU + 3 + 2 * NU);
+    L.A = take(N * NX * NX);
+    L.B = take(N * NX * NU);
+    L.C = take(N * MC * NX);
+    L.H = take(N * MC);
+    L.Pq = take((N + 1) * NX);
+    L.x0 = take(NX);
+    L.up = take(NU);
+    // W, Gb, Yb are contiguous: the Cholesky panel scratch aliases them after the K build
+    L.W = take(N * NX * NX);
+    L.Gb = take(NXP * NP);
+    L.Yb = take(NXP * NP);
+    L.X = take((N + 1) * NX);
+    L.dX = take((N + 1) * NX);
+    L.yb = take((N + 1) * NX);
+    L.U = take(NP);
+    L.dU = take(NP);
+    L.rd = take(NP);
+    L.gU = take(NP);
+    L.vb = take(NP);
+    L.thin = take(NP);
+    L.bU = take(NP);
+    L.Ld = take(T * 16 * 17);
+    L.red = take(16);
+    L.stamps = take(kStampSlots);
+    L.total = o;
+    return L;
+}
+
+// x_0 = x0 (LDS, or 0), x_{k+1} = A_k x_k + B_k u_k.  Lane (l & 15) = s < NX of every row of
+// 16 carries x_s (the rows are duplicates); x_t reaches the row by DPP row_newbcast.  The next
+// stage's A row and B u term are fetched while the current stage computes.
+template <int NX, int NU>
+__device__ __forceinline__ void fwd3(int l, int N, const double* A, const double* B, const double* x0,
+                                     const double* U, double* X) {
+    static_assert(NX <= 16, "row broadcast");
+    const int s = (l & 15) < NX ? (l & 15) : 0;
+    double xr = x0 ? x0[s] : 0.0;
+    if (l < NX) X[l] = xr;
+    double a[NX], bu = 0.0;
+    auto fetch = [&](int k, double* av, double& b) {
+#pragma unroll
+        for (int t = 0; t < NX; ++t) av[t] = A[(k * NX + s) * NX + t];
+        double v = 0.0;
+#pragma unroll
+        for (int i = 0; i < NU; ++i) v = fma(B[(k * NX + s) * NU + i], U[k * NU + i], v);
+        b = v;
+    };
+    if (N > 0) fetch(0, a, bu);
+    for (int k = 0; k < N; ++k) {
+        double an[NX], bn = 0.0;
+        if (k + 1 < N) fetch(k + 1, an, bn);
+        double v0 = bu, v1 = 0.0;
+        static_for<0, NX>([&](auto t) __attribute__((always_inline)) {
+            constexpr int tt = decltype(t)::value;
+            if constexpr (tt & 1) v1 = fma(a[tt], bcast16<tt>(xr), v1);
+            else v0 = fma(a[tt], bcast16<tt>(xr), v0);
+        });
+        xr = v0 + v1;
+        if (l < NX) X[(k + 1) * NX + l] = xr;
+#pragma unroll
+        for (int t = 0; t < NX; ++t) a[t] = an[t];
+        bu = bn;
+    }
+}
+
+// Two adjoints at once (rows 0,1 of the wave on y0 -> o0, rows 2,3 on y1 -> o1):
+// o_k = B_k' psi_{k+1}, psi_N = y_N, psi_k = y_k + A_k' psi_{k+1}.  Lane (l & 15) = s carries
+// psi_s; psi_t reaches the row by DPP row_newbcast; operands of stage k-1 are fetched ahead.
+template <int NX, int NU>
+__device__ __forceinline__ void adj3(int l, int N, const double* A, const double* B, const double* y0,
+                                     const double* y1, double* o0, double* o1) {
+    static_assert(NX <= 16 && NU <= 16, "row broadcast");
+    const int h = l >> 5, s = l & 15;
+    const int sx = s < NX ? s : 0, su = s < NU ? s : 0;
+    const bool wr = ((l & 16) == 0) && s < NU;  // rows 0 and 2 write the outputs
+    const double* y = h ? y1 : y0;
+    double* o = h ? o1 : o0;
+    double pr = y[N * NX + sx];
+    double a[NX], bb[NX], yk = 0.0;
+    auto fetch = [&](int k, double* av, double* bv, double& yv) {
+#pragma unroll
+        for (int t = 0; t < NX; ++t) {
+            av[t] = A[(k * NX + t) * NX + sx];
+            bv[t] = B[(k * NX + t) * NU + su];
+        }
+        yv = k > 0 ? y[k * NX + sx] : 0.0;
+    };
+    if (N > 0) fetch(N - 1, a, bb, yk);
+    for (int k = N - 1; k >= 0; --k) {
+        double an[NX], bn[NX], yn = 0.0;
+        if (k > 0) fetch(k - 1, an, bn, yn);
+        double ps[NX];
+        static_for<0, NX>([&](auto t) __attribute__((always_inline)) {
+            constexpr int tt = decltype(t)::value;
+            ps[tt] = bcast16<tt>(pr);
+        });
+        double v0 = 0.0, v1 = 0.0, p0 = yk, p1 = 0.0;
+#pragma unroll
+        for (int t = 0; t < NX; ++t) {
+            if (t & 1) {
+                v1 = fma(bb[t], ps[t], v1);
+                p1 = fma(a[t], ps[t], p1);
+            } else {
+                v0 = fma(bb[t], ps[t], v0);
+                p0 = fma(a[t], ps[t], p0);
+            }
+        }
+        if (wr) o[k * NU + s] = v0 + v1;
+        pr = p0 + p1;
+#pragma unroll
+        for (int t = 0; t < NX; ++t) {
+            a[t] = an[t];
+            bb[t] = bn[t];
+        }
+        yk = yn;
+    }
+}
+
+}  // namespace
+
+template <int T, int NX, int NU, int NB>
+__global__ __launch_bounds__(64, 1) void mpc_ipm3_kernel(const MpcConst c, const MpcPtrs P) {
+    constexpr int MC = 4 + NB, NS = 3, NT = T * (T + 1) / 2, NP = 16 * T, NXP = (NX + 3) & ~3;
+    constexpr int NI = 2 * NU, RX = MC > NI ? MC : NI;
+    extern __shared__ __attribute__((aligned(16))) double sm[];
+    const int l0 = threadIdx.x, b = blockIdx.x, N = c.N, n = N * NU, ms = N * MC;
+    const int l = l0;
+    const Lds3 L = lds3_layout<T, NX, NU, NB>(N);
+    double* Q2 = sm + L.cst;          // 2Q
+    double* R2 = Q2 + NX * NX;        // 2R
+    double* dR2 = R2 + NU * NU;       // 2dR
+    double* Qs2 = dR2 + NU * NU;      // 2Qs
+    double* ub = Qs2 + 3;
+    double* lb = ub + NU;
+    double* sA = sm + L.A;
+    double* sB = sm + L.B;
+    double* sC = sm + L.C;
+    double* sH = sm + L.H;
+    double* sP = sm + L.Pq;
+    double* sx0 = sm + L.x0;
+    double* sup = sm + L.up;
+    double* sW = sm + L.W;
+    double* Gb = sm + L.Gb;
+    double* Yb = sm + L.Yb;
+    double* X = sm + L.X;
+    double* dX = sm + L.dX;
+    double* yb = sm + L.yb;
+    double* U = sm + L.U;
+    double* dU = sm + L.dU;
+    double* rd = sm + L.rd;
+    double* gU = sm + L.gU;
+    double* vb = sm + L.vb;
+    double* thin = sm + L.thin;
+    double* bU = sm + L.bU;
+    double* Ld = sm + L.Ld;
+    double* red = sm + L.red;
+    double* SP = sW;  // Cholesky panel scratch (aliases W | Gb | Yb after the K build)
+    const bool stamp = P.stamps != nullptr && !c.debug;
+    // diagnostic per-section clock sums live in LDS (registers stay with the solver)
+    unsigned long long* tsum = reinterpret_cast<unsigned long long*>(sm + L.stamps);
+    if (l < kStampSlots) tsum[l] = 0;
+    unsigned long long t_a = stamp ? clock64_() : 0, t_b = 0;
+#define STAMP(slot)                                \
+    if (stamp) {                                   \
+        t_b = clock64_();                          \
+        if (l == 0) tsum[slot] += t_b - t_a;       \
+        t_a = t_b;                                 \
+    }
+
+    // ---------------- stage the agent's data and the shared weights into LDS ----------------
+    {
+        const double* gA = P.A + (size_t)b * N * NX * NX;
+        const double* gB = P.B + (size_t)b * N * NX * NU;
+        const double* gC = P.C + (size_t)b * N * MC * NX;
+        const double* gP = P.p + (size_t)b * (N + 1) * NX;
+        for (int i = l; i < N * NX * NX; i += 64) sA[i] = gA[i];
+        for (int i = l; i < N * NX * NU; i += 64) sB[i] = gB[i];
+        for (int i = l; i < N * MC * NX; i += 64) sC[i] = gC[i];
+        for (int i = l; i < ms; i += 64) sH[i] = P.h[(size_t)b * ms + i];
+        for (int i = l; i < (N + 1) * NX; i += 64) sP[i] = gP[i];
+        if (l < NX) sx0[l] = P.x0[(size_t)b * NX + l];
+        if (l < NU) sup[l] = P.up[(size_t)b * NU + l];
+        for (int i = l; i < NX * NX; i += 64) Q2[i] = 2.0 * c.Q[i];
+        if (l < NU * NU) {
+            R2[l] = 2.0 * c.R[l];
+            dR2[l] = 2.0 * c.dR[l];
+        }
+        if (l < 3) Qs2[l] = 2.0 * c.Qs[l];
+        if (l < NU) {
+            ub[l] = c.u_ub[l];
+            lb[l] = c.u_lb[l];
+        }
+        for (int i = l; i < NP; i += 64) {
+            U[i] = 0.0;
+            dU[i] = 0.0;
+            vb[i] = 0.0;
+            thin[i] = 0.0;
+            bU[i] = 0.0;
+        }
+    }
+    // ---- rows owned by this lane: stage k+1 rows (lanes 0..31) or input rows of u_k (32..63) ----
+    const bool lo = l < 32;
+    const int k = l & 31;
+    const bool own = k < N;
+    double t[RX], lam[RX], th[RX], rp[RX], rho[RX], gdu[RX];
+    unsigned actm = 0;  // bit r: row r of this lane exists and has a finite bound
+    auto wv = [&](int r) -> double {
+        if (lo) return sH[k * MC + r];
+        return (r & 1) ? -lb[r >> 1] : ub[r >> 1];
+    };
+    double sg[NS] = {0.0, 0.0, 0.0};
+    wsync();
+    if (own) {
+#pragma unroll
+        for (int r = 0; r < RX; ++r)
+            if ((lo ? r < MC : r < NI) && isfinite(wv(r))) actm |= 1u << r;
+    }
+#define ACT(r) ((actm >> (r)) & 1u)
+    fwd3<NX, NU>(l, N, sA, sB, sx0, U, X);
+    wsync();
+
+    // value of row r at (Xv, Uv[, sig]) for this lane's rows
+    auto rowval = [&](int r, const double* Xv, const double* Uv, bool with_sig) -> double {
+        if (lo) {
+            const double* cr = sC + (k * MC + r) * NX;
+            const double* xk = Xv + (k + 1) * NX;
+            double v = 0.0;
+#pragma unroll
+            for (int s = 0; s < NX; ++s) v = fma(cr[s], xk[s], v);
+            if (with_sig && slk(r) >= 0) v += sgn(r) * sg[slk(r)];
+            return v;
+        }
+        const double u = Uv[k * NU + (r >> 1)];
+        return (r & 1) ? -u : u;
+    };
+
+    double mact_l = 0.0, sp_l = 1.0;
+#pragma unroll
+    for (int r = 0; r < RX; ++r) {
+        if (ACT(r)) {
+            const double w = wv(r);
+            t[r] = fmax(w - rowval(r, X, U, true), 1.0);
+            lam[r] = 1.0;
+            mact_l += 1.0;
+            sp_l = fmax(sp_l, fabs(w));
+        } else {
+            t[r] = 1.0;
+            lam[r] = 0.0;
+        }
+        th[r] = rp[r] = rho[r] = gdu[r] = 0.0;
+    }
+    const double mact = fmax(wave_sum(mact_l), 1.0);
+    const double scale_p = wave_max(sp_l);
+    STAMP(14);
+
+    // best iterate by merit max(res, 1e4 mu) (< tol <=> converged), returned when the method
+    // stops short of convergence (iteration cap, factorisation breakdown, stagnation)
+    double best_m = INFINITY, best_kkt = INFINITY, bsg[NS] = {0.0, 0.0, 0.0};
+    int best_it = 0, stop = kStopMaxIter, it;
+    double kkt = INFINITY;
+    double Dsig[NS] = {1.0, 1.0, 1.0}, rsig[NS] = {0.0, 0.0, 0.0}, dsg[NS] = {0.0, 0.0, 0.0};
+    v4d acc[NT];
+    for (it = 1; it <= c.max_iter; ++it) {
+        // Opaque zero: the lane-index arithmetic and lane masks below are recomputed inside the
+        // iteration instead of being hoisted out of it by LICM (hoisted, they held hundreds of
+        // registers for the whole solve and spilled to scratch).
+        int oz_;
+        asm volatile("v_mov_b32 %0, 0" : "=v"(oz_));
+        const int l = l0 + oz_;
+        const bool lo = l < 32;
+        const int k = l & 31;
+        const bool own = k < N;
+        // ================= residuals =================
+        for (int i = l; i < (N + 1) * NX; i += 64) {
+            const int kk = i / NX, s = i - kk * NX;
+            double v = 2.0 * sP[i];
+#pragma unroll
+            for (int u = 0; u < NX; ++u) v = fma(Q2[s * NX + u], X[kk * NX + u], v);
+            yb[i] = v;
+        }
+        wsync();
+        // second adjoint input (in dX) = yb + C' lambda on stages 1..N
+        if (lo && own) {
+#pragma unroll
+            for (int s = 0; s < NX; ++s) {
+                double v = yb[(k + 1) * NX + s];
+#pragma unroll
+                for (int r = 0; r < MC; ++r) v = fma(lam[r], sC[(k * MC + r) * NX + s], v);
+                dX[(k + 1) * NX + s] = v;
+            }
+        }
+        if (l < NX) dX[l] = yb[l];
+        wsync();
+        STAMP(0);
+        adj3<NX, NU>(l, N, sA, sB, yb, dX, gU, rd);
+        wsync();
+        STAMP(1);
+        double gs_l = 1.0, nrd_l = 0.0, nrs_l = 0.0, nrp_l = 0.0, mu_l = 0.0;
+        if (own) {
+            if (lo) {
+#pragma unroll
+                for (int j = 0; j < NS; ++j) {
+                    double v = Qs2[j] * sg[j];
+#pragma unroll
+                    for (int r = 0; r < MC; ++r)
+                        if (slk(r) == j) v += sgn(r) * lam[r];
+                    rsig[j] = v;
+                    nrs_l = nmax(nrs_l, fabs(v));
+                }
+            } else {
+#pragma unroll
+                for (int i = 0; i < NU; ++i) {
+                    const int ci = k * NU + i;
+                    double v = 0.0;
+#pragma unroll
+                    for (int j = 0; j < NU; ++j) {
+                        const double uk = U[k * NU + j];
+                        const double duk = uk - (k ? U[(k - 1) * NU + j] : sup[j]);
+                        const double dun = (k + 1 < N) ? U[(k + 1) * NU + j] - uk : 0.0;
+                        v += R2[i * NU + j] * uk + dR2[i * NU + j] * (duk - dun);
+                    }
+                    const double g = gU[ci] + v;
+                    const double rdv = rd[ci] + v + lam[2 * i] - lam[2 * i + 1];
+                    rd[ci] = rdv;
+                    gs_l = nmax(gs_l, fabs(g));
+                    nrd_l = nmax(nrd_l, fabs(rdv));
+                }
+            }
+        }
+#pragma unroll
+        for (int r = 0; r < RX; ++r) {
+            if (ACT(r)) {
+                rp[r] = rowval(r, X, U, true) + t[r] - wv(r);
+                nrp_l = nmax(nrp_l, fabs(rp[r]));
+                mu_l += t[r] * lam[r];
+            } else {
+                rp[r] = 0.0;
+            }
+        }
+        const double mu = wave_sum(mu_l) / mact;
+        const double res = nmax(nmax(wave_max(nrd_l) / wave_max(gs_l), wave_max(nrs_l) / c.qs_max),
+                                wave_max(nrp_l) / scale_p);
+        kkt = nmax(res, mu);
+        STAMP(2);
+        const double merit = nmax(res, 1e4 * mu);
+        if (!isfinite(merit)) {
+            stop = kStopNonFinite;
+            break;
+        }
+        if (merit < best_m) {
+            best_m = merit;
+            best_kkt = kkt;
+            best_it = it;
+            for (int i = l; i < NP; i += 64) bU[i] = U[i];
+#pragma unroll
+            for (int j = 0; j < NS; ++j) bsg[j] = sg[j];
+        }
+        if (merit < c.tol) {
+            stop = kStopConverged;
+            break;
+        }
+        if (best_m < 1e3 * c.tol && it - best_it >= kStallIters) {
+            stop = kStopStalled;
+            break;
+        }
+
+        // ================= Newton matrix K = Gamma' W Gamma + Hc + diag =================
+#pragma unroll
+        for (int r = 0; r < RX; ++r) th[r] = ACT(r) ? lam[r] / t[r] : 0.0;
+#pragma unroll
+        for (int j = 0; j < NS; ++j) {
+            double v = Qs2[j];
+#pragma unroll
+            for (int r = 0; r < MC; ++r)
+                if (slk(r) == j) v += th[r];
+            Dsig[j] = v;
+        }
+        if (own) {
+            if (lo) {
+                // W_{k+1} = 2Q + sum_r th'_r c_r c_r' + sum_{pairs in a slack group} phi (a_r - a_r')(a_r - a_r')'
+                double thp[MC];
+#pragma unroll
+                for (int r = 0; r < MC; ++r) thp[r] = slk(r) < 0 ? th[r] : Qs2[slk(r)] * th[r] / Dsig[slk(r)];
+                const double* Ck = sC + k * MC * NX;
+                for (int s = 0; s < NX; ++s)
+                    for (int u = 0; u < NX; ++u) {
+                        double v = Q2[s * NX + u];
+#pragma unroll
+                        for (int r = 0; r < MC; ++r) v = fma(thp[r] * Ck[r * NX + s], Ck[r * NX + u], v);
+#pragma unroll
+                        for (int r = 0; r < MC; ++r) {
+                            if (slk(r) < 0) continue;
+#pragma unroll
+                            for (int r2 = r + 1; r2 < MC; ++r2) {
+                                if (slk(r2) != slk(r)) continue;
+                                const double phi = th[r] * th[r2] / Dsig[slk(r)];
+                                const double ds = sgn(r) * Ck[r * NX + s] - sgn(r2) * Ck[r2 * NX + s];
+                                const double du = sgn(r) * Ck[r * NX + u] - sgn(r2) * Ck[r2 * NX + u];
+                                v = fma(phi * ds, du, v);
+                            }
+                        }
+                        sW[(k * NX + s) * NX + u] = v;
+                    }
+            } else {
+#pragma unroll
+                for (int i = 0; i < NU; ++i) thin[k * NU + i] = th[2 * i] + th[2 * i + 1];
+            }
+        }
+        if constexpr (NXP > NX) {
+            // the MFMA K-groups read rows NX..NXP-1 of Gb / Yb (the Cholesky panel scratch
+            // aliases them): zero before every K build
+            for (int i = NX * NP + l; i < NXP * NP; i += 64) {
+                Gb[i] = 0.0;
+                Yb[i] = 0.0;
+            }
+        }
+        wsync();
+        STAMP(3);
+        // zero the accumulators with an MFMA so they are defined in the accumulator registers:
+        // a VALU zero made the tiles first touched in a late horizon segment live in VGPRs and
+        // cost a VGPR<->AGPR copy (and an MFMA-result stall) per stage
+        {
+            const v4d z4 = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+            for (int q = 0; q < NT; ++q) acc[q] = __builtin_amdgcn_mfma_f64_16x16x4f64(0.0, 0.0, z4, 0, 0, 0);
+        }
+        {
+            // lane l carries column l of Gamma_k (Gamma_0 = 0)
+            double g[NX];
+#pragma unroll
+            for (int s = 0; s < NX; ++s) g[s] = 0.0;
+            const int col = l;
+#pragma unroll
+            for (int tau = 0; tau < T; ++tau) {
+                // stages whose Gamma_{k+1} has tiles 0..tau nonzero (last column (k+1)NU-1 in tile tau)
+                const int kb = (16 * tau + NU) / NU - 1;
+                const int ke0 = (16 * (tau + 1) + NU) / NU - 1;
+                const int ke = ke0 < N ? ke0 : N;
+                for (int kk = kb; kk < ke; ++kk) {
+                    const double* Ak = sA + kk * NX * NX;
+                    const double* Bk = sB + kk * NX * NU;
+                    const double* Wk = sW + kk * NX * NX;
+                    const int jj = col - kk * NU;
+                    double gn[NX];
+#pragma unroll
+                    for (int s = 0; s < NX; ++s) {
+                        double v = 0.0;
+#pragma unroll
+                        for (int i = 0; i < NU; ++i) v = (jj == i) ? Bk[s * NU + i] : v;
+#pragma unroll
+                        for (int u = 0; u < NX; ++u) v = fma(Ak[s * NX + u], g[u], v);
+                        gn[s] = v;
+                    }
+#pragma unroll
+                    for (int s = 0; s < NX; ++s) g[s] = gn[s];
+                    if (col < NP) {
+#pragma unroll
+                        for (int s = 0; s < NX; ++s) {
+                            double y = 0.0;
+#pragma unroll
+                            for (int u = 0; u < NX; ++u) y = fma(Wk[s * NX + u], g[u], y);
+                            Gb[s * NP + col] = g[s];
+                            Yb[s * NP + col] = y;
+                        }
+                    }
+                    wsync();
+#pragma unroll
+                    for (int q = 0; q < NXP; q += 4) {
+                        const int row = q + (l >> 4);
+                        double af[T], bf[T];
+#pragma unroll
+                        for (int ti = 0; ti <= tau; ++ti) {
+                            af[ti] = Gb[row * NP + ti * 16 + (l & 15)];
+                            bf[ti] = Yb[row * NP + ti * 16 + (l & 15)];
+                        }
+#pragma unroll
+                        for (int ti = 0; ti <= tau; ++ti)
+#pragma unroll
+                            for (int tj = 0; tj <= ti; ++tj)
+                                acc[ti * (ti + 1) / 2 + tj] = __builtin_amdgcn_mfma_f64_16x16x4f64(
+                                    af[ti], bf[tj], acc[ti * (ti + 1) / 2 + tj], 0, 0, 0);
+                    }
+                    wsync();
+                }
+            }
+        }
+        STAMP(4);
+        // + 2R + 2D'dR D (block tridiagonal) + input-row curvature; identity on the padding
+#pragma unroll
+        for (int ti = 0; ti < T; ++ti)
+#pragma unroll
+            for (int tj = 0; tj <= ti; ++tj)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int row = ti * 16 + (l >> 4) + 4 * r, col = tj * 16 + (l & 15);
+                    double add = 0.0;
+                    if (row < n && col < n) {
+                        const int kr = row / NU, a = row - kr * NU, kc = col / NU, bq = col - kc * NU;
+                        if (kr == kc)
+                            add = R2[a * NU + bq] + dR2[a * NU + bq] * (kr + 1 < N ? 2.0 : 1.0) +
+                                  (row == col ? thin[row] : 0.0);
+                        else if (kr == kc + 1 || kc == kr + 1)
+                            add = -dR2[a * NU + bq];
+                    } else if (row == col) {
+                        add = 1.0;
+                    }
+                    acc[ti * (ti + 1) / 2 + tj][r] += add;
+                }
+        STAMP(5);
+
+        // ================= blocked Cholesky in the accumulator registers =================
+        bool chol_ok = true;
+#pragma unroll
+        for (int J = 0; J < T; ++J) {
+            const int JJ = J * (J + 1) / 2 + J;
+            double* S0 = Ld + J * 272;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) S0[((l >> 4) + 4 * r) * 17 + (l & 15)] = acc[JJ][r];
+            wsync();
+            // 16x16 diagonal factor: every row of 16 lanes holds the block (lane i: row i), pivots and
+            // L columns move by DPP row_newbcast; 1/sqrt by rsq + Newton
+            double rw[16];
+#pragma unroll
+            for (int cc = 0; cc < 16; ++cc) rw[cc] = S0[(l & 15) * 17 + cc];
+            {
+                const int i = l & 15;
+                static_for<0, 16>([&](auto jc) __attribute__((always_inline)) {
+                    constexpr int j = decltype(jc)::value;
+                    const double djj = bcast16<j>(rw[j]);
+                    if (!(djj > 0.0)) chol_ok = false;
+                    const double y = rsqrt_d(djj);
+                    const double lj = (i > j) ? rw[j] * y : ((i == j) ? djj * y : rw[j]);
+                    rw[j] = lj;
+                    static_for<j + 1, 16>([&](auto cc) __attribute__((always_inline)) {
+                        constexpr int c2 = decltype(cc)::value;
+                        rw[c2] = fma(-lj, bcast16<c2>(lj), rw[c2]);
+                    });
+                    __builtin_amdgcn_sched_barrier(0);  // keep the pivot steps' live ranges apart
+                });
+            }
+            if (l < 16) {
+#pragma unroll
+                for (int cc = 0; cc < 16; ++cc) S0[l * 17 + cc] = (cc <= l) ? rw[cc] : 0.0;
+            }
+            wsync();
+            STAMP(6);
+            if (J + 1 < T) {
+                // panel TRSM: L_IJ = K_IJ L_JJ^{-T}, one lane per stacked panel row, in LDS
+#pragma unroll
+                for (int I = J + 1; I < T; ++I)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r)
+                        SP[((I - J - 1) * 16 + (l >> 4) + 4 * r) * 17 + (l & 15)] = acc[I * (I + 1) / 2 + J][r];
+                wsync();
+                if (l < 16 * (T - 1 - J)) {
+                    double* yrow = SP + l * 17;
+#pragma unroll 1
+                    for (int cc = 0; cc < 16; ++cc) {
+                        double v = yrow[cc];
+                        for (int p = 0; p < cc; ++p) v = fma(-S0[cc * 17 + p], yrow[p], v);
+                        yrow[cc] = v / S0[cc * 17 + cc];
+                    }
+                }
+                wsync();
+#pragma unroll
+                for (int I = J + 1; I < T; ++I)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r)
+                        acc[I * (I + 1) / 2 + J][r] = SP[((I - J - 1) * 16 + (l >> 4) + 4 * r) * 17 + (l & 15)];
+                // trailing SYRK: K_IK -= L_IJ L_KJ'  (I >= K > J) on MFMA
+#pragma unroll
+                for (int q = 0; q < 16; q += 4) {
+                    double fr[T];
+#pragma unroll
+                    for (int I = J + 1; I < T; ++I) fr[I] = SP[((I - J - 1) * 16 + (l & 15)) * 17 + q + (l >> 4)];
+#pragma unroll
+                    for (int I = J + 1; I < T; ++I)
+#pragma unroll
+                        for (int K2 = J + 1; K2 <= I; ++K2)
+                            acc[I * (I + 1) / 2 + K2] =
+                                __builtin_amdgcn_mfma_f64_16x16x4f64(-fr[I], fr[K2], acc[I * (I + 1) / 2 + K2], 0, 0, 0);
+                }
+                wsync();
+            }
+            STAMP(7);
+        }
+        if (!chol_ok) {
+            stop = kStopBreakdown;
+            break;
+        }
+        // this lane's diagonal block (J = lane >> 4) row / column (l & 15) of L_JJ, and its inverse diagonal
+        const double* Lme = Ld + ((l >> 4) < T ? (l >> 4) : 0) * 272;
+        const double Ldinv = 1.0 / Lme[(l & 15) * 17 + (l & 15)];
+
+        // ================= predictor / corrector =================
+        double sig_c = 0.0, alpha = 0.0;
+        for (int pass = 0; pass < 2; ++pass) {
+            // pass 1: Mehrotra's second-order term dt_aff * dl_aff from the predictor still in (rho, gdu, dsg)
+#pragma unroll
+            for (int r = 0; r < RX; ++r) {
+                if (!ACT(r)) {
+                    rho[r] = 0.0;
+                    continue;
+                }
+                double rc = -t[r] * lam[r];
+                if (pass) {
+                    const double sd = (lo && slk(r) >= 0) ? sgn(r) * dsg[slk(r)] : 0.0;
+                    const double dta = -rp[r] - gdu[r] - sd;
+                    const double dla = rho[r] + th[r] * (gdu[r] + sd);
+                    rc += sig_c * mu - dta * dla;
+                }
+                rho[r] = (rc + lam[r] * rp[r]) / t[r];
+            }
+            // rho~ (stable slack-group form) of the stage rows enters only through C' rho~
+            if (lo && own) {
+                double ybv[NX];
+#pragma unroll
+                for (int s = 0; s < NX; ++s) ybv[s] = 0.0;
+#pragma unroll
+                for (int r = 0; r < MC; ++r) {
+                    double v = rho[r];
+                    if (slk(r) >= 0) {
+                        const int j = slk(r);
+                        v = Qs2[j] * rho[r] - th[r] * sgn(r) * rsig[j];
+#pragma unroll
+                        for (int r2 = 0; r2 < MC; ++r2) {
+                            if (r2 == r || slk(r2) != j) continue;
+                            v += th[r2] * rho[r] - th[r] * sgn(r) * sgn(r2) * rho[r2];
+                        }
+                        v /= Dsig[j];
+                    }
+#pragma unroll
+                    for (int s = 0; s < NX; ++s) ybv[s] = fma(v, sC[(k * MC + r) * NX + s], ybv[s]);
+                }
+#pragma unroll
+                for (int s = 0; s < NX; ++s) yb[(k + 1) * NX + s] = ybv[s];
+            }
+            if (l < NX) yb[l] = 0.0;
+            wsync();
+            STAMP(8);
+            adj3<NX, NU>(l, N, sA, sB, yb, yb, vb, vb);
+            wsync();
+            STAMP(9);
+            if (!lo && own) {
+#pragma unroll
+                for (int i = 0; i < NU; ++i) {
+                    const int ci = k * NU + i;
+                    vb[ci] = -rd[ci] - (vb[ci] + rho[2 * i] - rho[2 * i + 1]);
+                }
+            }
+            wsync();
+            // ---- forward solve L y = vb (block rows; L_JI tiles in acc, L_JJ in LDS) ----
+#pragma unroll
+            for (int J = 0; J < T; ++J) {
+                double pr4[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+                for (int I = 0; I < J; ++I) {
+                    const double yv = vb[I * 16 + (l & 15)];
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) pr4[r] = fma(acc[J * (J + 1) / 2 + I][r], yv, pr4[r]);
+                }
+                if (J > 0) {
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) pr4[r] = sum16(pr4[r]);
+                    if ((l & 15) == 0) {
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) red[(l >> 4) + 4 * r] = pr4[r];
+                    }
+                    wsync();
+                }
+                double rv = 0.0;
+                if ((l >> 4) == J) rv = vb[J * 16 + (l & 15)] - (J > 0 ? red[l & 15] : 0.0);
+                double Lr[16];
+#pragma unroll
+                for (int cc = 0; cc < 16; ++cc) Lr[cc] = Lme[(l & 15) * 17 + cc];
+                static_for<0, 16>([&](auto jc) __attribute__((always_inline)) {  // in-block substitution, row J broadcasts its lanes
+                    constexpr int cc = decltype(jc)::value;
+                    if ((l & 15) == cc) rv *= Ldinv;
+                    const double ycc = bcast16<cc>(rv);
+                    if ((l & 15) > cc) rv = fma(-Lr[cc], ycc, rv);
+                });
+                if ((l >> 4) == J) vb[J * 16 + (l & 15)] = rv;
+                wsync();
+            }
+            // ---- backward solve L' x = y ----
+#pragma unroll
+            for (int J = T - 1; J >= 0; --J) {
+                double p = 0.0;
+#pragma unroll
+                for (int I = J + 1; I < T; ++I)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r)
+                        p = fma(acc[I * (I + 1) / 2 + J][r], vb[I * 16 + (l >> 4) + 4 * r], p);
+                if (J + 1 < T) p = sum_groups(p);
+                double rv = ((l >> 4) == J) ? vb[J * 16 + (l & 15)] - p : 0.0;
+                double Lc[16];
+#pragma unroll
+                for (int cc = 0; cc < 16; ++cc) Lc[cc] = Lme[cc * 17 + (l & 15)];
+                static_for<0, 16>([&](auto jc) __attribute__((always_inline)) {
+                    constexpr int cc = 15 - decltype(jc)::value;
+                    if ((l & 15) == cc) rv *= Ldinv;
+                    const double xcc = bcast16<cc>(rv);
+                    if ((l & 15) < cc) rv = fma(-Lc[cc], xcc, rv);
+                });
+                if ((l >> 4) == J) vb[J * 16 + (l & 15)] = rv;
+                wsync();
+            }
+            for (int i = l; i < NP; i += 64) dU[i] = (i < n) ? vb[i] : 0.0;
+            wsync();
+            STAMP(10);
+            fwd3<NX, NU>(l, N, sA, sB, nullptr, dU, dX);
+            wsync();
+            STAMP(11);
+#pragma unroll
+            for (int r = 0; r < RX; ++r) gdu[r] = ACT(r) ? rowval(r, dX, dU, false) : 0.0;
+#pragma unroll
+            for (int j = 0; j < NS; ++j) {
+                double v = rsig[j];
+#pragma unroll
+                for (int r = 0; r < MC; ++r)
+                    if (slk(r) == j) v += sgn(r) * (rho[r] + th[r] * gdu[r]);
+                dsg[j] = (lo && own) ? -v / Dsig[j] : 0.0;
+            }
+            // dt_r = -rp - G dU - s dsig ;  dl_r = rho + th (G dU + s dsig)
+            auto sdr = [&](int r) -> double { return (lo && slk(r) >= 0) ? sgn(r) * dsg[slk(r)] : 0.0; };
+            double amax_l = 1.0e300;
+#pragma unroll
+            for (int r = 0; r < RX; ++r) {
+                if (!ACT(r)) continue;
+                const double sd = sdr(r);
+                const double dtv = -rp[r] - gdu[r] - sd;
+                const double dlv = rho[r] + th[r] * (gdu[r] + sd);
+                if (dtv < 0.0) amax_l = fmin(amax_l, -t[r] / dtv);
+                if (dlv < 0.0) amax_l = fmin(amax_l, -lam[r] / dlv);
+            }
+            const double amax = wave_min(amax_l);
+            if (!pass) {
+                const double a = fmin(amax, 1.0);
+                double mua_l = 0.0;
+#pragma unroll
+                for (int r = 0; r < RX; ++r) {
+                    if (!ACT(r)) continue;
+                    const double sd = sdr(r);
+                    mua_l += (t[r] + a * (-rp[r] - gdu[r] - sd)) * (lam[r] + a * (rho[r] + th[r] * (gdu[r] + sd)));
+                }
+                const double mu_aff = wave_sum(mua_l) / mact;
+                const double ratio = mu > 0.0 ? mu_aff / mu : 0.0;
+                sig_c = ratio * ratio * ratio;
+                STAMP(12);
+            } else {
+                alpha = fmin(1.0, 0.995 * amax);
+                // stay in the wide neighbourhood t_r lam_r >= gamma mu(alpha) (see kNbhdGamma)
+                for (int bt = 0; bt < kMaxBacktrack; ++bt) {
+                    double mn_l = 0.0, pm_l = INFINITY;
+#pragma unroll
+                    for (int r = 0; r < RX; ++r)
+                        if (ACT(r)) {
+                            const double sd = sdr(r);
+                            const double pr = (t[r] + alpha * (-rp[r] - gdu[r] - sd)) *
+                                              (lam[r] + alpha * (rho[r] + th[r] * (gdu[r] + sd)));
+                            mn_l += pr;
+                            pm_l = fmin(pm_l, pr);
+                        }
+                    if (wave_min(pm_l) >= kNbhdGamma * (wave_sum(mn_l) / mact)) break;
+                    alpha *= 0.8;
+                }
+#pragma unroll
+                for (int r = 0; r < RX; ++r)
+                    if (ACT(r)) {
+                        const double sd = sdr(r);
+                        t[r] = fma(alpha, -rp[r] - gdu[r] - sd, t[r]);
+                        lam[r] = fma(alpha, rho[r] + th[r] * (gdu[r] + sd), lam[r]);
+                    }
+#pragma unroll
+                for (int j = 0; j < NS; ++j) sg[j] = fma(alpha, dsg[j], sg[j]);
+                STAMP(12);
+            }
+        }
+        for (int i = l; i < n; i += 64) U[i] = fma(alpha, dU[i], U[i]);
+        for (int i = l; i < (N + 1) * NX; i += 64) X[i] = fma(alpha, dX[i], X[i]);
+        wsync();
+        STAMP(13);
+    }
+    if (it > c.max_iter) it = c.max_iter;
+    wsync();
+    int status = CMPC_SOLVED;
+    if (stop != kStopConverged) {
+        if (best_it > 0) {  // restore the best iterate
+            for (int i = l; i < NP; i += 64) U[i] = bU[i];
+#pragma unroll
+            for (int j = 0; j < NS; ++j) sg[j] = bsg[j];
+            kkt = best_kkt;
+        }
+        status = stop_status(stop, best_m, c.tol);
+    }
+    wsync();
+
+    // ---- output in the reference layout ----
+    fwd3<NX, NU>(l, N, sA, sB, sx0, U, X);
+    wsync();
+    constexpr int NXE = NX + NS;
+    const size_t nz = (size_t)NXE * (N + 1) + 2 * (size_t)n;
+    double* z = P.z + (size_t)b * nz;
+    for (int i = l; i < (N + 1) * NX; i += 64) {
+        const int kk = i / NX, s = i - kk * NX;
+        z[kk * NXE + s] = X[i];
+    }
+    if (l < NS) z[NX + l] = 0.0;
+    if (lo && own) {
+#pragma unroll
+        for (int j = 0; j < NS; ++j) z[(k + 1) * NXE + NX + j] = sg[j];
+    }
+    for (int i = l; i < n; i += 64) {
+        const int kk = i / NU, j = i - kk * NU;
+        z[(size_t)(N + 1) * NXE + i] = U[i];
+        z[(size_t)(N + 1) * NXE + n + i] = U[i] - (kk ? U[(kk - 1) * NU + j] : sup[j]);
+    }
+    if (l == 0) {
+        if (P.kkt) P.kkt[b] = kkt;
+        if (P.iters) P.iters[b] = it;
+        if (P.status) P.status[b] = status;
+        if (stamp) {
+            unsigned long long* st = P.stamps + (size_t)b * kStampSlots;
+            for (int i = 0; i < kStampSlots - 1; ++i) st[i] = tsum[i];
+            st[kStampSlots - 1] = it;
+        }
+    }
+#undef STAMP
+#undef ACT
+}
+
+template <int T, int NX, int NU, int NB>
+static hipError_t launch3(const MpcConst& c, const MpcPtrs& p, int batch, hipStream_t s) {
+    const size_t lds = sizeof(double) * (size_t)lds3_layout<T, NX, NU, NB>(c.N).total;
+    hipError_t e = hipFuncSetAttribute((const void*)mpc_ipm3_kernel<T, NX, NU, NB>,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL((mpc_ipm3_kernel<T, NX, NU, NB>), dim3(batch), dim3(64), lds, s, c, p);
+    return hipGetLastError();
+}
+
+template <int NX, int NU, int NB>
+static hipError_t launch3_t(const MpcConst& c, const MpcPtrs& p, int batch, hipStream_t s) {
+    switch (c.npad / 16) {
+        case 1: return launch3<1, NX, NU, NB>(c, p, batch, s);
+        case 2: return launch3<2, NX, NU, NB>(c, p, batch, s);
+        case 3: return launch3<3, NX, NU, NB>(c, p, batch, s);
+        default: return launch3<4, NX, NU, NB>(c, p, batch, s);
+    }
+}
+
+// This file is compiled once per instantiation set (CMPC_V3_SET = 1, 2, 3; see the Makefile) so
+// the instantiations build in parallel.  Set 1 also holds the dispatcher.
+#ifndef CMPC_V3_SET
+#define CMPC_V3_SET 1
+#endif
+#define CASE(NX_, NU_, NB_)                                 \
+    if (c.nx == NX_ && c.nu == NU_ && nb == NB_) {          \
+        *err = launch3_t<NX_, NU_, NB_>(c, p, batch, s);    \
+        return true;                                        \
+    }
+#if CMPC_V3_SET == 1
+bool mpc3_try_set2(const MpcConst& c, const MpcPtrs& p, int batch, hipStream_t s, hipError_t* err, int nb);
+bool mpc3_try_set3(const MpcConst& c, const MpcPtrs& p, int batch, hipStream_t s, hipError_t* err, int nb);
+
+// Returns true (and launches) when a v3 instantiation covers the problem: PlannerLPV row
+// pattern with nb <= 2 neighbour rows, N <= 32, N*nu <= 64; (nx, nu) in {(4,2), (9,2), (6,3)}.
+bool mpc3_try_launch(const MpcConst& c, const MpcPtrs& p, int batch, hipStream_t s, hipError_t* err) {
+    if (c.ns != 3 || c.N > 32 || c.mc < 4 || c.n > 64) return false;
+    for (int r = 0; r < c.mc; ++r)
+        if (c.row_slack[r] != slk(r) || c.row_sign[r] != (int)sgn(r)) return false;
+    const int nb = c.mc - 4;
+    CASE(4, 2, 2)
+    CASE(4, 2, 1)
+    CASE(4, 2, 0)
+    return mpc3_try_set2(c, p, batch, s, err, nb) || mpc3_try_set3(c, p, batch, s, err, nb);
+}
+#elif CMPC_V3_SET == 2
+bool mpc3_try_set2(const MpcConst& c, const MpcPtrs& p, int batch, hipStream_t s, hipError_t* err, int nb) {
+    CASE(9, 2, 2)
+    CASE(9, 2, 1)
+    CASE(9, 2, 0)
+    return false;
+}
+#else
+bool mpc3_try_set3(const MpcConst& c, const MpcPtrs& p, int batch, hipStream_t s, hipError_t* err, int nb) {
+    CASE(6, 3, 2)
+    return false;
+}
+#endif
+#undef CASE
+
+}  // namespace cmpc

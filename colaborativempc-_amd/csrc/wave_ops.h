@@ -2,6 +2,8 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <type_traits>
+
 namespace cmpc {
 
 typedef double v4d __attribute__((ext_vector_type(4)));
@@ -48,5 +50,30 @@ __device__ __forceinline__ double sum_groups(double v) {
 }
 
 __device__ __forceinline__ unsigned long long clock64_() { return __builtin_amdgcn_s_memtime(); }
+
+// Compile-time loop: f(std::integral_constant<int, I>) for I in [B, E).
+template <int B, int E, class F>
+__device__ __forceinline__ void static_for(F&& f) {
+    if constexpr (B < E) {
+        f(std::integral_constant<int, B>{});
+        static_for<B + 1, E>(f);
+    }
+}
+
+// Lane J of each row of 16 lanes, broadcast to the whole row: one v_mov_b64_dpp row_newbcast:J
+// (no SGPR round trip, unlike v_readlane).
+template <int J>
+__device__ __forceinline__ double bcast16(double x) {
+    static_assert(J >= 0 && J < 16, "row_newbcast lane");
+    return __builtin_amdgcn_update_dpp(x, x, 0x150 + J, 0xF, 0xF, false);
+}
+
+// 1/sqrt(x) to full double precision: hardware estimate + two Newton steps.
+__device__ __forceinline__ double rsqrt_d(double x) {
+    double y = __builtin_amdgcn_rsq(x);
+    y = y * fma(-0.5 * x, y * y, 1.5);
+    y = y * fma(-0.5 * x, y * y, 1.5);
+    return y;
+}
 
 }  // namespace cmpc

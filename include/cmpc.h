@@ -73,7 +73,7 @@ typedef struct {
     double tol;    /* relative stationarity/feasibility tolerance (complementarity: 1e-4*tol); <= 0 selects 1e-9 */
     int max_iter;  /* interior-point iteration cap; <= 0 selects 60 */
     int flags;     /* CMPC_FLAG_* */
-    void* stamps;  /* optional DEVICE buffer, batch x 8 uint64: per-phase shader-clock counts of the
+    void* stamps;  /* optional DEVICE buffer, batch x 16 uint64: per-section shader-clock counts of the
                       specialised kernel (diagnostic; NULL in production) */
 } cmpc_opts;
 

@@ -1,6 +1,5 @@
-"""Diagnostic: per-phase shader-clock breakdown of the specialised solver kernel
-(cfg3 round 0 problem).  Usage: python tools/stamps.py [agents] [N]"""
-import ctypes as ct
+"""Diagnostic: per-section shader-clock breakdown of the v3 solver kernel (cfg3 round-0
+problem).  Usage: python tools/stamps.py [agents] [N]"""
 import os
 import sys
 
@@ -11,17 +10,21 @@ sys.path.insert(0, os.path.join(ROOT, "colaborativempc-_amd"))
 sys.path.insert(0, ROOT)
 import torch  # noqa: E402
 
-import cmpc  # noqa: E402
 from cmpc import _lib as L  # noqa: E402
 from cmpc import scenarios as S  # noqa: E402
 from cmpc.rounds import DIRounds  # noqa: E402
 
+SLOTS = 16
+NAMES = {14: "setup", 0: "residual: Q X, C'lam", 1: "residual: 2 adjoints", 2: "residual: rows, norms",
+         3: "W_k build", 4: "K: Gamma rec + MFMA", 5: "K: diag adds", 6: "chol: 16x16 factors",
+         7: "chol: panel + SYRK", 8: "solve: rho, C'rho", 9: "solve: adjoint", 10: "solve: tri-solves",
+         11: "solve: fwd sim", 12: "solve: rows, step", 13: "update"}
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 1024
 N = int(sys.argv[2]) if len(sys.argv) > 2 else 30
 sc = S.make_di(n, N, 2, 2)
 R = DIRounds(sc)
 R.build()
-st = torch.zeros((n, 8), dtype=torch.int64, device="cuda")
+st = torch.zeros((n, SLOTS), dtype=torch.int64, device="cuda")
 R.opts = L.opts(stamps=st.data_ptr())
 for _ in range(3):
     R.solve()
@@ -32,16 +35,17 @@ R.solve()
 ev[1].record()
 torch.cuda.synchronize()
 a = st.cpu().numpy().astype(np.float64)
-names = ["setup+residuals", "W+K build", "cholesky", "predictor", "corrector", "update"]
-it = a[:, 6]
-tot = a[:, :6].sum(1)
-print(f"agents {n} N {N}: kernel {ev[0].elapsed_time(ev[1]):.3f} ms (with stamps); iters mean {it.mean():.2f} max {it.max():.0f}")
-for i, nm in enumerate(names):
-    print(f"  {nm:16s} {a[:, i].mean() / it.mean():10.0f} clk/iter   {100 * a[:, i].sum() / tot.sum():5.1f} %")
-print(f"  total            {tot.mean() / it.mean():10.0f} clk/iter ; slowest agent {tot.max():.0f} clk")
+it = a[:, SLOTS - 1]
+tot = a[:, :SLOTS - 1].sum(1)
+print(f"agents {n} N {N}: kernel {ev[0].elapsed_time(ev[1]):.3f} ms (with stamps); iters mean {it.mean():.2f} "
+      f"max {it.max():.0f}")
+for i in sorted(NAMES, key=lambda i: (i != 14, i)):
+    print(f"  {NAMES[i]:24s} {a[:, i].mean() / it.mean():10.0f} clk/iter   {100 * a[:, i].sum() / tot.sum():5.1f} %")
+print(f"  total                    {tot.mean() / it.mean():10.0f} clk/iter ; slowest agent {tot.max():.0f} clk")
 R.opts = L.opts()
 ev[0].record()
 R.solve()
 ev[1].record()
 torch.cuda.synchronize()
-print(f"kernel without stamps {ev[0].elapsed_time(ev[1]):.3f} ms; status {np.unique(R.status.cpu().numpy(), return_counts=True)}")
+print(f"kernel without stamps {ev[0].elapsed_time(ev[1]):.3f} ms; status "
+      f"{dict(zip(*np.unique(R.status.cpu().numpy(), return_counts=True)))}")
