@@ -92,6 +92,26 @@ class cmpc_di_dims(ct.Structure):
     _fields_ = [(k, ct.c_int) for k in ("batch", "N", "nb", "self_offset")]
 
 
+class cmpc_qp_dims(ct.Structure):
+    _fields_ = [(k, ct.c_int) for k in ("n", "m_ineq", "m_eq", "batch", "col_major")]
+
+
+class cmpc_qp_data(ct.Structure):
+    _fields_ = [(k, _DP) for k in ("H", "f", "A", "b", "Aeq", "beq", "lb", "ub")]
+
+
+class cmpc_qp_out(ct.Structure):
+    _fields_ = [("x", _DP), ("fval", _DP), ("exitflag", _IP), ("iters", _IP), ("lambda_ineqlin", _DP),
+                ("lambda_eqlin", _DP), ("lambda_lower", _DP), ("lambda_upper", _DP), ("residual", _DP)]
+
+
+CMPC_QP_CONVERGED = 1
+CMPC_QP_MAXITER = 0
+CMPC_QP_INFEASIBLE = -2
+CMPC_QP_UNBOUNDED = -3
+CMPC_QP_NONCONVEX = -6
+
+
 class CmpcError(RuntimeError):
     def __init__(self, code, msg=""):
         super().__init__(f"libcmpc error {code}: {msg}")
@@ -121,6 +141,8 @@ SIGNATURES = {
                                      _IP, _DP, _DP, _DP, _DP, _DP, ct.c_void_p]),
     "cmpc_di_advance_dev": (ct.c_int, [ct.c_void_p, ct.POINTER(cmpc_di_params), ct.POINTER(cmpc_di_dims),
                                        _DP, _DP, _DP, _DP, ct.c_void_p]),
+    "cmpc_solve_qp_batch": (ct.c_int, [ct.c_void_p, ct.POINTER(cmpc_qp_dims), ct.POINTER(cmpc_qp_data),
+                                       ct.POINTER(cmpc_qp_out), ct.POINTER(cmpc_opts)]),
     "cmpc_selftest_mfma": (ct.c_int, [ct.c_void_p, _DP, _DP, _DP]),
 }
 

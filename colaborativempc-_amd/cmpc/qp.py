@@ -1,0 +1,114 @@
+"""Dense standard-form QP batch with MATLAB ``quadprog`` semantics on the GPU
+(``cmpc_solve_qp_batch``, include/cmpc.h), and the ``osqp_solve_qp`` adapter.
+
+* ``quadprog(H, f, A, b, Aeq, beq, lb, ub)`` — the call YALMIP makes
+  (Matlab-tests/yalmip/yalmip/YALMIP-master/solvers/callquadprog.m:63-69); the MEX
+  gateway (mex/cmpc_quadprog_mex.c) binds the same C entry point.
+* ``osqp_solve_qp(P, q, G, h, A, b, initvals)`` — same signature, return value
+  ``(res, feasible)`` and status rule as the reference's wrapper
+  (planner/lib/plan_lib/distributedPlanner/LPV_Planner.py:192-249): ``res.x``,
+  ``res.info.status_val`` / ``res.info.status`` with OSQP's codes, and
+  ``feasible = status_val in {1, 2, -2}``.
+
+Both accept one problem or a batch (leading batch axis on every array).
+"""
+from __future__ import annotations
+
+import ctypes as ct
+from types import SimpleNamespace
+
+import numpy as np
+
+from . import _lib as L
+
+# quadprog exitflag -> OSQP status_val / status text (the reference prints the text on failure)
+_OSQP_OF_FLAG = {L.CMPC_QP_CONVERGED: (1, "solved"), L.CMPC_QP_MAXITER: (-2, "maximum iterations reached"),
+                 L.CMPC_QP_INFEASIBLE: (-3, "primal infeasible"), L.CMPC_QP_UNBOUNDED: (-4, "dual infeasible"),
+                 L.CMPC_QP_NONCONVEX: (-7, "problem non convex")}
+
+
+def _dense(a):
+    if a is None:
+        return None
+    if hasattr(a, "toarray"):
+        a = a.toarray()
+    return np.asarray(a, dtype=np.float64)
+
+
+def quadprog(H, f, A=None, b=None, Aeq=None, beq=None, lb=None, ub=None, ctx=None, tol=None, max_iter=None):
+    """Solve min 1/2 x'Hx + f'x s.t. A x <= b, Aeq x = beq, lb <= x <= ub on the GPU.
+
+    Single problem: H (n,n), f (n,) ...; batch: a leading axis on every given array.
+    Returns dict(x, fval, exitflag, iterations, lambda=dict(ineqlin, eqlin, lower, upper), residual)."""
+    H = _dense(H)
+    single = H.ndim == 2
+    if single:
+        H = H[None]
+    B, n = H.shape[0], H.shape[1]
+
+    def prep(a, shape_tail, name):
+        if a is None:
+            return None
+        a = _dense(a)
+        if a.size == 0:
+            return None
+        a = a[None] if single else a
+        a = np.ascontiguousarray(a.reshape((B,) + shape_tail))
+        return a
+
+    f = prep(f, (n,), "f")
+    if f is None:
+        raise ValueError("f is required")
+    A_ = None if A is None or np.size(A) == 0 else _dense(A)
+    mi = 0 if A_ is None else A_.shape[-2]
+    Aeq_ = None if Aeq is None or np.size(Aeq) == 0 else _dense(Aeq)
+    me = 0 if Aeq_ is None else Aeq_.shape[-2]
+    A_ = prep(A_, (mi, n), "A")
+    b_ = prep(b, (mi,), "b") if mi else None
+    E_ = prep(Aeq_, (me, n), "Aeq")
+    e_ = prep(beq, (me,), "beq") if me else None
+    lb_ = prep(lb, (n,), "lb")
+    ub_ = prep(ub, (n,), "ub")
+    ctx = ctx or L.default_context()
+    keep = [np.ascontiguousarray(H), f, A_, b_, E_, e_, lb_, ub_]
+    data = L.cmpc_qp_data(*[L.dptr(a) for a in keep])
+    x = np.zeros((B, n))
+    fval = np.zeros(B)
+    flag = np.zeros(B, np.int32)
+    it = np.zeros(B, np.int32)
+    li = np.zeros((B, mi))
+    le = np.zeros((B, me))
+    llo = np.zeros((B, n))
+    lup = np.zeros((B, n))
+    resid = np.zeros(B)
+    out = L.cmpc_qp_out(L.dptr(x), L.dptr(fval), L.iptr(flag), L.iptr(it), L.dptr(li) if mi else None,
+                        L.dptr(le) if me else None, L.dptr(llo), L.dptr(lup), L.dptr(resid))
+    dims = L.cmpc_qp_dims(n, mi, me, B, 0)
+    ctx.check(ctx.lib.cmpc_solve_qp_batch(ctx.h, ct.byref(dims), ct.byref(data), ct.byref(out),
+                                          ct.byref(L.opts(tol, max_iter))))
+    del keep
+    res = dict(x=x, fval=fval, exitflag=flag, iterations=it, residual=resid,
+               **{"lambda": dict(ineqlin=li, eqlin=le, lower=llo, upper=lup)})
+    if single:
+        res = {k: (v[0] if not isinstance(v, dict) else {kk: vv[0] for kk, vv in v.items()}) for k, v in res.items()}
+    return res
+
+
+def osqp_solve_qp(P, q, G=None, h=None, A=None, b=None, initvals=None, ctx=None):
+    """Drop-in for the reference's ``osqp_solve_qp`` (LPV_Planner.py:192-249): the same QP
+    (min 1/2 x'Px + q'x s.t. G x <= h, A x = b) solved on the GPU.  ``initvals`` is accepted
+    and ignored, as in the reference (it never warm-starts OSQP).  Returns (res, feasible)."""
+    r = quadprog(P, q, G, h, A, b, ctx=ctx)
+    flags = np.atleast_1d(r["exitflag"])
+    out = []
+    for i, fl in enumerate(flags):
+        sv, text = _OSQP_OF_FLAG.get(int(fl), (-10, "unsolved"))
+        x = np.atleast_2d(r["x"])[i]
+        res = SimpleNamespace(x=x, y=None, info=SimpleNamespace(status_val=sv, status=text,
+                                                                   iter=int(np.atleast_1d(r["iterations"])[i]),
+                                                                   obj_val=float(np.atleast_1d(r["fval"])[i])))
+        feasible = 1 if sv in (1, 2, -2) else 0   # LPV_Planner.py:243-249
+        if sv != 1:
+            print("OSQP exited with status '%s'" % text)
+        out.append((res, feasible))
+    return out[0] if np.ndim(r["exitflag"]) == 0 else out

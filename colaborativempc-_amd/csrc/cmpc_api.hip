@@ -319,6 +319,61 @@ int cmpc_di_advance_dev(cmpc_ctx* ctx, const cmpc_di_params* prm, const cmpc_di_
     return CMPC_OK;
 }
 
+int cmpc_solve_qp_batch(cmpc_ctx* ctx, const cmpc_qp_dims* d, const cmpc_qp_data* in, const cmpc_qp_out* out,
+                        const cmpc_opts* opts) {
+    if (!ctx) return CMPC_ERR_ARG;
+    if (!d || !in || !out || !out->x) return fail(ctx, CMPC_ERR_ARG, "null argument");
+    if (d->n < 1 || d->m_ineq < 0 || d->m_eq < 0 || d->batch < 0)
+        return fail(ctx, CMPC_ERR_ARG, "bad QP dimensions");
+    if (!in->H || !in->f) return fail(ctx, CMPC_ERR_ARG, "H and f are required");
+    if (d->m_ineq > 0 && (!in->A || !in->b)) return fail(ctx, CMPC_ERR_ARG, "m_ineq > 0 needs A and b");
+    if (d->m_eq > 0 && (!in->Aeq || !in->beq)) return fail(ctx, CMPC_ERR_ARG, "m_eq > 0 needs Aeq and beq");
+    if ((double)(d->n + d->m_eq) * (d->n + d->m_eq) > 2.0e8) return fail(ctx, CMPC_ERR_UNSUPPORTED, "QP too large");
+    int rc = set_device(ctx);
+    if (rc != CMPC_OK) return rc;
+    if (d->batch == 0) return CMPC_OK;
+    const size_t B = d->batch, n = d->n, mi = d->m_ineq, me = d->m_eq;
+    const size_t sH = B * n * n, sf = B * n, sA = B * mi * n, sb = B * mi, sE = B * me * n, se = B * me,
+                 sl = in->lb ? B * n : 0, su = in->ub ? B * n : 0, ws = B * cmpc::qp_ws_doubles(d->n, d->m_ineq, d->m_eq);
+    const size_t bytes = 8 * (sH + sf + sA + sb + sE + se + sl + su + ws + B * n + B * mi + B * me + 2 * B * n + 2 * B) +
+                         8 * B + 24 * 256;
+    char* base = arena(ctx, bytes);
+    if (!base) return fail(ctx, CMPC_ERR_NOMEM, "device arena allocation failed");
+    Carve cv{base};
+    double *dH = cv.take<double>(sH), *df = cv.take<double>(sf), *dA = mi ? cv.take<double>(sA) : nullptr,
+           *db = mi ? cv.take<double>(sb) : nullptr, *dE = me ? cv.take<double>(sE) : nullptr,
+           *de = me ? cv.take<double>(se) : nullptr, *dl = sl ? cv.take<double>(sl) : nullptr,
+           *du = su ? cv.take<double>(su) : nullptr, *dws = cv.take<double>(ws), *dx = cv.take<double>(B * n),
+           *dli = cv.take<double>(B * mi + 1), *dle = cv.take<double>(B * me + 1), *dlo = cv.take<double>(B * n),
+           *dup = cv.take<double>(B * n), *dfv = cv.take<double>(B), *dmr = cv.take<double>(B);
+    int *dfl = cv.take<int>(B), *dit = cv.take<int>(B);
+    hipStream_t s = ctx->stream;
+    HIP_TRY(hipMemcpyAsync(dH, in->H, 8 * sH, hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemcpyAsync(df, in->f, 8 * sf, hipMemcpyHostToDevice, s));
+    if (mi) HIP_TRY(hipMemcpyAsync(dA, in->A, 8 * sA, hipMemcpyHostToDevice, s));
+    if (mi) HIP_TRY(hipMemcpyAsync(db, in->b, 8 * sb, hipMemcpyHostToDevice, s));
+    if (me) HIP_TRY(hipMemcpyAsync(dE, in->Aeq, 8 * sE, hipMemcpyHostToDevice, s));
+    if (me) HIP_TRY(hipMemcpyAsync(de, in->beq, 8 * se, hipMemcpyHostToDevice, s));
+    if (sl) HIP_TRY(hipMemcpyAsync(dl, in->lb, 8 * sl, hipMemcpyHostToDevice, s));
+    if (su) HIP_TRY(hipMemcpyAsync(du, in->ub, 8 * su, hipMemcpyHostToDevice, s));
+    cmpc::QpConst qc{d->n, d->m_ineq, d->m_eq, d->col_major ? 1 : 0,
+                     (opts && opts->max_iter > 0) ? opts->max_iter : 100, 8,
+                     (opts && opts->tol > 0) ? opts->tol : 1e-9, 1e-8};
+    cmpc::QpPtrs qp{dH, df, dA, db, dE, de, dl, du, dx, dfv, dli, dle, dlo, dup, dmr, dfl, dit, dws};
+    HIP_TRY(cmpc::qp_launch(qc, qp, d->batch, s));
+    HIP_TRY(hipMemcpyAsync(out->x, dx, 8 * B * n, hipMemcpyDeviceToHost, s));
+    if (out->fval) HIP_TRY(hipMemcpyAsync(out->fval, dfv, 8 * B, hipMemcpyDeviceToHost, s));
+    if (out->exitflag) HIP_TRY(hipMemcpyAsync(out->exitflag, dfl, 4 * B, hipMemcpyDeviceToHost, s));
+    if (out->iters) HIP_TRY(hipMemcpyAsync(out->iters, dit, 4 * B, hipMemcpyDeviceToHost, s));
+    if (out->residual) HIP_TRY(hipMemcpyAsync(out->residual, dmr, 8 * B, hipMemcpyDeviceToHost, s));
+    if (out->lambda_ineqlin && mi) HIP_TRY(hipMemcpyAsync(out->lambda_ineqlin, dli, 8 * B * mi, hipMemcpyDeviceToHost, s));
+    if (out->lambda_eqlin && me) HIP_TRY(hipMemcpyAsync(out->lambda_eqlin, dle, 8 * B * me, hipMemcpyDeviceToHost, s));
+    if (out->lambda_lower) HIP_TRY(hipMemcpyAsync(out->lambda_lower, dlo, 8 * B * n, hipMemcpyDeviceToHost, s));
+    if (out->lambda_upper) HIP_TRY(hipMemcpyAsync(out->lambda_upper, dup, 8 * B * n, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    return CMPC_OK;
+}
+
 int cmpc_selftest_mfma(cmpc_ctx* ctx, const double* A, const double* B, double* D) {
     if (!ctx || !A || !B || !D) return CMPC_ERR_ARG;
     int rc = set_device(ctx);

@@ -127,4 +127,22 @@ hipError_t di_advance_launch(const DiConst& c, const double* z, double* x0, doub
 
 hipError_t selftest_mfma_launch(const double* A, const double* B, double* D, hipStream_t s);
 
+// Dense standard-form QP batch (quadprog semantics), qp_dense.hip.
+struct QpConst {
+    int n, mi, me;   // variables, general inequality rows, equality rows
+    int col_major;   // matrices A, Aeq given column-major (MATLAB)
+    int max_iter, refine;
+    double tol, reg; // tolerance; quasi-definite regularisation rho = delta
+};
+
+struct QpPtrs {
+    const double *H, *f, *A, *b, *Aeq, *beq, *lb, *ub;  // batch-major; A/b, Aeq/beq, lb, ub may be null
+    double *x, *fval, *lam_ineq, *lam_eq, *lam_lo, *lam_up, *merit;
+    int *exitflag, *iters;
+    double* ws;  // batch x qp_ws_doubles
+};
+
+size_t qp_ws_doubles(int n, int mi, int me);
+hipError_t qp_launch(const QpConst& c, const QpPtrs& p, int batch, hipStream_t s);
+
 }  // namespace cmpc

@@ -225,6 +225,50 @@ int cmpc_di_advance_dev(cmpc_ctx* ctx, const cmpc_di_params* prm, const cmpc_di_
                         double* u_prev /* batch x nu */, double* traj_local /* batch x (N+1) x 2 */,
                         void* hip_stream);
 
+/* ------------------------------------------------------------------------
+ * Dense standard-form QP batch with MATLAB quadprog semantics (the MEX drop-in
+ * for quadprog(H,f,A,b,Aeq,beq,lb,ub) as YALMIP calls it, callquadprog.m:63-69,
+ * and the generic back end of the osqp_solve_qp adapter, LPV_Planner.py:192-249):
+ *
+ *   min 1/2 x'Hx + f'x   s.t.  A x <= b,  Aeq x = beq,  lb <= x <= ub
+ *
+ * HOST pointers, batch-major (problem p's block contiguous).  H n x n (its symmetric
+ * part is used), A m_ineq x n, Aeq m_eq x n, row-major unless col_major (MATLAB
+ * layout).  A/b, Aeq/beq, lb, ub may be NULL (absent); +-inf bounds are inactive;
+ * all-zero constraint rows are dropped (or make the problem infeasible).
+ * exitflag: CMPC_QP_CONVERGED 1, CMPC_QP_MAXITER 0, CMPC_QP_INFEASIBLE -2,
+ * CMPC_QP_UNBOUNDED -3, CMPC_QP_NONCONVEX -6 (quadprog's codes).
+ * ---------------------------------------------------------------------- */
+#define CMPC_QP_CONVERGED 1
+#define CMPC_QP_MAXITER 0
+#define CMPC_QP_INFEASIBLE (-2)
+#define CMPC_QP_UNBOUNDED (-3)
+#define CMPC_QP_NONCONVEX (-6)
+
+typedef struct {
+    int n, m_ineq, m_eq, batch;
+    int col_major;
+} cmpc_qp_dims;
+
+typedef struct {
+    const double *H, *f, *A, *b, *Aeq, *beq, *lb, *ub;
+} cmpc_qp_data;
+
+typedef struct {
+    double* x;               /* batch x n */
+    double* fval;            /* batch (may be NULL) */
+    int* exitflag;           /* batch (may be NULL) */
+    int* iters;              /* batch (may be NULL) */
+    double* lambda_ineqlin;  /* batch x m_ineq (may be NULL) */
+    double* lambda_eqlin;    /* batch x m_eq (may be NULL) */
+    double* lambda_lower;    /* batch x n (may be NULL) */
+    double* lambda_upper;    /* batch x n (may be NULL) */
+    double* residual;        /* batch: final scaled KKT merit (may be NULL) */
+} cmpc_qp_out;
+
+int cmpc_solve_qp_batch(cmpc_ctx* ctx, const cmpc_qp_dims* dims, const cmpc_qp_data* host_in,
+                        const cmpc_qp_out* host_out, const cmpc_opts* opts);
+
 /* Device self-test of the f64 MFMA fragment mapping used by the solver
  * (D = A*B for one 16x16x4 tile, A,B host 16x4 / 4x16 row-major, D host 16x16). */
 int cmpc_selftest_mfma(cmpc_ctx* ctx, const double* A, const double* B, double* D);

@@ -1,0 +1,78 @@
+"""TEST INFRASTRUCTURE: drive the MEX gateway (colaborativempc-_amd/mex/cmpc_quadprog_mex.c)
+through the mock mex.h build (libcmpc_mex_mock.so) — MATLAB is not available here."""
+import ctypes as ct
+import os
+
+import numpy as np
+
+from cmpc import _lib as L
+
+MOCK = os.path.join(os.path.dirname(L.LIB_PATH), "libcmpc_mex_mock.so")
+_M = None
+
+
+def lib():
+    global _M
+    if _M is None:
+        L.load()   # torch first, then libcmpc (one HIP runtime), then the gateway
+        m = ct.CDLL(MOCK)
+        m.mock_array.restype = ct.c_void_p
+        m.mock_array.argtypes = [ct.c_int, ct.POINTER(ct.c_long), ct.POINTER(ct.c_double)]
+        m.mock_struct2.restype = ct.c_void_p
+        m.mock_struct2.argtypes = [ct.c_char_p, ct.c_void_p, ct.c_char_p, ct.c_void_p]
+        m.mock_call.restype = ct.c_int
+        m.mock_call.argtypes = [ct.c_int, ct.POINTER(ct.c_void_p), ct.c_int, ct.POINTER(ct.c_void_p)]
+        m.mock_err_id.restype = ct.c_char_p
+        m.mock_err_msg.restype = ct.c_char_p
+        m.mock_data.restype = ct.POINTER(ct.c_double)
+        m.mock_data.argtypes = [ct.c_void_p]
+        m.mock_numel.restype = ct.c_size_t
+        m.mock_numel.argtypes = [ct.c_void_p]
+        m.mock_field.restype = ct.c_void_p
+        m.mock_field.argtypes = [ct.c_void_p, ct.c_char_p]
+        m.mock_string.restype = ct.c_char_p
+        m.mock_string.argtypes = [ct.c_void_p]
+        _M = m
+    return _M
+
+
+def mx(a):
+    """numpy array -> mock mxArray (MATLAB column-major; 1-D becomes a column; None -> [])."""
+    m = lib()
+    if a is None:
+        dims = (ct.c_long * 2)(0, 0)
+        return m.mock_array(2, dims, None)
+    a = np.asarray(a, dtype=np.float64)
+    if a.ndim == 1:
+        a = a[:, None]
+    dims = (ct.c_long * a.ndim)(*a.shape)
+    buf = np.asfortranarray(a).ravel(order="F")
+    return m.mock_array(a.ndim, dims, buf.ctypes.data_as(ct.POINTER(ct.c_double)))
+
+
+def values(p):
+    m = lib()
+    k = m.mock_numel(p)
+    return np.ctypeslib.as_array(m.mock_data(p), shape=(k,)).copy() if k else np.zeros(0)
+
+
+def call(args, nlhs=5, opts=None):
+    """cmpc_quadprog(*args [, x0=[], opts]) -> (outputs | None, (err_id, err_msg) | None)."""
+    m = lib()
+    ps = [mx(a) for a in args]
+    if opts is not None:
+        while len(ps) < 8:
+            ps.append(mx(None))
+        ps.append(mx(None))  # x0
+        ps.append(m.mock_struct2(b"MaxIterations", mx(np.array([opts.get("MaxIterations", 0.0)])),
+                                 b"OptimalityTolerance", mx(np.array([opts.get("OptimalityTolerance", 0.0)]))))
+    prhs = (ct.c_void_p * len(ps))(*ps)
+    plhs = (ct.c_void_p * nlhs)()
+    rc = m.mock_call(nlhs, plhs, len(ps), prhs)
+    if rc:
+        return None, (m.mock_err_id().decode(), m.mock_err_msg().decode())
+    return list(plhs), None
+
+
+def field(p, name):
+    return lib().mock_field(p, name.encode())
