@@ -112,6 +112,10 @@ CMPC_QP_UNBOUNDED = -3
 CMPC_QP_NONCONVEX = -6
 
 
+class cmpc_ocd_dims(ct.Structure):
+    _fields_ = [(k, ct.c_int) for k in ("batch", "N", "nb", "self_offset")]
+
+
 class CmpcError(RuntimeError):
     def __init__(self, code, msg=""):
         super().__init__(f"libcmpc error {code}: {msg}")
@@ -143,6 +147,10 @@ SIGNATURES = {
                                        _DP, _DP, _DP, _DP, ct.c_void_p]),
     "cmpc_solve_qp_batch": (ct.c_int, [ct.c_void_p, ct.POINTER(cmpc_qp_dims), ct.POINTER(cmpc_qp_data),
                                        ct.POINTER(cmpc_qp_out), ct.POINTER(cmpc_opts)]),
+    "cmpc_ocd_update_dev": (ct.c_int, [ct.c_void_p, ct.POINTER(cmpc_ocd_dims), ct.c_double, ct.c_double, _IP, _DP,
+                                       _DP, ct.c_void_p]),
+    "cmpc_ocd_converged_dev": (ct.c_int, [ct.c_void_p, ct.c_int, ct.c_int, ct.c_double, ct.c_double, _DP, _DP, _IP,
+                                          ct.c_void_p]),
     "cmpc_selftest_mfma": (ct.c_int, [ct.c_void_p, _DP, _DP, _DP]),
 }
 

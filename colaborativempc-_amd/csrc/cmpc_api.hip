@@ -374,6 +374,29 @@ int cmpc_solve_qp_batch(cmpc_ctx* ctx, const cmpc_qp_dims* d, const cmpc_qp_data
     return CMPC_OK;
 }
 
+int cmpc_ocd_update_dev(cmpc_ctx* ctx, const cmpc_ocd_dims* d, double alpha, double dth, const int* nbr,
+                        const double* traj_all, double* lam, void* stream) {
+    if (!ctx) return CMPC_ERR_ARG;
+    if (!d || d->batch < 0 || d->N < 1 || d->nb < 0 || d->self_offset < 0) return fail(ctx, CMPC_ERR_ARG, "bad OCD dims");
+    if (d->batch && d->nb && (!nbr || !traj_all || !lam)) return fail(ctx, CMPC_ERR_ARG, "null argument");
+    int rc = set_device(ctx);
+    if (rc != CMPC_OK) return rc;
+    cmpc::OcdConst c{d->batch, d->N, d->nb, d->self_offset, alpha, dth};
+    HIP_TRY(cmpc::ocd_update_launch(c, nbr, traj_all, lam, (hipStream_t)stream));
+    return CMPC_OK;
+}
+
+int cmpc_ocd_converged_dev(cmpc_ctx* ctx, int batch, int per, double atol, double rtol, const double* x_old,
+                           const double* x_pred, int* close, void* stream) {
+    if (!ctx) return CMPC_ERR_ARG;
+    if (batch < 0 || per < 0) return fail(ctx, CMPC_ERR_ARG, "bad sizes");
+    if (batch && (!x_old || !x_pred || !close)) return fail(ctx, CMPC_ERR_ARG, "null argument");
+    int rc = set_device(ctx);
+    if (rc != CMPC_OK) return rc;
+    HIP_TRY(cmpc::ocd_close_launch(batch, per, atol, rtol, x_old, x_pred, close, (hipStream_t)stream));
+    return CMPC_OK;
+}
+
 int cmpc_selftest_mfma(cmpc_ctx* ctx, const double* A, const double* B, double* D) {
     if (!ctx || !A || !B || !D) return CMPC_ERR_ARG;
     int rc = set_device(ctx);

@@ -127,6 +127,15 @@ hipError_t di_advance_launch(const DiConst& c, const double* z, double* x0, doub
 
 hipError_t selftest_mfma_launch(const double* A, const double* B, double* D, hipStream_t s);
 
+// OCD coupling-dual round (ocd.hip).
+struct OcdConst {
+    int batch, N, nb, self_offset;
+    double alpha, dth;
+};
+hipError_t ocd_update_launch(const OcdConst& c, const int* nbr, const double* traj, double* lam, hipStream_t s);
+hipError_t ocd_close_launch(int batch, int per, double atol, double rtol, const double* xo, const double* xp,
+                            int* close, hipStream_t s);
+
 // Dense standard-form QP batch (quadprog semantics), qp_dense.hip.
 struct QpConst {
     int n, mi, me;   // variables, general inequality rows, equality rows

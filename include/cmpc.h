@@ -269,6 +269,25 @@ typedef struct {
 int cmpc_solve_qp_batch(cmpc_ctx* ctx, const cmpc_qp_dims* dims, const cmpc_qp_data* host_in,
                         const cmpc_qp_out* host_out, const cmpc_opts* opts);
 
+/* ------------------------------------------------------------------------
+ * OCD coupling-dual round (planner/scripts/NL_EU_N_main.py:119-162; ROS variant
+ * ROS/src/planner_experiments/src/OCD_ROS_main.py:200-239), DEVICE pointers:
+ *   lam[b, s, k-1] += alpha * (dth - ||p_g(k) - p_j(k)||),  g = self_offset + b,
+ *   j = nbr[b, s], for k = 1..N and only when g < j (the reference fills i < j);
+ *   p from traj_all (n_total x (N+1) x 2).  alpha = 0.25 in the reference
+ *   (config/NL/config.py:5-8), dth its safety distance.
+ * cmpc_ocd_converged_dev: close[b] = numpy allclose(x_old[b], x_pred[b], atol, rtol)
+ *   over `per` values per agent (the reference's convergence test, :143-162).
+ * ---------------------------------------------------------------------- */
+typedef struct {
+    int batch, N, nb, self_offset;
+} cmpc_ocd_dims;
+
+int cmpc_ocd_update_dev(cmpc_ctx* ctx, const cmpc_ocd_dims* dims, double alpha, double dth, const int* nbr,
+                        const double* traj_all, double* lam, void* hip_stream);
+int cmpc_ocd_converged_dev(cmpc_ctx* ctx, int batch, int per, double atol, double rtol, const double* x_old,
+                           const double* x_pred, int* close, void* hip_stream);
+
 /* Device self-test of the f64 MFMA fragment mapping used by the solver
  * (D = A*B for one 16x16x4 tile, A,B host 16x4 / 4x16 row-major, D host 16x16). */
 int cmpc_selftest_mfma(cmpc_ctx* ctx, const double* A, const double* B, double* D);

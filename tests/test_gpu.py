@@ -224,3 +224,32 @@ def test_unsupported_sizes_are_rejected(gpu_ctx):
     P = synth.structured(sc.shared, sc.params, sc.A, sc.B, sc.x0, sc.u_prev, sc.lane, sc.nbr, sc.traj, np.arange(2))
     with pytest.raises(cmpc.CmpcError):
         cmpc.solve_mpc(P, gpu_ctx)
+
+
+def test_ocd_dual_update_and_convergence_match_reference(gpu_ctx):
+    """OCD round (NL_EU_N_main.py:119-162) on the device vs the oracle restatement:
+    all-to-all 4 agents (the reference's neighbour sets) and a sharded offset."""
+    import torch
+    from cmpc import ocd
+    from oracle import ocd_ref
+
+    rng = np.random.default_rng(5)
+    n, N, dth = 4, 12, 0.25
+    agents = rng.standard_normal((N + 1, n, 2))
+    lam0 = rng.standard_normal((n, n, N))
+    ref = ocd_ref.ocd_update(lam0, agents, N, dth)
+    nbr = np.array([[j for j in range(n) if j != i] for i in range(n)], np.int32)
+    traj = torch.tensor(np.swapaxes(agents, 0, 1).copy(), device="cuda")        # (n, N+1, 2)
+    for off in (0, 2):                                                            # whole set, or ranks' halves
+        rows = slice(off, off + 2) if off else slice(0, n)
+        lam = torch.tensor(ocd_ref.to_neighbour_layout(lam0, nbr)[rows].copy(), device="cuda")
+        ocd.dual_update(lam, traj, torch.tensor(nbr[rows].copy(), device="cuda"), self_offset=off, dth=dth,
+                        ctx=gpu_ctx)
+        got = lam.cpu().numpy()
+        want = ocd_ref.to_neighbour_layout(ref, nbr)[rows]
+        np.testing.assert_allclose(got, want, rtol=1e-15, atol=1e-15)
+    xo = rng.standard_normal((n, N + 1, 9))
+    xp = xo + rng.uniform(-0.02, 0.02, xo.shape) * (np.arange(n) % 2)[:, None, None]
+    close, allc = ocd.converged(torch.tensor(xo, device="cuda"), torch.tensor(xp, device="cuda"), ctx=gpu_ctx)
+    want = ocd_ref.allclose_agents(xo, xp)
+    assert np.array_equal(close.cpu().numpy().astype(bool), want) and allc == bool(want.all())
