@@ -37,6 +37,7 @@ _IP = ct.POINTER(ct.c_int)
 
 
 CMPC_FLAG_GENERIC = 1
+CMPC_FLAG_FP32 = 8
 
 
 class cmpc_opts(ct.Structure):

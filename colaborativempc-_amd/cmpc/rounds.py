@@ -44,7 +44,8 @@ def exchange_positions(traj_all, traj_local, world=1, group=None):
 
 
 class DIRounds:
-    def __init__(self, scen, rank=0, world=1, device=None, ctx=None, tol=None, max_iter=None, group=None):
+    def __init__(self, scen, rank=0, world=1, device=None, ctx=None, tol=None, max_iter=None, group=None,
+                 fp32=False):
         import torch
 
         self.torch = torch
@@ -83,7 +84,9 @@ class DIRounds:
         self.ddims = L.cmpc_di_dims(self.B, self.N, self.nb, self.off)
         self.mdims = _dims(sh, self.B)
         self.w, self._wkeep = _weights(sh)
-        self.opts = L.opts(tol, max_iter)
+        from .solver import FP32_TOL
+
+        self.opts = L.opts(tol or (FP32_TOL if fp32 else None), max_iter, L.CMPC_FLAG_FP32 if fp32 else 0)
         self.data = L.cmpc_mpc_data(*[_tptr(t) for t in (self.A, self.Bm, self.x0, self.u_prev, self.qlin,
                                                           self.C, self.h)])
         self.out = L.cmpc_mpc_out(_tptr(self.z), _tptr(self.kkt), _tptr(self.iters), _tptr(self.status))

@@ -23,6 +23,7 @@ struct MpcConst {
     int ldk;    // leading dimension of the LDS Hessian (odd)
     int max_iter;
     int debug;  // CMPC_FLAG_DEBUG: dump the first Newton matrix into opts->stamps
+    int wg;     // 0: one-wave kernels; 1: workgroup kernel in fp64 (N*nu > 64); 2: workgroup kernel in fp32
     double tol;
     double qs_max;  // max(1, 2*max(Qs)) — slack residual scale
     double Q[CMPC_MAX_NX * CMPC_MAX_NX];
@@ -68,6 +69,11 @@ __host__ __device__ inline int stop_status(int stop, double best_m, double tol) 
     if (best_m < 1e3 * tol) return CMPC_SOLVED_INACCURATE;
     return stop == kStopMaxIter ? CMPC_MAX_ITER_REACHED : CMPC_UNSOLVED;
 }
+
+// Long-horizon workgroup-per-agent kernel (mpc_ipm_wg.hip), fp32 or fp64, N*nu <= 256.
+size_t mpc_wg_lds_bytes(const MpcConst& c, bool fp32);
+hipError_t mpc_wg_launch(const MpcConst& c, const MpcPtrs& p, int batch, hipStream_t s, bool fp32);
+constexpr size_t kMaxLdsBytes = 160 * 1024;
 
 // Fills the derived fields of MpcConst; returns CMPC_OK or an error code with msg.
 int mpc_prepare(const cmpc_mpc_dims* d, const cmpc_mpc_weights* w, const cmpc_opts* o,

@@ -63,11 +63,14 @@ extern "C" {
 #define CMPC_MAX_NU 4
 #define CMPC_MAX_NS 4
 #define CMPC_MAX_MC 16
-#define CMPC_MAX_NCOND 64
+#define CMPC_MAX_NCOND 64      /* one-wavefront-per-agent solvers (fp64) */
+#define CMPC_MAX_NCOND_WG 256  /* workgroup-per-agent solver (fp32, or fp64 while LDS allows) */
 
 typedef struct cmpc_ctx cmpc_ctx;
 
 #define CMPC_FLAG_GENERIC 1  /* force the generic (runtime-dimension) kernel */
+#define CMPC_FLAG_FP32 8     /* fp32 workgroup-per-agent solver (long horizons, BASELINE cfg5);
+                                opts.tol should then be ~1e-5 */
 
 typedef struct {
     double tol;    /* relative stationarity/feasibility tolerance (complementarity: 1e-4*tol); <= 0 selects 1e-9 */
