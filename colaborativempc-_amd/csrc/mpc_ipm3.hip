@@ -603,28 +603,35 @@ __global__ __launch_bounds__(64, 1) void mpc_ipm3_kernel(const MpcConst c, const
             wsync();
             STAMP(6);
             if (J + 1 < T) {
-                // panel TRSM: L_IJ = K_IJ L_JJ^{-T}, one lane per stacked panel row, in LDS
+                // panel TRSM in the accumulator layout: L_IJ = K_IJ L_JJ^{-T} column by column; lane l
+                // holds column (l & 15) of every panel tile, its own row of L_JJ in rw (lane = row), so
+                // L[l & 15][cc] = rw[cc] and Y[:, cc] reaches the row of 16 lanes by DPP row_newbcast
+                {
+                    const int i16 = l & 15;
+                    const double inv_own = 1.0 / S0[i16 * 17 + i16];
+                    static_for<0, 16>([&](auto jc) __attribute__((always_inline)) {
+                        constexpr int cc = decltype(jc)::value;
+                        const double lcc = rw[cc];
+#pragma unroll
+                        for (int I = J + 1; I < T; ++I)
+#pragma unroll
+                            for (int r = 0; r < 4; ++r) {
+                                double v = acc[I * (I + 1) / 2 + J][r];
+                                if (i16 == cc) v *= inv_own;
+                                const double ycc = bcast16<cc>(v);
+                                if (i16 > cc) v = fma(-ycc, lcc, v);
+                                acc[I * (I + 1) / 2 + J][r] = v;
+                            }
+                        __builtin_amdgcn_sched_barrier(0);
+                    });
+                }
+                // stacked panel rows to LDS for the transposed MFMA operands of the SYRK
 #pragma unroll
                 for (int I = J + 1; I < T; ++I)
 #pragma unroll
                     for (int r = 0; r < 4; ++r)
                         SP[((I - J - 1) * 16 + (l >> 4) + 4 * r) * 17 + (l & 15)] = acc[I * (I + 1) / 2 + J][r];
                 wsync();
-                if (l < 16 * (T - 1 - J)) {
-                    double* yrow = SP + l * 17;
-#pragma unroll 1
-                    for (int cc = 0; cc < 16; ++cc) {
-                        double v = yrow[cc];
-                        for (int p = 0; p < cc; ++p) v = fma(-S0[cc * 17 + p], yrow[p], v);
-                        yrow[cc] = v / S0[cc * 17 + cc];
-                    }
-                }
-                wsync();
-#pragma unroll
-                for (int I = J + 1; I < T; ++I)
-#pragma unroll
-                    for (int r = 0; r < 4; ++r)
-                        acc[I * (I + 1) / 2 + J][r] = SP[((I - J - 1) * 16 + (l >> 4) + 4 * r) * 17 + (l & 15)];
                 // trailing SYRK: K_IK -= L_IJ L_KJ'  (I >= K > J) on MFMA
 #pragma unroll
                 for (int q = 0; q < 16; q += 4) {
