@@ -239,6 +239,55 @@ __global__ __launch_bounds__(64,1) void k_mfma_dep(const double* gA, double* out
   if (l == 0) cyc[blockIdx.x] = (t1 - t0);
   out[blockIdx.x * 64 + l] = s0;
 }
+
+__global__ __launch_bounds__(64,1) void k_mfma_tp(const double* gA, double* out, unsigned long long* cyc) {
+  int l = threadIdx.x;
+  v4d acc[10];
+  for (int q = 0; q < 10; ++q) acc[q] = v4d{0,0,0,0};
+  double a = gA[l], b = gA[64 + l];
+  double av[10];
+  for (int q = 0; q < 10; ++q) av[q] = a + q;
+  unsigned long long t0 = stamp();
+  for (int rep = 0; rep < 32; ++rep) {
+#pragma unroll
+    for (int q = 0; q < 10; ++q) acc[q] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[q], b, acc[q], 0, 0, 0);
+  }
+  double s = 0;
+#pragma unroll
+  for (int q = 0; q < 10; ++q) s += acc[q][0];
+  asm volatile("v_mov_b64 %0, %0" : "+v"(s));
+  unsigned long long t1 = stamp();
+  if (l == 0) cyc[blockIdx.x] = (t1 - t0);
+  out[blockIdx.x * 64 + l] = s;
+}
+__global__ __launch_bounds__(64,1) void k_fma_tp(const double* gA, double* out, unsigned long long* cyc) {
+  int l = threadIdx.x;
+  double x[16];
+  for (int q = 0; q < 16; ++q) x[q] = gA[l] + q;
+  double y = gA[64 + l];
+  unsigned long long t0 = stamp();
+  for (int rep = 0; rep < 32; ++rep) {
+#pragma unroll
+    for (int q = 0; q < 16; ++q) x[q] = fma(x[q], y, 0.5);
+  }
+  double s = 0;
+  for (int q = 0; q < 16; ++q) s += x[q];
+  asm volatile("v_mov_b64 %0, %0" : "+v"(s));
+  unsigned long long t1 = stamp();
+  if (l == 0) cyc[blockIdx.x] = (t1 - t0);
+  out[blockIdx.x * 64 + l] = s;
+}
+__global__ __launch_bounds__(64,1) void k_dpp(const double* gA, double* out, unsigned long long* cyc) {
+  int l = threadIdx.x;
+  double v = gA[l];
+  unsigned long long t0 = stamp();
+#pragma unroll
+  for (int i = 0; i < 32; ++i) v = fma(cmpc::bcast16<3>(v), 0.5, v);
+  asm volatile("v_mov_b64 %0, %0" : "+v"(v));
+  unsigned long long t1 = stamp();
+  if (l == 0) cyc[blockIdx.x] = (t1 - t0);
+  out[blockIdx.x * 64 + l] = v;
+}
 int main() {
   const int nb = 1024;
   std::vector<double> hA(N*NX*NX*1 + 4096), hK(256);
@@ -260,6 +309,9 @@ int main() {
     hipLaunchKernelGGL(k_chol_lds, dim3(nb), dim3(64), 0, 0, dK, out, cyc); rep("chol16 rsq+lds", 1);
     hipLaunchKernelGGL(k_mfma, dim3(nb), dim3(64), 0, 0, dA, out, cyc); rep("mfma f64 x10 indep (per mfma)", 100);
     hipLaunchKernelGGL(k_mfma_dep, dim3(nb), dim3(64), 0, 0, dA, out, cyc); rep("mfma f64 dependent chain", 32);
+    hipLaunchKernelGGL(k_mfma_tp, dim3(nb), dim3(64), 0, 0, dA, out, cyc); rep("mfma f64 throughput (10 indep, drained)", 320);
+    hipLaunchKernelGGL(k_fma_tp, dim3(nb), dim3(64), 0, 0, dA, out, cyc); rep("fma f64 throughput (16 indep)", 512);
+    hipLaunchKernelGGL(k_dpp, dim3(nb), dim3(64), 0, 0, dA, out, cyc); rep("dpp bcast -> fma dep chain", 32);
     hipLaunchKernelGGL(k_fma, dim3(nb), dim3(64), 0, 0, dA, out, cyc); rep("fma f64 dep chain", 64);
     hipLaunchKernelGGL(k_lds, dim3(nb), dim3(64), 0, 0, dA, out, cyc); rep("lds dep read", 32);
     hipLaunchKernelGGL(k_readlane, dim3(nb), dim3(64), 0, 0, dA, out, cyc); rep("readlane_d->fma dep", 32);
