@@ -15,8 +15,8 @@
 //  * batch-shared weights live in LDS, not in kernel-argument SGPRs;
 //  * K = sum_k Gamma_{k+1}' W_{k+1} Gamma_{k+1}: lane c carries column c of Gamma_k in
 //    registers through the recursion Gamma_{k+1} = A_k Gamma_k + [0 .. B_k], forms
-//    W Gamma in registers, hands both to the MFMA fragment layout through LDS and
-//    accumulates with V_MFMA_F64_16X16X4_F64 only on the tiles that are nonzero for the
+//    W Gamma in registers, moves both to the MFMA fragment layout by an in-register row
+//    transpose (v_permlane32_swap / v_permlane16_swap) and accumulates with V_MFMA_F64_16X16X4_F64 only on the tiles that are nonzero for the
 //    stage (static per horizon segment: no data-dependent branch around an MFMA);
 //  * K is factored in the accumulators (blocked right-looking Cholesky: 16x16 diagonal
 //    factor, panel substitution, trailing SYRK on MFMA); the diagonal factors L_JJ are
@@ -64,6 +64,7 @@ __host__ __device__ inline Lds3 lds3_layout(int N) {
     L.x0 = take(NX);
     L.up = take(NU);
     // W, Gb, Yb are contiguous: the Cholesky panel scratch aliases them after the K build
+    // (Gb / Yb are only that scratch's extent now: the K build transposes in registers)
     L.W = take(N * NX * NX);
     L.Gb = take(NXP * NP);
     L.Yb = take(NXP * NP);
@@ -198,8 +199,6 @@ __global__ __launch_bounds__(64, 1) void mpc_ipm3_kernel(const MpcConst c, const
     double* sx0 = sm + L.x0;
     double* sup = sm + L.up;
     double* sW = sm + L.W;
-    double* Gb = sm + L.Gb;
-    double* Yb = sm + L.Yb;
     double* X = sm + L.X;
     double* dX = sm + L.dX;
     double* yb = sm + L.yb;
@@ -464,14 +463,6 @@ __global__ __launch_bounds__(64, 1) void mpc_ipm3_kernel(const MpcConst c, const
                 for (int i = 0; i < NU; ++i) thin[k * NU + i] = th[2 * i] + th[2 * i + 1];
             }
         }
-        if constexpr (NXP > NX) {
-            // the MFMA K-groups read rows NX..NXP-1 of Gb / Yb (the Cholesky panel scratch
-            // aliases them): zero before every K build
-            for (int i = NX * NP + l; i < NXP * NP; i += 64) {
-                Gb[i] = 0.0;
-                Yb[i] = 0.0;
-            }
-        }
         wsync();
         STAMP(3);
         // zero the accumulators with an MFMA so they are defined in the accumulator registers:
@@ -483,11 +474,23 @@ __global__ __launch_bounds__(64, 1) void mpc_ipm3_kernel(const MpcConst c, const
             for (int q = 0; q < NT; ++q) acc[q] = __builtin_amdgcn_mfma_f64_16x16x4f64(0.0, 0.0, z4, 0, 0, 0);
         }
         {
-            // lane l carries column l of Gamma_k (Gamma_0 = 0)
+            // lane l carries column l of Gamma_k (Gamma_0 = 0) and of W_k Gamma_k; both reach the
+            // MFMA fragment layout by an in-register row transpose (no LDS round trip).  For small
+            // NX, A_k and B_k are loaded one stage ahead (registers) so their LDS latency overlaps
+            // the MFMAs; larger NX read them in place (the prefetch would not fit the VGPR file).
+            constexpr bool kPf = NX * (NX + NU) <= 24;
+            constexpr int PA = kPf ? NX * NX : 1, PB = kPf ? NX * NU : 1;
             double g[NX];
 #pragma unroll
             for (int s = 0; s < NX; ++s) g[s] = 0.0;
             const int col = l;
+            double an[PA], bn[PB];
+            if constexpr (kPf) {
+#pragma unroll
+                for (int i = 0; i < PA; ++i) an[i] = sA[i];
+#pragma unroll
+                for (int i = 0; i < PB; ++i) bn[i] = sB[i];
+            }
 #pragma unroll
             for (int tau = 0; tau < T; ++tau) {
                 // stages whose Gamma_{k+1} has tiles 0..tau nonzero (last column (k+1)NU-1 in tile tau)
@@ -498,47 +501,64 @@ __global__ __launch_bounds__(64, 1) void mpc_ipm3_kernel(const MpcConst c, const
                     const double* Ak = sA + kk * NX * NX;
                     const double* Bk = sB + kk * NX * NU;
                     const double* Wk = sW + kk * NX * NX;
+                    double ak[PA], bk[PB];
+                    if constexpr (kPf) {
+#pragma unroll
+                        for (int i = 0; i < PA; ++i) ak[i] = an[i];
+#pragma unroll
+                        for (int i = 0; i < PB; ++i) bk[i] = bn[i];
+                        const int kn = kk + 1 < N ? kk + 1 : kk;
+#pragma unroll
+                        for (int i = 0; i < PA; ++i) an[i] = sA[kn * NX * NX + i];
+#pragma unroll
+                        for (int i = 0; i < PB; ++i) bn[i] = sB[kn * NX * NU + i];
+                    }
+                    auto A_ = [&](int i) __attribute__((always_inline)) {
+                        if constexpr (kPf) return ak[i];
+                        else return Ak[i];
+                    };
+                    auto B_ = [&](int i) __attribute__((always_inline)) {
+                        if constexpr (kPf) return bk[i];
+                        else return Bk[i];
+                    };
                     const int jj = col - kk * NU;
                     double gn[NX];
 #pragma unroll
                     for (int s = 0; s < NX; ++s) {
                         double v = 0.0;
 #pragma unroll
-                        for (int i = 0; i < NU; ++i) v = (jj == i) ? Bk[s * NU + i] : v;
+                        for (int i = 0; i < NU; ++i) {
+                            const double bv = B_(s * NU + i);  // unconditional load, register select
+                            v = (jj == i) ? bv : v;
+                        }
 #pragma unroll
-                        for (int u = 0; u < NX; ++u) v = fma(Ak[s * NX + u], g[u], v);
+                        for (int u = 0; u < NX; ++u) v = fma(A_(s * NX + u), g[u], v);
                         gn[s] = v;
                     }
 #pragma unroll
                     for (int s = 0; s < NX; ++s) g[s] = gn[s];
-                    if (col < NP) {
+                    double gf[NXP], yf[NXP];
 #pragma unroll
-                        for (int s = 0; s < NX; ++s) {
-                            double y = 0.0;
+                    for (int s = 0; s < NXP; ++s) {
+                        double y = 0.0;
+                        if (s < NX) {
 #pragma unroll
                             for (int u = 0; u < NX; ++u) y = fma(Wk[s * NX + u], g[u], y);
-                            Gb[s * NP + col] = g[s];
-                            Yb[s * NP + col] = y;
                         }
+                        gf[s] = s < NX ? g[s] : 0.0;
+                        yf[s] = y;
                     }
-                    wsync();
 #pragma unroll
                     for (int q = 0; q < NXP; q += 4) {
-                        const int row = q + (l >> 4);
-                        double af[T], bf[T];
-#pragma unroll
-                        for (int ti = 0; ti <= tau; ++ti) {
-                            af[ti] = Gb[row * NP + ti * 16 + (l & 15)];
-                            bf[ti] = Yb[row * NP + ti * 16 + (l & 15)];
-                        }
+                        transpose_rows4(gf[q], gf[q + 1], gf[q + 2], gf[q + 3]);
+                        transpose_rows4(yf[q], yf[q + 1], yf[q + 2], yf[q + 3]);
 #pragma unroll
                         for (int ti = 0; ti <= tau; ++ti)
 #pragma unroll
                             for (int tj = 0; tj <= ti; ++tj)
                                 acc[ti * (ti + 1) / 2 + tj] = __builtin_amdgcn_mfma_f64_16x16x4f64(
-                                    af[ti], bf[tj], acc[ti * (ti + 1) / 2 + tj], 0, 0, 0);
+                                    gf[q + ti], yf[q + tj], acc[ti * (ti + 1) / 2 + tj], 0, 0, 0);
                     }
-                    wsync();
                 }
             }
         }

@@ -76,4 +76,34 @@ __device__ __forceinline__ double rsqrt_d(double x) {
     return y;
 }
 
+// CDNA4 row exchanges on doubles (one instruction per dword):
+//  swap_half: lanes 32..63 of a <-> lanes 0..31 of b   (v_permlane32_swap)
+//  swap_odd:  odd 16-lane rows of a <-> even rows of b  (v_permlane16_swap)
+__device__ __forceinline__ void swap_half(double& a, double& b) {
+    const unsigned long long ua = __builtin_bit_cast(unsigned long long, a);
+    const unsigned long long ub = __builtin_bit_cast(unsigned long long, b);
+    const auto lo = __builtin_amdgcn_permlane32_swap((unsigned)ua, (unsigned)ub, false, false);
+    const auto hi = __builtin_amdgcn_permlane32_swap((unsigned)(ua >> 32), (unsigned)(ub >> 32), false, false);
+    a = __builtin_bit_cast(double, (unsigned long long)lo[0] | ((unsigned long long)hi[0] << 32));
+    b = __builtin_bit_cast(double, (unsigned long long)lo[1] | ((unsigned long long)hi[1] << 32));
+}
+__device__ __forceinline__ void swap_odd(double& a, double& b) {
+    const unsigned long long ua = __builtin_bit_cast(unsigned long long, a);
+    const unsigned long long ub = __builtin_bit_cast(unsigned long long, b);
+    const auto lo = __builtin_amdgcn_permlane16_swap((unsigned)ua, (unsigned)ub, false, false);
+    const auto hi = __builtin_amdgcn_permlane16_swap((unsigned)(ua >> 32), (unsigned)(ub >> 32), false, false);
+    a = __builtin_bit_cast(double, (unsigned long long)lo[0] | ((unsigned long long)hi[0] << 32));
+    b = __builtin_bit_cast(double, (unsigned long long)lo[1] | ((unsigned long long)hi[1] << 32));
+}
+
+// 4x4 transpose of (register, 16-lane row): on return r[t] holds, in row k, what r[k] held in
+// row t.  With lane c carrying column c of a 4 x 64 matrix M in r[0..3], r[t] becomes the
+// f64 16x16x4 MFMA fragment of the columns 16t..16t+15 (lane i + 16k: M[k][16t + i]).
+__device__ __forceinline__ void transpose_rows4(double& r0, double& r1, double& r2, double& r3) {
+    swap_half(r0, r2);
+    swap_half(r1, r3);
+    swap_odd(r0, r1);
+    swap_odd(r2, r3);
+}
+
 }  // namespace cmpc
