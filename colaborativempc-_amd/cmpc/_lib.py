@@ -14,7 +14,8 @@ import numpy as np
 
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(PKG_DIR)
-LIB_PATH = os.path.join(ROOT, "lib", "libcmpc.so")
+# CMPC_LIB_PATH: an alternative build of the same ABI (profiling variants under tools/)
+LIB_PATH = os.environ.get("CMPC_LIB_PATH") or os.path.join(ROOT, "lib", "libcmpc.so")
 HEADER = os.path.join(os.path.dirname(ROOT), "include", "cmpc.h")
 
 CMPC_OK = 0

@@ -17,6 +17,9 @@
  * (oracle/qp_ipm.py) on QPs captured from the reference (tests/golden).
  */
 #include <math.h>
+#ifdef ORACLE_TRACE
+#include <stdio.h>
+#endif
 #include <stdlib.h>
 #include <string.h>
 #ifdef _OPENMP
@@ -110,8 +113,9 @@ static void chol_solve(const double* L, int n, double* b) {
     }
 }
 
+/* largest step keeping v + a dv >= 0 (unbounded: +inf; callers clip) */
 static double max_step(const double* v, const double* dv, const unsigned char* act, int m) {
-    double a = 1.0;
+    double a = INFINITY;
     for (int r = 0; r < m; ++r)
         if (act[r] && dv[r] < 0.0) {
             double c = -v[r] / dv[r];
@@ -275,6 +279,10 @@ static int solve_one(const shared_t* S, const agent_t* a, double tol, int max_it
             memcpy(bU, U, sizeof(double) * n);
             memcpy(bsig, sig, sizeof(double) * N * ns);
         }
+#ifdef ORACLE_TRACE
+        fprintf(stderr, "it %2d mu %.3e res %.3e (rd %.2e rs %.2e rp %.2e) merit %.3e\n", it, mu, res,
+                nrd / gscale, nrs / qs_max, nrp / scale_p, merit);
+#endif
         if (merit < tol) { stop = 1; break; }
         /* near-converged but no progress for STALL_ITERS iterations: rounding floor reached */
         if (best_m < 1e3 * tol && it - best_it >= STALL_ITERS) { stop = 3; break; }
@@ -411,6 +419,7 @@ static int solve_one(const shared_t* S, const agent_t* a, double tol, int max_it
             double ap = max_step(t, dt, wk->act, m), ad = max_step(lam, dl, wk->act, m);
             double al = ap < ad ? ap : ad;
             if (!pass) {
+                if (al > 1.0) al = 1.0;
                 mu_aff = 0.0;
                 for (int r = 0; r < m; ++r)
                     if (wk->act[r]) mu_aff += (t[r] + al * dt[r]) * (lam[r] + al * dl[r]);
@@ -432,7 +441,22 @@ static int solve_one(const shared_t* S, const agent_t* a, double tol, int max_it
                         }
                     if (pmin >= NBHD_GAMMA * (mn / mact)) break;
                     al *= 0.8;
+#ifdef ORACLE_TRACE
+                    fprintf(stderr, "      backtrack %d al %.3e\n", bt, al);
+#endif
                 }
+#ifdef ORACLE_TRACE
+                {
+                    int blk = -1; double amin = INFINITY;
+                    for (int r = 0; r < m; ++r) if (wk->act[r]) {
+                        if (dt[r] < 0 && -t[r] / dt[r] < amin) { amin = -t[r] / dt[r]; blk = r; }
+                        if (dl[r] < 0 && -lam[r] / dl[r] < amin) { amin = -lam[r] / dl[r]; blk = 10000 + r; }
+                    }
+                    if (blk >= 0)
+                        fprintf(stderr, "      step al %.3e sigma %.2e mu_aff/mu %.2e blocking %d (t %.2e lam %.2e)\n",
+                                al, sig_c, mu > 0 ? mu_aff / mu : 0.0, blk, t[blk % 10000], lam[blk % 10000]);
+                }
+#endif
                 for (int c = 0; c < n; ++c) U[c] += al * wk->dU[c];
                 for (int q = 0; q < N * ns; ++q) sig[q] += al * wk->dsig[q];
                 for (int r = 0; r < m; ++r)
