@@ -438,12 +438,34 @@ __global__ __launch_bounds__(64, 1) void mpc_ipm3_kernel(const MpcConst c, const
                 double thp[MC];
 #pragma unroll
                 for (int r = 0; r < MC; ++r) thp[r] = slk(r) < 0 ? th[r] : Qs2[slk(r)] * th[r] / Dsig[slk(r)];
-                const double* Ck = sC + k * MC * NX;
-                for (int s = 0; s < NX; ++s)
-                    for (int u = 0; u < NX; ++u) {
-                        double v = Q2[s * NX + u];
+                // the stage's rows and 2Q into registers in one batch of LDS reads (read inside the
+                // loops below they were issued one dependent wait at a time)
+                // (small NX only: larger ones would not fit the VGPR file and read in place)
+                constexpr bool kWr = NX * (MC + NX) <= 48;
+                constexpr int PC = kWr ? MC * NX : 1, PQ = kWr ? NX * NX : 1;
+                double ckr[PC], q2r[PQ];
+                if constexpr (kWr) {
 #pragma unroll
-                        for (int r = 0; r < MC; ++r) v = fma(thp[r] * Ck[r * NX + s], Ck[r * NX + u], v);
+                    for (int i = 0; i < PC; ++i) ckr[i] = sC[k * MC * NX + i];
+#pragma unroll
+                    for (int i = 0; i < PQ; ++i) q2r[i] = Q2[i];
+                }
+                const double* Ckp = sC + k * MC * NX;
+                auto Ck_ = [&](int i) __attribute__((always_inline)) {
+                    if constexpr (kWr) return ckr[i];
+                    else return Ckp[i];
+                };
+                auto q2_ = [&](int i) __attribute__((always_inline)) {
+                    if constexpr (kWr) return q2r[i];
+                    else return Q2[i];
+                };
+#pragma unroll
+                for (int s = 0; s < NX; ++s)
+#pragma unroll
+                    for (int u = 0; u < NX; ++u) {
+                        double v = q2_(s * NX + u);
+#pragma unroll
+                        for (int r = 0; r < MC; ++r) v = fma(thp[r] * Ck_(r * NX + s), Ck_(r * NX + u), v);
 #pragma unroll
                         for (int r = 0; r < MC; ++r) {
                             if (slk(r) < 0) continue;
@@ -451,8 +473,8 @@ __global__ __launch_bounds__(64, 1) void mpc_ipm3_kernel(const MpcConst c, const
                             for (int r2 = r + 1; r2 < MC; ++r2) {
                                 if (slk(r2) != slk(r)) continue;
                                 const double phi = th[r] * th[r2] / Dsig[slk(r)];
-                                const double ds = sgn(r) * Ck[r * NX + s] - sgn(r2) * Ck[r2 * NX + s];
-                                const double du = sgn(r) * Ck[r * NX + u] - sgn(r2) * Ck[r2 * NX + u];
+                                const double ds = sgn(r) * Ck_(r * NX + s) - sgn(r2) * Ck_(r2 * NX + s);
+                                const double du = sgn(r) * Ck_(r * NX + u) - sgn(r2) * Ck_(r2 * NX + u);
                                 v = fma(phi * ds, du, v);
                             }
                         }
@@ -563,25 +585,26 @@ __global__ __launch_bounds__(64, 1) void mpc_ipm3_kernel(const MpcConst c, const
             }
         }
         STAMP(4);
-        // + 2R + 2D'dR D (block tridiagonal) + input-row curvature; identity on the padding
+        // + 2R + 2D'dR D (block tridiagonal) + input-row curvature; identity on the padding.
+        // The band half-width 2NU - 1 < 16 touches only the diagonal and first sub-diagonal tiles;
+        // branch-free: unconditional (clamped) LDS reads and selects.
 #pragma unroll
         for (int ti = 0; ti < T; ++ti)
 #pragma unroll
-            for (int tj = 0; tj <= ti; ++tj)
+            for (int tj = (ti > 0 ? ti - 1 : 0); tj <= ti; ++tj)
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
                     const int row = ti * 16 + (l >> 4) + 4 * r, col = tj * 16 + (l & 15);
-                    double add = 0.0;
-                    if (row < n && col < n) {
-                        const int kr = row / NU, a = row - kr * NU, kc = col / NU, bq = col - kc * NU;
-                        if (kr == kc)
-                            add = R2[a * NU + bq] + dR2[a * NU + bq] * (kr + 1 < N ? 2.0 : 1.0) +
-                                  (row == col ? thin[row] : 0.0);
-                        else if (kr == kc + 1 || kc == kr + 1)
-                            add = -dR2[a * NU + bq];
-                    } else if (row == col) {
-                        add = 1.0;
-                    }
+                    const int kr = row / NU, a = row - kr * NU, kc = col / NU, bq = col - kc * NU;
+                    const double r2 = R2[a * NU + bq], d2 = dR2[a * NU + bq], thr = thin[row];
+                    const bool in = row < n && col < n;
+                    // 0/1 masks instead of selects around the loaded values (the compiler turns those
+                    // into divergent branches with the loads inside); thin of a padding row may be
+                    // garbage: the final select drops it
+                    const double md = (kr == kc) ? 1.0 : 0.0, mo = (kr == kc + 1 || kc == kr + 1) ? 1.0 : 0.0;
+                    const double me = (row == col) ? 1.0 : 0.0, f = (kr + 1 < N) ? 2.0 : 1.0;
+                    double add = fma(md, fma(d2, f, r2), fma(md * me, thr, -mo * d2));
+                    add = in ? add : me;
                     acc[ti * (ti + 1) / 2 + tj][r] += add;
                 }
         STAMP(5);
