@@ -86,17 +86,19 @@ __host__ __device__ inline Lds3 lds3_layout(int N) {
 }
 
 // x_0 = x0 (LDS, or 0), x_{k+1} = A_k x_k + B_k u_k.  Lane (l & 15) = s < NX of every row of
-// 16 carries x_s (the rows are duplicates); x_t reaches the row by DPP row_newbcast.  The next
-// stage's A row and B u term are fetched while the current stage computes.
+// 16 carries x_s (the rows are duplicates; lanes with s >= NX duplicate x_0); x_t reaches the
+// row by DPP row_newbcast.  The next stage's A row and B u term are fetched while the current
+// stage computes, into ping-pong registers (unrolled by two: no copies, no branches; the
+// fetch index is clamped instead of guarded).  Every lane stores: duplicates write equal values.
 template <int NX, int NU>
 __device__ __forceinline__ void fwd3(int l, int N, const double* A, const double* B, const double* x0,
                                      const double* U, double* X) {
     static_assert(NX <= 16, "row broadcast");
     const int s = (l & 15) < NX ? (l & 15) : 0;
     double xr = x0 ? x0[s] : 0.0;
-    if (l < NX) X[l] = xr;
-    double a[NX], bu = 0.0;
-    auto fetch = [&](int k, double* av, double& b) {
+    X[s] = xr;
+    if (N <= 0) return;
+    auto fetch = [&](int k, double* av, double& b) __attribute__((always_inline)) {
 #pragma unroll
         for (int t = 0; t < NX; ++t) av[t] = A[(k * NX + s) * NX + t];
         double v = 0.0;
@@ -104,50 +106,53 @@ __device__ __forceinline__ void fwd3(int l, int N, const double* A, const double
         for (int i = 0; i < NU; ++i) v = fma(B[(k * NX + s) * NU + i], U[k * NU + i], v);
         b = v;
     };
-    if (N > 0) fetch(0, a, bu);
-    for (int k = 0; k < N; ++k) {
-        double an[NX], bn = 0.0;
-        if (k + 1 < N) fetch(k + 1, an, bn);
-        double v0 = bu, v1 = 0.0;
+    auto step = [&](int k, const double* av, double b) __attribute__((always_inline)) {
+        double v0 = b, v1 = 0.0;
         static_for<0, NX>([&](auto t) __attribute__((always_inline)) {
             constexpr int tt = decltype(t)::value;
-            if constexpr (tt & 1) v1 = fma(a[tt], bcast16<tt>(xr), v1);
-            else v0 = fma(a[tt], bcast16<tt>(xr), v0);
+            if constexpr (tt & 1) v1 = fma(av[tt], bcast16<tt>(xr), v1);
+            else v0 = fma(av[tt], bcast16<tt>(xr), v0);
         });
         xr = v0 + v1;
-        if (l < NX) X[(k + 1) * NX + l] = xr;
-#pragma unroll
-        for (int t = 0; t < NX; ++t) a[t] = an[t];
-        bu = bn;
+        X[(k + 1) * NX + s] = xr;
+    };
+    double a0[NX], a1[NX], b0, b1;
+    fetch(0, a0, b0);
+    int k = 0;
+    for (; k + 1 < N; k += 2) {
+        fetch(k + 1, a1, b1);
+        step(k, a0, b0);
+        fetch(k + 2 < N ? k + 2 : N - 1, a0, b0);
+        step(k + 1, a1, b1);
     }
+    if (k < N) step(k, a0, b0);
 }
 
 // Two adjoints at once (rows 0,1 of the wave on y0 -> o0, rows 2,3 on y1 -> o1):
 // o_k = B_k' psi_{k+1}, psi_N = y_N, psi_k = y_k + A_k' psi_{k+1}.  Lane (l & 15) = s carries
-// psi_s; psi_t reaches the row by DPP row_newbcast; operands of stage k-1 are fetched ahead.
+// psi_s; psi_t reaches the row by DPP row_newbcast; operands of stage k-1 are fetched ahead into
+// ping-pong registers (unrolled by two, clamped fetch index, no branches).  Every lane stores
+// o[k NU + su]: rows 0/1 (2/3) and lanes s >= NU (which compute column 0) duplicate values.
 template <int NX, int NU>
 __device__ __forceinline__ void adj3(int l, int N, const double* A, const double* B, const double* y0,
                                      const double* y1, double* o0, double* o1) {
     static_assert(NX <= 16 && NU <= 16, "row broadcast");
     const int h = l >> 5, s = l & 15;
     const int sx = s < NX ? s : 0, su = s < NU ? s : 0;
-    const bool wr = ((l & 16) == 0) && s < NU;  // rows 0 and 2 write the outputs
     const double* y = h ? y1 : y0;
     double* o = h ? o1 : o0;
     double pr = y[N * NX + sx];
-    double a[NX], bb[NX], yk = 0.0;
-    auto fetch = [&](int k, double* av, double* bv, double& yv) {
+    if (N <= 0) return;
+    auto fetch = [&](int k, double* av, double* bv, double& yv) __attribute__((always_inline)) {
 #pragma unroll
         for (int t = 0; t < NX; ++t) {
             av[t] = A[(k * NX + t) * NX + sx];
             bv[t] = B[(k * NX + t) * NU + su];
         }
-        yv = k > 0 ? y[k * NX + sx] : 0.0;
+        const double yy = y[k * NX + sx];
+        yv = k > 0 ? yy : 0.0;
     };
-    if (N > 0) fetch(N - 1, a, bb, yk);
-    for (int k = N - 1; k >= 0; --k) {
-        double an[NX], bn[NX], yn = 0.0;
-        if (k > 0) fetch(k - 1, an, bn, yn);
+    auto step = [&](int k, const double* av, const double* bv, double yk) __attribute__((always_inline)) {
         double ps[NX];
         static_for<0, NX>([&](auto t) __attribute__((always_inline)) {
             constexpr int tt = decltype(t)::value;
@@ -157,22 +162,26 @@ __device__ __forceinline__ void adj3(int l, int N, const double* A, const double
 #pragma unroll
         for (int t = 0; t < NX; ++t) {
             if (t & 1) {
-                v1 = fma(bb[t], ps[t], v1);
-                p1 = fma(a[t], ps[t], p1);
+                v1 = fma(bv[t], ps[t], v1);
+                p1 = fma(av[t], ps[t], p1);
             } else {
-                v0 = fma(bb[t], ps[t], v0);
-                p0 = fma(a[t], ps[t], p0);
+                v0 = fma(bv[t], ps[t], v0);
+                p0 = fma(av[t], ps[t], p0);
             }
         }
-        if (wr) o[k * NU + s] = v0 + v1;
+        o[k * NU + su] = v0 + v1;
         pr = p0 + p1;
-#pragma unroll
-        for (int t = 0; t < NX; ++t) {
-            a[t] = an[t];
-            bb[t] = bn[t];
-        }
-        yk = yn;
+    };
+    double a0[NX], bb0[NX], y0k, a1[NX], bb1[NX], y1k;
+    fetch(N - 1, a0, bb0, y0k);
+    int k = N - 1;
+    for (; k >= 1; k -= 2) {
+        fetch(k - 1, a1, bb1, y1k);
+        step(k, a0, bb0, y0k);
+        fetch(k >= 2 ? k - 2 : 0, a0, bb0, y0k);
+        step(k - 1, a1, bb1, y1k);
     }
+    if (k == 0) step(0, a0, bb0, y0k);
 }
 
 }  // namespace

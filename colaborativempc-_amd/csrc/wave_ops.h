@@ -61,11 +61,13 @@ __device__ __forceinline__ void static_for(F&& f) {
 }
 
 // Lane J of each row of 16 lanes, broadcast to the whole row: one v_mov_b64_dpp row_newbcast:J
-// (no SGPR round trip, unlike v_readlane).
+// (no SGPR round trip, unlike v_readlane).  Every lane reads a valid source lane, so the old
+// value is dead: bound_ctrl with old = 0 lets the compiler drop the copy of x it otherwise
+// makes into the destination first.
 template <int J>
 __device__ __forceinline__ double bcast16(double x) {
     static_assert(J >= 0 && J < 16, "row_newbcast lane");
-    return __builtin_amdgcn_update_dpp(x, x, 0x150 + J, 0xF, 0xF, false);
+    return __builtin_amdgcn_update_dpp(0.0, x, 0x150 + J, 0xF, 0xF, true);
 }
 
 // 1/sqrt(x) to full double precision: hardware estimate + two Newton steps.
