@@ -506,92 +506,102 @@ __global__ __launch_bounds__(64, 1) void mpc_ipm3_kernel(const MpcConst c, const
         }
         {
             // lane l carries column l of Gamma_k (Gamma_0 = 0) and of W_k Gamma_k; both reach the
-            // MFMA fragment layout by an in-register row transpose (no LDS round trip).  For small
-            // NX, A_k and B_k are loaded one stage ahead (registers) so their LDS latency overlaps
-            // the MFMAs; larger NX read them in place (the prefetch would not fit the VGPR file).
-            constexpr bool kPf = NX * (NX + NU) <= 24;
-            constexpr int PA = kPf ? NX * NX : 1, PB = kPf ? NX * NU : 1;
+            // MFMA fragment layout by an in-register row transpose (no LDS round trip).
+            //  * column l = kc NU + ic is zero up to stage kc, where it becomes B_kc[:, ic]: the lane
+            //    loads that column once and selects it at its stage (A_k Gamma_k is exactly 0 there);
+            //  * for small NX, A_k is fetched one stage ahead into ping-pong registers (the stage
+            //    loop is unrolled by two: no copies); larger NX read A_k in place.
+            constexpr bool kPf = NX * NX <= 16;
+            constexpr int PA = kPf ? NX * NX : 1;
             double g[NX];
 #pragma unroll
             for (int s = 0; s < NX; ++s) g[s] = 0.0;
             const int col = l;
-            double an[PA], bn[PB];
-            if constexpr (kPf) {
+            const int kc = col / NU, ic = col - kc * NU, kcl = kc < N ? kc : N - 1;
+            double bcol[NX];
 #pragma unroll
-                for (int i = 0; i < PA; ++i) an[i] = sA[i];
+            for (int s = 0; s < NX; ++s) bcol[s] = sB[(kcl * NX + s) * NU + ic];
+            double a0[PA], a1[PA];
+            auto fetchA = [&](int kk, double* av) __attribute__((always_inline)) {
+                if constexpr (kPf) {
 #pragma unroll
-                for (int i = 0; i < PB; ++i) bn[i] = sB[i];
-            }
+                    for (int i = 0; i < PA; ++i) av[i] = sA[kk * NX * NX + i];
+                }
+            };
+            fetchA(0, a0);
+            auto stage = [&](auto tau_c, int kk, const double* av) __attribute__((always_inline)) {
+                constexpr int tau = decltype(tau_c)::value;
+                const double* Ak = sA + kk * NX * NX;
+                const double* Wk = sW + kk * NX * NX;
+                double wk[PA];
+                if constexpr (kPf) {
 #pragma unroll
-            for (int tau = 0; tau < T; ++tau) {
+                    for (int i = 0; i < PA; ++i) wk[i] = Wk[i];
+                }
+                auto A_ = [&](int i) __attribute__((always_inline)) {
+                    if constexpr (kPf) return av[i];
+                    else return Ak[i];
+                };
+                auto W_ = [&](int i) __attribute__((always_inline)) {
+                    if constexpr (kPf) return wk[i];
+                    else return Wk[i];
+                };
+                const bool inj = kk == kc;
+                double gn[NX];
+#pragma unroll
+                for (int s = 0; s < NX; ++s) {
+                    double v = 0.0;
+#pragma unroll
+                    for (int u = 0; u < NX; ++u) v = fma(A_(s * NX + u), g[u], v);
+                    gn[s] = inj ? bcol[s] : v;
+                }
+#pragma unroll
+                for (int s = 0; s < NX; ++s) g[s] = gn[s];
+                double gf[NXP], yf[NXP];
+                static_for<0, NXP>([&](auto s_c) __attribute__((always_inline)) {
+                    constexpr int s = decltype(s_c)::value;
+                    double y = 0.0;
+                    if constexpr (s < NX) {
+#pragma unroll
+                        for (int u = 0; u < NX; ++u) y = fma(W_(s * NX + u), g[u], y);
+                        gf[s] = g[s];
+                    } else {
+                        gf[s] = 0.0;
+                    }
+                    yf[s] = y;
+                });
+#pragma unroll
+                for (int q = 0; q < NXP; q += 4) {
+                    transpose_rows4(gf[q], gf[q + 1], gf[q + 2], gf[q + 3]);
+                    transpose_rows4(yf[q], yf[q + 1], yf[q + 2], yf[q + 3]);
+#pragma unroll
+                    for (int ti = 0; ti <= tau; ++ti)
+#pragma unroll
+                        for (int tj = 0; tj <= ti; ++tj)
+                            acc[ti * (ti + 1) / 2 + tj] = __builtin_amdgcn_mfma_f64_16x16x4f64(
+                                gf[q + ti], yf[q + tj], acc[ti * (ti + 1) / 2 + tj], 0, 0, 0);
+                }
+            };
+            static_for<0, T>([&](auto tau_c) __attribute__((always_inline)) {
+                constexpr int tau = decltype(tau_c)::value;
                 // stages whose Gamma_{k+1} has tiles 0..tau nonzero (last column (k+1)NU-1 in tile tau)
                 const int kb = (16 * tau + NU) / NU - 1;
                 const int ke0 = (16 * (tau + 1) + NU) / NU - 1;
                 const int ke = ke0 < N ? ke0 : N;
-                for (int kk = kb; kk < ke; ++kk) {
-                    const double* Ak = sA + kk * NX * NX;
-                    const double* Bk = sB + kk * NX * NU;
-                    const double* Wk = sW + kk * NX * NX;
-                    double ak[PA], bk[PB];
-                    if constexpr (kPf) {
-#pragma unroll
-                        for (int i = 0; i < PA; ++i) ak[i] = an[i];
-#pragma unroll
-                        for (int i = 0; i < PB; ++i) bk[i] = bn[i];
-                        const int kn = kk + 1 < N ? kk + 1 : kk;
-#pragma unroll
-                        for (int i = 0; i < PA; ++i) an[i] = sA[kn * NX * NX + i];
-#pragma unroll
-                        for (int i = 0; i < PB; ++i) bn[i] = sB[kn * NX * NU + i];
-                    }
-                    auto A_ = [&](int i) __attribute__((always_inline)) {
-                        if constexpr (kPf) return ak[i];
-                        else return Ak[i];
-                    };
-                    auto B_ = [&](int i) __attribute__((always_inline)) {
-                        if constexpr (kPf) return bk[i];
-                        else return Bk[i];
-                    };
-                    const int jj = col - kk * NU;
-                    double gn[NX];
-#pragma unroll
-                    for (int s = 0; s < NX; ++s) {
-                        double v = 0.0;
-#pragma unroll
-                        for (int i = 0; i < NU; ++i) {
-                            const double bv = B_(s * NU + i);  // unconditional load, register select
-                            v = (jj == i) ? bv : v;
-                        }
-#pragma unroll
-                        for (int u = 0; u < NX; ++u) v = fma(A_(s * NX + u), g[u], v);
-                        gn[s] = v;
-                    }
-#pragma unroll
-                    for (int s = 0; s < NX; ++s) g[s] = gn[s];
-                    double gf[NXP], yf[NXP];
-#pragma unroll
-                    for (int s = 0; s < NXP; ++s) {
-                        double y = 0.0;
-                        if (s < NX) {
-#pragma unroll
-                            for (int u = 0; u < NX; ++u) y = fma(Wk[s * NX + u], g[u], y);
-                        }
-                        gf[s] = s < NX ? g[s] : 0.0;
-                        yf[s] = y;
-                    }
-#pragma unroll
-                    for (int q = 0; q < NXP; q += 4) {
-                        transpose_rows4(gf[q], gf[q + 1], gf[q + 2], gf[q + 3]);
-                        transpose_rows4(yf[q], yf[q + 1], yf[q + 2], yf[q + 3]);
-#pragma unroll
-                        for (int ti = 0; ti <= tau; ++ti)
-#pragma unroll
-                            for (int tj = 0; tj <= ti; ++tj)
-                                acc[ti * (ti + 1) / 2 + tj] = __builtin_amdgcn_mfma_f64_16x16x4f64(
-                                    gf[q + ti], yf[q + tj], acc[ti * (ti + 1) / 2 + tj], 0, 0, 0);
-                    }
+                int kk = kb;
+                for (; kk + 1 < ke; kk += 2) {
+                    fetchA(kk + 1, a1);
+                    stage(tau_c, kk, a0);
+                    fetchA(kk + 2 < N ? kk + 2 : N - 1, a0);
+                    stage(tau_c, kk + 1, a1);
                 }
-            }
+                if (kk < ke) {
+                    fetchA(kk + 1 < N ? kk + 1 : N - 1, a1);
+                    stage(tau_c, kk, a0);
+#pragma unroll
+                    for (int i = 0; i < PA; ++i) a0[i] = a1[i];
+                }
+            });
         }
         STAMP(4);
         // + 2R + 2D'dR D (block tridiagonal) + input-row curvature; identity on the padding.
