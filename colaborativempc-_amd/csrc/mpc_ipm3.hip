@@ -715,9 +715,33 @@ __global__ __launch_bounds__(64, 1) void mpc_ipm3_kernel(const MpcConst c, const
             stop = kStopBreakdown;
             break;
         }
-        // this lane's diagonal block (J = lane >> 4) row / column (l & 15) of L_JJ, and its inverse diagonal
+        // diagonal blocks L_JJ -> L_JJ^{-1} in place (LDS, lower triangle; zeros above): row q of the
+        // wave inverts block q, lane (q, j) forms column j by forward substitution.  Done once per
+        // factorisation, it turns every in-block substitution of the four triangular solves per
+        // iteration (16 dependent broadcast -> multiply -> fma steps) into a 16-term mat-vec
+        {
+            const int q = l >> 4, j = l & 15;
+            double* Lq = Ld + (q < T ? q : 0) * 272;
+            double x[16];
+            static_for<0, 16>([&](auto i_c) __attribute__((always_inline)) {
+                constexpr int i = decltype(i_c)::value;
+                double s0 = (j == i) ? 1.0 : 0.0, s1 = 0.0;
+#pragma unroll
+                for (int c = 0; c < i; ++c) {
+                    if (c & 1) s1 = fma(-Lq[i * 17 + c], x[c], s1);
+                    else s0 = fma(-Lq[i * 17 + c], x[c], s0);
+                }
+                x[i] = (s0 + s1) * (1.0 / Lq[i * 17 + i]);
+            });
+            wsync();
+            if (q < T) {
+#pragma unroll
+                for (int i = 0; i < 16; ++i) Lq[i * 17 + j] = x[i];
+            }
+            wsync();
+        }
+        // this lane's diagonal block (J = lane >> 4) of L^{-1}: row / column (l & 15)
         const double* Lme = Ld + ((l >> 4) < T ? (l >> 4) : 0) * 272;
-        const double Ldinv = 1.0 / Lme[(l & 15) * 17 + (l & 15)];
 
         // ================= predictor / corrector =================
         double sig_c = 0.0, alpha = 0.0;
@@ -800,12 +824,14 @@ __global__ __launch_bounds__(64, 1) void mpc_ipm3_kernel(const MpcConst c, const
                 double Lr[16];
 #pragma unroll
                 for (int cc = 0; cc < 16; ++cc) Lr[cc] = Lme[(l & 15) * 17 + cc];
-                static_for<0, 16>([&](auto jc) __attribute__((always_inline)) {  // in-block substitution, row J broadcasts its lanes
-                    constexpr int cc = decltype(jc)::value;
-                    if ((l & 15) == cc) rv *= Ldinv;
-                    const double ycc = bcast16<cc>(rv);
-                    if ((l & 15) > cc) rv = fma(-Lr[cc], ycc, rv);
-                });
+                {  // y_J = L_JJ^{-1} r_J: row J broadcasts its lanes, four independent fma chains
+                    double y4[4] = {0.0, 0.0, 0.0, 0.0};
+                    static_for<0, 16>([&](auto jc) __attribute__((always_inline)) {
+                        constexpr int cc = decltype(jc)::value;
+                        y4[cc & 3] = fma(Lr[cc], bcast16<cc>(rv), y4[cc & 3]);
+                    });
+                    rv = (y4[0] + y4[1]) + (y4[2] + y4[3]);
+                }
                 if ((l >> 4) == J) vb[J * 16 + (l & 15)] = rv;
                 wsync();
             }
@@ -823,12 +849,14 @@ __global__ __launch_bounds__(64, 1) void mpc_ipm3_kernel(const MpcConst c, const
                 double Lc[16];
 #pragma unroll
                 for (int cc = 0; cc < 16; ++cc) Lc[cc] = Lme[cc * 17 + (l & 15)];
-                static_for<0, 16>([&](auto jc) __attribute__((always_inline)) {
-                    constexpr int cc = 15 - decltype(jc)::value;
-                    if ((l & 15) == cc) rv *= Ldinv;
-                    const double xcc = bcast16<cc>(rv);
-                    if ((l & 15) < cc) rv = fma(-Lc[cc], xcc, rv);
-                });
+                {  // x_J = L_JJ^{-T} r_J
+                    double x4[4] = {0.0, 0.0, 0.0, 0.0};
+                    static_for<0, 16>([&](auto jc) __attribute__((always_inline)) {
+                        constexpr int cc = decltype(jc)::value;
+                        x4[cc & 3] = fma(Lc[cc], bcast16<cc>(rv), x4[cc & 3]);
+                    });
+                    rv = (x4[0] + x4[1]) + (x4[2] + x4[3]);
+                }
                 if ((l >> 4) == J) vb[J * 16 + (l & 15)] = rv;
                 wsync();
             }

@@ -21,33 +21,24 @@ __device__ __forceinline__ double readlane_d(double v, int lane) {
 // NaN-propagating max: a NaN residual must never look converged (fmax drops NaNs).
 __device__ __forceinline__ double nmax(double a, double b) { return (a > b || a != a) ? a : b; }
 
-__device__ __forceinline__ double wave_max(double v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v = nmax(v, __shfl_xor(v, o));
-    return v;
+// Cross-lane reductions without LDS (a __shfl_xor of a double is two ds_bpermute plus a full
+// lgkmcnt wait per step): DPP row rotations within a row of 16 lanes, then the permlane
+// row swaps across rows.  Every stage combines commutatively, so all lanes end with the
+// bit-identical value (the solver's wave-uniform decisions rely on it).
+template <int N>
+__device__ __forceinline__ double ror16(double x) {
+    return __builtin_amdgcn_update_dpp(0.0, x, 0x120 + N, 0xF, 0xF, true);  // row_ror:N
 }
-__device__ __forceinline__ double wave_min(double v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v = fmin(v, __shfl_xor(v, o));
-    return v;
+template <class Op>
+__device__ __forceinline__ double row_reduce(double v, Op op) {
+    v = op(v, ror16<8>(v));
+    v = op(v, ror16<4>(v));
+    v = op(v, ror16<2>(v));
+    return op(v, ror16<1>(v));
 }
-__device__ __forceinline__ double wave_sum(double v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
-    return v;
-}
-// sum over the 16 lanes that share (lane >> 4)
-__device__ __forceinline__ double sum16(double v) {
-#pragma unroll
-    for (int o = 8; o > 0; o >>= 1) v += __shfl_xor(v, o);
-    return v;
-}
-// sum over the 4 lanes that share (lane & 15)
-__device__ __forceinline__ double sum_groups(double v) {
-    v += __shfl_xor(v, 16);
-    v += __shfl_xor(v, 32);
-    return v;
-}
+__device__ __forceinline__ double add_(double a, double b) { return a + b; }
+__device__ __forceinline__ double min_(double a, double b) { return fmin(a, b); }
+__device__ __forceinline__ double nmax_(double a, double b) { return nmax(a, b); }
 
 __device__ __forceinline__ unsigned long long clock64_() { return __builtin_amdgcn_s_memtime(); }
 
@@ -97,6 +88,25 @@ __device__ __forceinline__ void swap_odd(double& a, double& b) {
     a = __builtin_bit_cast(double, (unsigned long long)lo[0] | ((unsigned long long)hi[0] << 32));
     b = __builtin_bit_cast(double, (unsigned long long)lo[1] | ((unsigned long long)hi[1] << 32));
 }
+
+// over the 4 rows (lanes sharing l & 15)
+template <class Op>
+__device__ __forceinline__ double rows_reduce(double v, Op op) {
+    double a = v, b = v;
+    swap_odd(a, b);  // a: rows (0,0,2,2), b: rows (1,1,3,3)
+    v = op(a, b);
+    a = v;
+    b = v;
+    swap_half(a, b);  // a: rows (0,1,0,1), b: rows (2,3,2,3)
+    return op(a, b);
+}
+__device__ __forceinline__ double wave_max(double v) { return rows_reduce(row_reduce(v, nmax_), nmax_); }
+__device__ __forceinline__ double wave_min(double v) { return rows_reduce(row_reduce(v, min_), min_); }
+__device__ __forceinline__ double wave_sum(double v) { return rows_reduce(row_reduce(v, add_), add_); }
+// sum over the 16 lanes that share (lane >> 4)
+__device__ __forceinline__ double sum16(double v) { return row_reduce(v, add_); }
+// sum over the 4 lanes that share (lane & 15)
+__device__ __forceinline__ double sum_groups(double v) { return rows_reduce(v, add_); }
 
 // 4x4 transpose of (register, 16-lane row): on return r[t] holds, in row k, what r[k] held in
 // row t.  With lane c carrying column c of a 4 x 64 matrix M in r[0..3], r[t] becomes the
