@@ -655,7 +655,7 @@ __global__ __launch_bounds__(64, 1) void mpc_ipm3_kernel(const MpcConst c, const
                         constexpr int c2 = decltype(cc)::value;
                         rw[c2] = fma(-lj, bcast16<c2>(lj), rw[c2]);
                     });
-                    __builtin_amdgcn_sched_barrier(0);  // keep the pivot steps' live ranges apart
+                    // (no scheduling barrier: the next pivot overlaps this one's trailing updates)
                 });
             }
             if (l < 16) {
@@ -684,7 +684,7 @@ __global__ __launch_bounds__(64, 1) void mpc_ipm3_kernel(const MpcConst c, const
                                 if (i16 > cc) v = fma(-ycc, lcc, v);
                                 acc[I * (I + 1) / 2 + J][r] = v;
                             }
-                        __builtin_amdgcn_sched_barrier(0);
+                        // (no scheduling barrier between panel columns)
                     });
                 }
                 // stacked panel rows to LDS for the transposed MFMA operands of the SYRK
