@@ -431,8 +431,12 @@ __global__ __launch_bounds__(64, 1) void mpc_ipm3_kernel(const MpcConst c, const
         }
 
         // ================= Newton matrix K = Gamma' W Gamma + Hc + diag =================
+        // 1 / t_r once per iteration (theta and both passes' rho use it)
+        double tin[RX];
 #pragma unroll
-        for (int r = 0; r < RX; ++r) th[r] = ACT(r) ? lam[r] / t[r] : 0.0;
+        for (int r = 0; r < RX; ++r) tin[r] = ACT(r) ? 1.0 / t[r] : 0.0;
+#pragma unroll
+        for (int r = 0; r < RX; ++r) th[r] = lam[r] * tin[r];
 #pragma unroll
         for (int j = 0; j < NS; ++j) {
             double v = Qs2[j];
@@ -760,7 +764,7 @@ __global__ __launch_bounds__(64, 1) void mpc_ipm3_kernel(const MpcConst c, const
                     const double dla = rho[r] + th[r] * (gdu[r] + sd);
                     rc += sig_c * mu - dta * dla;
                 }
-                rho[r] = (rc + lam[r] * rp[r]) / t[r];
+                rho[r] = (rc + lam[r] * rp[r]) * tin[r];
             }
             // rho~ (stable slack-group form) of the stage rows enters only through C' rho~
             if (lo && own) {
@@ -885,8 +889,9 @@ __global__ __launch_bounds__(64, 1) void mpc_ipm3_kernel(const MpcConst c, const
                 const double sd = sdr(r);
                 const double dtv = -rp[r] - gdu[r] - sd;
                 const double dlv = rho[r] + th[r] * (gdu[r] + sd);
-                if (dtv < 0.0) amax_l = fmin(amax_l, -t[r] / dtv);
-                if (dlv < 0.0) amax_l = fmin(amax_l, -lam[r] / dlv);
+                // ratio tests by the hardware reciprocal: the step is cut to 0.995 of it anyway
+                if (dtv < 0.0) amax_l = fmin(amax_l, -t[r] * __builtin_amdgcn_rcp(dtv));
+                if (dlv < 0.0) amax_l = fmin(amax_l, -lam[r] * __builtin_amdgcn_rcp(dlv));
             }
             const double amax = wave_min(amax_l);
             if (!pass) {

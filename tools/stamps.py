@@ -35,6 +35,8 @@ R.solve()
 ev[1].record()
 torch.cuda.synchronize()
 a = st.cpu().numpy().astype(np.float64)
+print("stamped run: status", dict(zip(*np.unique(R.status.cpu().numpy(), return_counts=True))),
+      "kkt max", float(R.kkt.max()), "iters", dict(zip(*np.unique(R.iters.cpu().numpy(), return_counts=True))))
 it = a[:, SLOTS - 1]
 tot = a[:, :SLOTS - 1].sum(1)
 print(f"agents {n} N {N}: kernel {ev[0].elapsed_time(ev[1]):.3f} ms (with stamps); iters mean {it.mean():.2f} "
