@@ -671,25 +671,31 @@ __global__ __launch_bounds__(64, 1) void mpc_ipm3_kernel(const MpcConst c, const
             if (J + 1 < T) {
                 // panel TRSM in the accumulator layout: L_IJ = K_IJ L_JJ^{-T} column by column; lane l
                 // holds column (l & 15) of every panel tile, its own row of L_JJ in rw (lane = row), so
-                // L[l & 15][cc] = rw[cc] and Y[:, cc] reaches the row of 16 lanes by DPP row_newbcast
+                // L[l & 15][cc] = rw[cc] and Y[:, cc] reaches the row of 16 lanes by DPP row_newbcast.
+                // Unscaled form: with y_c = x_c L_cc the update is k_i -= y_c (L_ic / L_cc) for i > c
+                // (a zero multiplier elsewhere), so each step is one broadcast and one fma per value;
+                // x = y / L_ii once at the end
                 {
                     const int i16 = l & 15;
                     const double inv_own = 1.0 / S0[i16 * 17 + i16];
                     static_for<0, 16>([&](auto jc) __attribute__((always_inline)) {
                         constexpr int cc = decltype(jc)::value;
-                        const double lcc = rw[cc];
+                        // the broadcast stays outside the select: under a divergent EXEC mask the
+                        // source lane cc would be inactive (DPP then reads 0)
+                        const double dcc = bcast16<cc>(inv_own);
+                        const double lcc = (i16 > cc) ? rw[cc] * dcc : 0.0;
 #pragma unroll
                         for (int I = J + 1; I < T; ++I)
 #pragma unroll
                             for (int r = 0; r < 4; ++r) {
-                                double v = acc[I * (I + 1) / 2 + J][r];
-                                if (i16 == cc) v *= inv_own;
-                                const double ycc = bcast16<cc>(v);
-                                if (i16 > cc) v = fma(-ycc, lcc, v);
-                                acc[I * (I + 1) / 2 + J][r] = v;
+                                const double v = acc[I * (I + 1) / 2 + J][r];
+                                acc[I * (I + 1) / 2 + J][r] = fma(-bcast16<cc>(v), lcc, v);
                             }
-                        // (no scheduling barrier between panel columns)
                     });
+#pragma unroll
+                    for (int I = J + 1; I < T; ++I)
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) acc[I * (I + 1) / 2 + J][r] *= inv_own;
                 }
                 // stacked panel rows to LDS for the transposed MFMA operands of the SYRK
 #pragma unroll

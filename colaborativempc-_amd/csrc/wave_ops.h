@@ -54,7 +54,8 @@ __device__ __forceinline__ void static_for(F&& f) {
 // Lane J of each row of 16 lanes, broadcast to the whole row: one v_mov_b64_dpp row_newbcast:J
 // (no SGPR round trip, unlike v_readlane).  Every lane reads a valid source lane, so the old
 // value is dead: bound_ctrl with old = 0 lets the compiler drop the copy of x it otherwise
-// makes into the destination first.
+// makes into the destination first.  Call it with the whole wave active (never inside a
+// divergent branch or select arm): a disabled source lane reads as 0.
 template <int J>
 __device__ __forceinline__ double bcast16(double x) {
     static_assert(J >= 0 && J < 16, "row_newbcast lane");
