@@ -270,9 +270,14 @@ __global__ __launch_bounds__(64, 1) void mpc_ipm3_kernel(const MpcConst c, const
     const bool own = k < N;
     double t[RX], lam[RX], th[RX], rp[RX], rho[RX], gdu[RX];
     unsigned actm = 0;  // bit r: row r of this lane exists and has a finite bound
+    // rows are evaluated branch-free: every LDS read is unconditional (indices of lanes that
+    // own no such row stay inside the LDS allocation and are masked afterwards); a read inside a
+    // select arm cannot be speculated, and each became a divergent branch with its own wait
     auto wv = [&](int r) -> double {
-        if (lo) return sH[k * MC + r];
-        return (r & 1) ? -lb[r >> 1] : ub[r >> 1];
+        const double h = sH[k * MC + r];
+        const double bl = lb[r >> 1], bu = ub[r >> 1];
+        const double wi = (r & 1) ? -bl : bu;
+        return lo ? h : wi;
     };
     double sg[NS] = {0.0, 0.0, 0.0};
     wsync();
@@ -287,17 +292,18 @@ __global__ __launch_bounds__(64, 1) void mpc_ipm3_kernel(const MpcConst c, const
 
     // value of row r at (Xv, Uv[, sig]) for this lane's rows
     auto rowval = [&](int r, const double* Xv, const double* Uv, bool with_sig) -> double {
-        if (lo) {
-            const double* cr = sC + (k * MC + r) * NX;
-            const double* xk = Xv + (k + 1) * NX;
-            double v = 0.0;
+        const double* cr = sC + (k * MC + r) * NX;
+        const double* xk = Xv + (k + 1) * NX;
+        double v = 0.0;
 #pragma unroll
-            for (int s = 0; s < NX; ++s) v = fma(cr[s], xk[s], v);
-            if (with_sig && slk(r) >= 0) v += sgn(r) * sg[slk(r)];
-            return v;
+        for (int s = 0; s < NX; ++s) {
+            const double cs = cr[s], xs = xk[s];
+            v = fma(cs, xs, v);
         }
+        if (with_sig && slk(r) >= 0) v += sgn(r) * sg[slk(r)];
         const double u = Uv[k * NU + (r >> 1)];
-        return (r & 1) ? -u : u;
+        const double uu = (r & 1) ? -u : u;
+        return lo ? v : uu;
     };
 
     double mact_l = 0.0, sp_l = 1.0;
@@ -395,8 +401,9 @@ __global__ __launch_bounds__(64, 1) void mpc_ipm3_kernel(const MpcConst c, const
         }
 #pragma unroll
         for (int r = 0; r < RX; ++r) {
+            const double rvr = rowval(r, X, U, true), wr = wv(r);
             if (ACT(r)) {
-                rp[r] = rowval(r, X, U, true) + t[r] - wv(r);
+                rp[r] = rvr + t[r] - wr;
                 nrp_l = nmax(nrp_l, fabs(rp[r]));
                 mu_l += t[r] * lam[r];
             } else {
@@ -877,7 +884,10 @@ __global__ __launch_bounds__(64, 1) void mpc_ipm3_kernel(const MpcConst c, const
             wsync();
             STAMP(11);
 #pragma unroll
-            for (int r = 0; r < RX; ++r) gdu[r] = ACT(r) ? rowval(r, dX, dU, false) : 0.0;
+            for (int r = 0; r < RX; ++r) {
+                const double rvr = rowval(r, dX, dU, false);
+                gdu[r] = ACT(r) ? rvr : 0.0;
+            }
 #pragma unroll
             for (int j = 0; j < NS; ++j) {
                 double v = rsig[j];
