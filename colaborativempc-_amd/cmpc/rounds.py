@@ -91,6 +91,12 @@ class DIRounds:
                                                           self.C, self.h)])
         self.out = L.cmpc_mpc_out(_tptr(self.z), _tptr(self.kkt), _tptr(self.iters), _tptr(self.status))
 
+    def bind_outputs(self, kkt, iters, status):
+        """Point the solver's per-agent kkt / iters / status outputs at other (B,) device
+        tensors (e.g. one row per round of a preallocated history), without copies."""
+        self.kkt, self.iters, self.status = kkt, iters, status
+        self.out = L.cmpc_mpc_out(_tptr(self.z), _tptr(kkt), _tptr(iters), _tptr(status))
+
     def _stream(self):
         return ct.c_void_p(self.torch.cuda.current_stream(self.dev).cuda_stream)
 
