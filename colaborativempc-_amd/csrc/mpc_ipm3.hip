@@ -748,7 +748,7 @@ __global__ __launch_bounds__(64, 1) void mpc_ipm3_kernel(const MpcConst c, const
                     if (c & 1) s1 = fma(-Lq[i * 17 + c], x[c], s1);
                     else s0 = fma(-Lq[i * 17 + c], x[c], s0);
                 }
-                x[i] = (s0 + s1) * (1.0 / Lq[i * 17 + i]);
+                x[i] = (s0 + s1) * rcp_d(Lq[i * 17 + i]);
             });
             wsync();
             if (q < T) {

@@ -70,6 +70,14 @@ __device__ __forceinline__ double rsqrt_d(double x) {
     return y;
 }
 
+// 1/x to full double precision: hardware estimate + two Newton steps (no IEEE divide sequence).
+__device__ __forceinline__ double rcp_d(double x) {
+    double r = __builtin_amdgcn_rcp(x);
+    r = fma(r, fma(-x, r, 1.0), r);
+    r = fma(r, fma(-x, r, 1.0), r);
+    return r;
+}
+
 // CDNA4 row exchanges on doubles (one instruction per dword):
 //  swap_half: lanes 32..63 of a <-> lanes 0..31 of b   (v_permlane32_swap)
 //  swap_odd:  odd 16-lane rows of a <-> even rows of b  (v_permlane16_swap)

@@ -176,6 +176,36 @@ def test_deterministic_and_permutation_invariant(gpu_ctx):
     assert np.array_equal(zp, z1[perm])
 
 
+def test_stamped_solve_is_bit_identical(gpu_ctx):
+    """The per-section clock stamps (cmpc_opts.stamps) add only timing code: the solve with
+    stamps must reproduce the plain solve bit for bit.  This caught a DPP broadcast placed
+    under a divergent EXEC mask (its source lane disabled), which only showed in one layout."""
+    import torch
+
+    import cmpc
+    from cmpc import _lib as L
+    from cmpc import scenarios as S
+    from cmpc.rounds import DIRounds
+
+    R = DIRounds(S.make_di(1024, 30, 2, 2), ctx=gpu_ctx)
+    for _ in range(2):  # round 0 and a round with active coupling rows
+        R.build()
+        R.opts = L.opts()
+        R.solve()
+        torch.cuda.synchronize()
+        z0, it0, st0 = R.z.clone(), R.iters.clone(), R.status.clone()
+        stamps = torch.zeros((R.B, 16), dtype=torch.int64, device=R.z.device)
+        R.opts = L.opts(stamps=stamps.data_ptr())
+        R.solve()
+        torch.cuda.synchronize()
+        assert torch.equal(R.z, z0) and torch.equal(R.iters, it0) and torch.equal(R.status, st0)
+        assert ((st0 == cmpc.CMPC_SOLVED) | (st0 == cmpc.CMPC_SOLVED_INACCURATE)).all()
+        assert int(stamps[:, :15].sum()) > 0
+        R.opts = L.opts()
+        R.advance()
+        R.exchange()
+
+
 def test_edge_cases(gpu_ctx):
     import cmpc
     from cmpc import scenarios as S
