@@ -32,7 +32,7 @@ HBM_PEAK_GBS = 8000.0
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--agents", type=int, default=1024, help="agents per GPU")
     ap.add_argument("--horizon", type=int, default=30)
@@ -108,14 +108,7 @@ def main():
     flops = S.alg_flops(nx, nu, N, m_rows, mean_iters)
     achieved_tf = flops * args.agents / (kern_ms * 1e-3) / 1e12
     alg_bytes = S.di_alg_bytes(nx, nu, N, args.nb)
-    traffic = None
-    pmc = os.path.join(ROOT, "profiles", "pmc_r01.json")
-    if os.path.exists(pmc):
-        try:
-            with open(pmc) as f:
-                traffic = json.load(f).get("solve_kernel", {}).get("hbm_bytes_per_launch")
-        except Exception:
-            traffic = None
+    traffic, traffic_src = pmc_traffic()
 
     cpu = None
     max_err = None
@@ -155,6 +148,7 @@ def main():
                 "unit": "TFLOP/s",
                 "frac": achieved_tf / FP64_PEAK_TFLOPS,
                 "traffic": traffic,
+                "traffic_source": traffic_src,
                 "kernel_ms_per_launch": kern_ms,
                 "alg_flops_per_qp": flops,
                 "alg_bytes_per_qp": alg_bytes,
@@ -168,42 +162,90 @@ def main():
         dist.destroy_process_group()
 
 
-def cpu_baseline(R, seconds):
-    """The oracle's plain-C restatement (oracle/cmpc_oracle.c, OpenMP) on a bounded
-    sample of the SAME round problem the GPU solves: build the current round on the
-    device, copy it to the host, time the CPU solve of the first S agents."""
+def pmc_traffic():
+    """HBM bytes per solver launch from the newest committed PMC summary (profiles/pmc_r*.json,
+    FETCH_SIZE and WRITE_SIZE in separate rocprofv3 --pmc passes, tools/prof_summary.py).  PMC
+    counters cannot be collected inside this process, so the figure carries its provenance:
+    the commit it was measured at, and "stale" = whether the kernel sources (sha256 over
+    csrc/ and cmpc.h) differ from the ones that were profiled."""
+    import glob
+
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    from prof_summary import solver_sources_sha
+
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "pmc_r*.json")))
+    if not files:
+        return None, None
+    try:
+        with open(files[-1]) as f:
+            rec = json.load(f)
+        traffic = rec.get("solve_kernel", {}).get("hbm_bytes_per_launch")
+    except (OSError, ValueError):
+        return None, None
+    sha = rec.get("sources_sha")
+    return traffic, {"file": os.path.relpath(files[-1], ROOT), "commit": rec.get("commit"),
+                     "stale": None if sha is None else sha != solver_sources_sha()}
+
+
+def host_cpu():
+    """(model name, nproc, usable CPUs) of this host."""
+    model = None
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    nproc = os.cpu_count() or 1
+    usable = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else nproc
+    return model, nproc, usable
+
+
+def cpu_baseline(R, seconds, rounds=4):
+    """The oracle's plain-C restatement (oracle/cmpc_oracle.c, OpenMP, one agent-QP per
+    thread) timed on this host over whole rounds of the SAME workload the GPU solves:
+    `rounds` consecutive consensus rounds are built and solved on the device, each round's
+    full structured problem (every agent of this rank) is copied to the host, and the CPU
+    solves all of them, repeated until about `seconds` of CPU time.  Threads: every CPU this
+    process may use, capped by OMP_NUM_THREADS when it is set (the GPU box grants each job a
+    16-CPU share of a larger host, so nproc there is not the usable count)."""
     import torch
 
     from oracle import cmpc_oracle as CO
 
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
-    R.build()
-    prob = R.snapshot()
-    R.solve()
-    torch.cuda.synchronize()
-    zg = R.z.cpu().numpy()
-
-    def take(n):
-        p = dict(prob)
-        for k in ("A", "B", "x0", "u_prev", "qlin", "C", "h"):
-            p[k] = prob[k][:n]
-        return p
-
-    B = prob["A"].shape[0]
-    n0 = min(B, 4 * threads)
+    model, nproc, usable = host_cpu()
+    env = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    threads = min(usable, env) if env > 0 else usable
+    probs, zs = [], []
+    for _ in range(rounds):
+        R.build()
+        probs.append(R.snapshot())
+        R.solve()
+        torch.cuda.synchronize()
+        zs.append(R.z.cpu().numpy().copy())
+        R.advance()
+        R.exchange()
+    B = probs[0]["A"].shape[0]
+    err = 0.0
     t = time.perf_counter()
-    CO.solve_batch(take(n0), nthreads=threads)
-    dt0 = time.perf_counter() - t
-    reps = max(1, int(seconds / max(dt0, 1e-6)))
-    # sample = `reps` passes over the first n0 agents (bounded CPU time), plus one full-batch check
-    t = time.perf_counter()
-    for _ in range(reps):
-        zc, _, _, _ = CO.solve_batch(take(n0), nthreads=threads)
-    el = time.perf_counter() - t
-    err = float(np.abs(zg[:n0] - zc).max())
-    return ({"value": reps * n0 / el, "unit": "agent-QP/s", "cores": threads, "kind": "port",
-             "sample": f"{reps} x {n0} agents of one cfg3 round (same device-built problems), "
-                       f"oracle/cmpc_oracle.c fp64, OpenMP {threads} threads, {el:.1f} s"}, err)
+    passes = 0
+    while True:
+        for p, zg in zip(probs, zs):
+            zc, _, _, _ = CO.solve_batch(p, nthreads=threads)
+            if passes == 0:
+                err = max(err, float(np.abs(zg - zc).max()))
+        passes += 1
+        el = time.perf_counter() - t
+        if el >= seconds:
+            break
+    solved = passes * rounds * B
+    return ({"value": solved / el, "unit": "agent-QP/s", "cores": threads, "kind": "port",
+             "nproc": nproc, "cpu_model": model,
+             "sample": f"{passes} pass(es) over {rounds} consecutive full cfg3 rounds of {B} agents "
+                       f"(device-built problems copied to the host), oracle/cmpc_oracle.c fp64, OpenMP "
+                       f"{threads} threads, {el:.1f} s"}, err)
 
 
 if __name__ == "__main__":

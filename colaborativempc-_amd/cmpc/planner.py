@@ -3,7 +3,8 @@
 ``PlannerLPV`` has the constructor and ``solve`` signature of the reference's
 ``plan_lib.distributedPlanner.PlannerLPV`` (planner/lib/plan_lib/
 distributedPlanner/LPV_Planner.py:15-182) and sets the same attributes
-(xPred, uPred, sPred, raw_States, planes, weights, OldSteering, OldAccelera), so
+(xPred, uPred, duPred, sPred, raw_States, planes, weights, dist, OldSteering,
+OldAccelera), so
 an agent loop written against the reference runs unchanged.  Every call goes
 through libcmpc's fused GPU path (cmpc_solve_lpv_batch): LPV scheduling,
 hyperplanes, weights, QP build and the condensed interior-point solve all run
@@ -103,14 +104,37 @@ class PlannerLPVBatch:
 
 
 def unpack(z, N):
-    """Solution unpacking of LPV_Planner.py:164-178 (xPred, uPred, duPred, sPred, raw_States)."""
+    """Solution unpacking of LPV_Planner.py:164-178 (xPred, uPred, duPred, sPred, raw_States).
+
+    ``duPred`` keeps the reference's index expression verbatim (:175):
+    ``n_exp(N+1) + arange(n_u N) + arange(n_u N)`` = base + 2 j, i.e. every other entry of
+    the [u | du] block, so it holds the steering components of u_0..u_{N-1} followed by
+    those of du_0..du_{N-1} — not the input rates.  Nothing downstream of the reference
+    reads it; the true rates are z[base + n_u N : base + 2 n_u N] (``du_of``)."""
     xi = z[: N_EXP * (N + 1)].reshape(N + 1, N_EXP)
     x_pred = xi[:, :N_S].copy()
     s_pred = xi[1:, N_S:].copy()
     base = N_EXP * (N + 1)
     u_pred = z[base: base + N_U * N].reshape(N, N_U).copy()
-    du_pred = z[base + N_U * N: base + 2 * N_U * N].reshape(N, N_U).copy()
+    j = np.arange(N_U * N)
+    du_pred = z[base + j + j].reshape(N, N_U).copy()
     return x_pred, u_pred, du_pred, s_pred, xi.copy()
+
+
+def du_of(z, N):
+    """The input rates du_0..du_{N-1} of a reference-layout solution (N, n_u)."""
+    base = N_EXP * (N + 1) + N_U * N
+    return z[base: base + N_U * N].reshape(N, N_U).copy()
+
+
+def weights_of(pose, x_agents, min_dist):
+    """compute_weights (utilities/misc.py:10-18): dist[h, i] = ||pose[h+1] - x_agents[h+1, i]||,
+    weights = (2 D - dist) / nb, both (N, nb)."""
+    pose = np.asarray(pose, float)
+    xa = np.asarray(x_agents, float)
+    nb = xa.shape[1]
+    d = np.sqrt((pose[1:, None, 0] - xa[1:, :, 0]) ** 2 + (pose[1:, None, 1] - xa[1:, :, 1]) ** 2)
+    return (2 * min_dist - d) / nb, d
 
 
 def feasible_of(status):
@@ -159,11 +183,16 @@ class PlannerLPV:
         if feasible == 0:
             print("QUIT...")
         Solution = res["z"][0]
-        if x_agents is None:
+        if status == L.CMPC_UNSOLVED and np.isnan(Solution).all():
+            # the builder's track-segment lookup failed; the reference raises there (misc.py:97)
+            raise ValueError("curvature/get_ey: s of the previous prediction lies on no single track segment")
+        if x_agents is None:   # LPV_Planner.py:132-135
             self.planes = np.zeros((self.N, self.n_agents, 3))
             self.weights = np.ones((self.N, self.n_agents))
-        else:
+            self.dist = -self.weights
+        else:                  # :137-139
             self.planes = res["planes"][0]
+            self.weights, self.dist = weights_of(pose, x_agents, self.min_dist)
         self.xPred, self.uPred, self.duPred, self.sPred, self.raw_States = unpack(Solution, self.N)
         self.OldSteering = [self.uPred[0, 0]]
         self.OldAccelera = [self.uPred[0, 1]]

@@ -59,9 +59,11 @@ def quadprog(H, f, A=None, b=None, Aeq=None, beq=None, lb=None, ub=None, ctx=Non
     f = prep(f, (n,), "f")
     if f is None:
         raise ValueError("f is required")
-    A_ = None if A is None or np.size(A) == 0 else _dense(A)
+    # emptiness by shape: np.size of a scipy sparse matrix is its nnz, and a sparse G with no
+    # stored entries still carries its rows (and their right-hand sides)
+    A_ = None if A is None or 0 in np.shape(A) else _dense(A)
     mi = 0 if A_ is None else A_.shape[-2]
-    Aeq_ = None if Aeq is None or np.size(Aeq) == 0 else _dense(Aeq)
+    Aeq_ = None if Aeq is None or 0 in np.shape(Aeq) else _dense(Aeq)
     me = 0 if Aeq_ is None else Aeq_.shape[-2]
     A_ = prep(A_, (mi, n), "A")
     b_ = prep(b, (mi,), "b") if mi else None
@@ -97,7 +99,9 @@ def quadprog(H, f, A=None, b=None, Aeq=None, beq=None, lb=None, ub=None, ctx=Non
 def osqp_solve_qp(P, q, G=None, h=None, A=None, b=None, initvals=None, ctx=None):
     """Drop-in for the reference's ``osqp_solve_qp`` (LPV_Planner.py:192-249): the same QP
     (min 1/2 x'Px + q'x s.t. G x <= h, A x = b) solved on the GPU.  ``initvals`` is accepted
-    and ignored, as in the reference (it never warm-starts OSQP).  Returns (res, feasible)."""
+    but unused: the reference passes it to ``osqp.warm_start`` (:237-238), while the
+    interior-point method here starts from its own interior point (the caller in the
+    reference, PlannerLPV.solve :156-157, never passes it).  Returns (res, feasible)."""
     r = quadprog(P, q, G, h, A, b, ctx=ctx)
     flags = np.atleast_1d(r["exitflag"])
     out = []

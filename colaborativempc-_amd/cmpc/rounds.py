@@ -94,6 +94,12 @@ class DIRounds:
     def bind_outputs(self, kkt, iters, status):
         """Point the solver's per-agent kkt / iters / status outputs at other (B,) device
         tensors (e.g. one row per round of a preallocated history), without copies."""
+        torch = self.torch
+        for name, t, dt in (("kkt", kkt, torch.float64), ("iters", iters, torch.int32),
+                            ("status", status, torch.int32)):
+            if not isinstance(t, torch.Tensor) or t.device != self.dev or t.dtype != dt or \
+                    tuple(t.shape) != (self.B,) or not t.is_contiguous():
+                raise ValueError(f"{name}: need a contiguous ({self.B},) {dt} tensor on {self.dev}")
         self.kkt, self.iters, self.status = kkt, iters, status
         self.out = L.cmpc_mpc_out(_tptr(self.z), _tptr(kkt), _tptr(iters), _tptr(status))
 

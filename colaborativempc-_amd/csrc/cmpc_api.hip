@@ -229,7 +229,7 @@ static int lpv_run(cmpc_ctx* ctx, const cmpc_lpv_params* prm, const cmpc_track* 
     HIP_TRY(cmpc::lpv_build_launch(lc, lp, d->batch, s));
     cmpc::MpcPtrs mp{A, Bm, in->x0, in->u_old, p, C, h, out->z, out->kkt, out->iters, out->status, nullptr};
     HIP_TRY(cmpc::mpc_launch(mc, mp, d->batch, s, opts ? opts->flags : 0));
-    if (out->status) HIP_TRY(cmpc::lpv_mark_launch(err, out->status, d->batch, s));
+    HIP_TRY(cmpc::lpv_mark_launch(err, out->status, out->z, (int)(12 * (N + 1) + 4 * N), d->batch, s));
     return CMPC_OK;
 }
 

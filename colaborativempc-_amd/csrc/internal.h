@@ -22,7 +22,6 @@ struct MpcConst {
     int npad;   // n rounded up to 16 (MFMA tile)
     int ldk;    // leading dimension of the LDS Hessian (odd)
     int max_iter;
-    int debug;  // CMPC_FLAG_DEBUG: dump the first Newton matrix into opts->stamps
     int wg;     // 0: one-wave kernels; 1: workgroup kernel in fp64 (N*nu > 64); 2: workgroup kernel in fp32
     double tol;
     double qs_max;  // max(1, 2*max(Qs)) — slack residual scale
@@ -109,8 +108,9 @@ struct LpvPtrs {
 };
 
 hipError_t lpv_build_launch(const LpvConst& c, const LpvPtrs& p, int batch, hipStream_t s);
-// status[b] = CMPC_UNSOLVED where the builder flagged agent b (track lookup failed).
-hipError_t lpv_mark_launch(const int* err, int* status, int batch, hipStream_t s);
+// Where the builder flagged agent b (track lookup failed, the reference raises): status[b] =
+// CMPC_UNSOLVED (status may be null) and z[b, :] = NaN.
+hipError_t lpv_mark_launch(const int* err, int* status, double* z, int nz, int batch, hipStream_t s);
 
 // Synthetic double-integrator family (bench workload).
 struct DiConst {

@@ -96,7 +96,20 @@ __global__ __launch_bounds__(kWave) void lpv_build_kernel(const LpvConst c, cons
         const double vx = st[0], vy = st[1], eyv = st[3], epsi = st[4], theta = st[5], sv = st[6];
         const int sg = seg_lookup(c, sv);
         if (sg < 0) {
+            // the reference raises here (misc.py:97): write a defined stage (A = I, B = 0, zero
+            // half-width) so the solver runs on known data, and flag the agent; lpv_mark_kernel
+            // then reports it CMPC_UNSOLVED and NaN-fills its z
             bad = 1;
+            double* Ak = A + (size_t)h1 * 81;
+            for (int i = 0; i < 81; ++i) Ak[i] = (i % 10) == 0 ? 1.0 : 0.0;
+            double* Bk = B + (size_t)h1 * 18;
+            for (int i = 0; i < 18; ++i) Bk[i] = 0.0;
+            for (int r = 0; r < 4; ++r)
+                for (int s = 0; s < 9; ++s) Ck[r * 9 + s] = 0.0;
+            Ck[0 * 9 + 0] = -1.0; hk[0] = -c.min_vel;
+            Ck[1 * 9 + 0] = 1.0;  hk[1] = c.max_vel;
+            Ck[2 * 9 + 3] = 1.0;  hk[2] = 0.0;
+            Ck[3 * 9 + 3] = -1.0; hk[3] = 0.0;
             continue;
         }
         const double cur = c.curv[sg];
@@ -153,14 +166,16 @@ hipError_t lpv_build_launch(const LpvConst& c, const LpvPtrs& p, int batch, hipS
     return hipGetLastError();
 }
 
-__global__ void lpv_mark_kernel(const int* err, int* status, int batch) {
-    const int b = blockIdx.x * blockDim.x + threadIdx.x;
-    if (b < batch && err[b]) status[b] = CMPC_UNSOLVED;
+__global__ void lpv_mark_kernel(const int* err, int* status, double* z, int nz, int batch) {
+    const int b = blockIdx.x;
+    if (b >= batch || !err[b]) return;
+    if (status && threadIdx.x == 0) status[b] = CMPC_UNSOLVED;
+    for (int i = threadIdx.x; i < nz; i += blockDim.x) z[(size_t)b * nz + i] = __builtin_nan("");
 }
 
-hipError_t lpv_mark_launch(const int* err, int* status, int batch, hipStream_t s) {
+hipError_t lpv_mark_launch(const int* err, int* status, double* z, int nz, int batch, hipStream_t s) {
     if (batch == 0) return hipSuccess;
-    hipLaunchKernelGGL(lpv_mark_kernel, dim3((batch + 255) / 256), dim3(256), 0, s, err, status, batch);
+    hipLaunchKernelGGL(lpv_mark_kernel, dim3(batch), dim3(kWave), 0, s, err, status, z, nz, batch);
     return hipGetLastError();
 }
 

@@ -460,13 +460,6 @@ __global__ __launch_bounds__(kWave) void mpc_ipm_kernel(const MpcConst c, const 
         }
         bar();
 
-        if (c.debug && it == 1 && P.stamps) {  // diagnostic: dump K (lower, npad x npad) to the stamps buffer
-            double* dk = reinterpret_cast<double*>(P.stamps) + (size_t)b * npad * npad;
-            for (int i = l; i < n * n; i += kWave) {
-                const int r = i / n, cc = i - r * n;
-                dk[r * npad + cc] = (cc <= r) ? K[r * ldk + cc] : 0.0;
-            }
-        }
         // ================= Cholesky K = L L' (lane i owns row i) =================
         bool chol_ok = true;
         for (int j = 0; j < n; ++j) {
@@ -667,6 +660,10 @@ int mpc_prepare(const cmpc_mpc_dims* d, const cmpc_mpc_weights* wt, const cmpc_o
         *msg = "dimension out of range (nx<=12, nu<=4, ns<=4, mc<=16)";
         return CMPC_ERR_UNSUPPORTED;
     }
+    if (o && (o->flags & ~CMPC_FLAG_ALL)) {
+        *msg = "unknown bits in opts.flags";
+        return CMPC_ERR_ARG;
+    }
     const bool fp32 = o && (o->flags & CMPC_FLAG_FP32);
     if (d->N * d->nu > CMPC_MAX_NCOND_WG) {
         *msg = "N*nu > 256: exceeds the workgroup-per-agent solver";
@@ -686,7 +683,6 @@ int mpc_prepare(const cmpc_mpc_dims* d, const cmpc_mpc_weights* wt, const cmpc_o
     c->ldk = (c->n & 1) ? c->n : c->n + 1;
     c->tol = (o && o->tol > 0) ? o->tol : 1e-9;
     c->max_iter = (o && o->max_iter > 0) ? o->max_iter : 60;
-    c->debug = (o && (o->flags & 2)) ? 1 : 0;
     c->wg = fp32 ? 2 : (c->n > CMPC_MAX_NCOND ? 1 : 0);
     double qs = 1.0;
     for (int i = 0; i < d->nx * d->nx; ++i) c->Q[i] = wt->Q[i];

@@ -221,7 +221,7 @@ __global__ __launch_bounds__(64, 1) void mpc_ipm3_kernel(const MpcConst c, const
     double* Ld = sm + L.Ld;
     double* red = sm + L.red;
     double* SP = sW;  // Cholesky panel scratch (aliases W | Gb | Yb after the K build)
-    const bool stamp = P.stamps != nullptr && !c.debug;
+    const bool stamp = P.stamps != nullptr;
     // diagnostic per-section clock sums live in LDS (registers stay with the solver)
     unsigned long long* tsum = reinterpret_cast<unsigned long long*>(sm + L.stamps);
     if (l < kStampSlots) tsum[l] = 0;

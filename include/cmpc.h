@@ -71,6 +71,7 @@ typedef struct cmpc_ctx cmpc_ctx;
 #define CMPC_FLAG_GENERIC 1  /* force the generic (runtime-dimension) kernel */
 #define CMPC_FLAG_FP32 8     /* fp32 workgroup-per-agent solver (long horizons, BASELINE cfg5);
                                 opts.tol should then be ~1e-5 */
+#define CMPC_FLAG_ALL (CMPC_FLAG_GENERIC | CMPC_FLAG_FP32)  /* any other bit: CMPC_ERR_ARG */
 
 typedef struct {
     double tol;    /* relative stationarity/feasibility tolerance (complementarity: 1e-4*tol); <= 0 selects 1e-9 */

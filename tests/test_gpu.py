@@ -334,3 +334,45 @@ def test_ocd_dual_update_and_convergence_match_reference(gpu_ctx):
     close, allc = ocd.converged(torch.tensor(xo, device="cuda"), torch.tensor(xp, device="cuda"), ctx=gpu_ctx)
     want = ocd_ref.allclose_agents(xo, xp)
     assert np.array_equal(close.cpu().numpy().astype(bool), want) and allc == bool(want.all())
+
+
+def test_lpv_offtrack_agent_is_flagged_and_isolated(gpu_ctx):
+    """An agent whose previous prediction leaves the track (no segment holds s: the reference
+    raises in curvature/get_ey, misc.py:97) comes back CMPC_UNSOLVED with a NaN z, the other
+    agents of the batch are unaffected, and the PlannerLPV drop-in raises like the reference."""
+    import cmpc
+    from oracle import lpv_ref as L
+
+    g, model = _gains()
+    tr = L.Track.build("Highway")
+    cs = [c for _, c in lpv_qps("lpv_n10_a2") if c["step"] == 0]
+    N = cs[0]["N"]
+    lim = L.scaled_car_limits(cs[0]["vx_ref"])
+    bp = cmpc.PlannerLPVBatch(g["Q"], g["Qs"], g["R"], g["dR"], N, cs[0]["dt"], tr, g["wq"], model, lim, ctx=gpu_ctx)
+    xl = np.stack([c["x_last"] for c in cs])
+    xl[0, 3, 6] = np.nan
+    args = (np.stack([c["x0"] for c in cs]), xl, np.stack([c["u_last"] for c in cs]),
+            np.stack([c["u_old"] for c in cs]), np.stack([c["x_agents"] for c in cs]), np.stack([c["pose"] for c in cs]))
+    res = bp.solve(*args)
+    assert res["status"][0] == cmpc.CMPC_UNSOLVED and np.isnan(res["z"][0]).all()
+    assert res["status"][1] == cmpc.CMPC_SOLVED and np.abs(res["z"][1] - cs[1]["z"]).max() < Z_TOL
+    pl = cmpc.PlannerLPV(g["Q"], g["Qs"], g["R"], g["dR"], N, cs[0]["dt"], tr, 0, g["wq"], model, lim, ctx=gpu_ctx)
+    with pytest.raises(ValueError):
+        pl.solve(args[0][0], xl[0], args[2][0], args[4][0], [1], args[5][0])
+
+
+def test_unknown_option_flags_are_rejected(gpu_ctx):
+    import cmpc
+    from cmpc import _lib as Lb
+    from cmpc import scenarios as S
+    from oracle import synth
+
+    sc = S.make_di(2, 10, 1, 2)
+    P = synth.structured(sc.shared, sc.params, sc.A, sc.B, sc.x0, sc.u_prev, sc.lane, sc.nbr, sc.traj, np.arange(2))
+    orig = Lb.opts
+    try:
+        Lb.opts = lambda *a, **k: orig(flags=2)
+        with pytest.raises(cmpc.CmpcError):
+            cmpc.solve_mpc(P, gpu_ctx)
+    finally:
+        Lb.opts = orig

@@ -7,7 +7,7 @@ cd "$GRAFT_REPO_ROOT"
 mkdir -p gpurun_out/$TAG
 O=gpurun_out/$TAG
 export TMPDIR=/tmp
-BENCH="bench.py --steps 20 --warmup 5"
+BENCH="bench.py --steps 100 --warmup 5"
 timeout -k 10 420 python -u -m pytest tests -m gpu -x -q -p no:cacheprovider --timeout 120 --timeout-method thread > $O/pytest_gpu.log 2>&1 &&
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 &&
 timeout -k 10 420 python $BENCH > $O/bench.json 2> $O/bench.err &&

@@ -4,14 +4,33 @@
       per-dispatch durations of the solver kernel; the average over the bench's timed
       launches (dispatches warmup .. warmup+steps-1) is the number bench.py's
       roofline.kernel_ms_per_launch must agree with.
-  python tools/prof_summary.py pmc <counter_collection.csv (FETCH pass)> <(WRITE pass)> <out.json>
+  python tools/prof_summary.py pmc <counter_collection.csv (FETCH pass)> <(WRITE pass)> <out.json> [commit]
       HBM bytes per launch of the solver kernel from FETCH_SIZE / WRITE_SIZE (kB), with the
       gfx950 correction of /opt/skills/guides/MI355X_MICROARCH.md (FETCH_SIZE counts half the
       bytes of wide coalesced reads: x2).
 """
 import csv
+import glob
+import hashlib
 import json
+import os
 import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def solver_sources_sha():
+    """sha256 over the HIP sources and headers libcmpc is built from (bench.py recomputes it to
+    tell whether a committed PMC figure still describes the current kernels)."""
+    h = hashlib.sha256()
+    files = sorted(glob.glob(os.path.join(ROOT, "colaborativempc-_amd", "csrc", "*.hip")) +
+                   glob.glob(os.path.join(ROOT, "colaborativempc-_amd", "csrc", "*.h")) +
+                   [os.path.join(ROOT, "include", "cmpc.h")])
+    for f in files:
+        h.update(os.path.basename(f).encode())
+        with open(f, "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:16]
 
 SOLVER = "mpc_ipm"   # matches mpc_ipm_kernel<...> and mpc_ipm2_kernel<...>
 
@@ -44,7 +63,7 @@ def _pmc(path, counter):
     return [vals[k] for k in sorted(vals)]
 
 
-def pmc(fetch_csv, write_csv, out):
+def pmc(fetch_csv, write_csv, out, commit=None):
     fk = _pmc(fetch_csv, "FETCH_SIZE")
     wk = _pmc(write_csv, "WRITE_SIZE")
     # skip the first dispatch of each run (cold caches / first touch)
@@ -55,7 +74,8 @@ def pmc(fetch_csv, write_csv, out):
     res = {"solve_kernel": {"fetch_bytes_per_launch": fetch_b, "write_bytes_per_launch": write_b,
                             "hbm_bytes_per_launch": fetch_b + write_b,
                             "fetch_kB_raw": fk, "write_kB_raw": wk,
-                            "note": "FETCH_SIZE x2 (gfx950 half-count of wide reads); first dispatch skipped"}}
+                            "note": "FETCH_SIZE x2 (gfx950 half-count of wide reads); first dispatch skipped"},
+           "commit": commit, "sources_sha": solver_sources_sha()}
     json.dump(res, open(out, "w"), indent=1)
     print(json.dumps(res))
 
@@ -64,4 +84,4 @@ if __name__ == "__main__":
     if sys.argv[1] == "trace":
         trace(sys.argv[2], int(sys.argv[3]), int(sys.argv[4]), sys.argv[5])
     else:
-        pmc(sys.argv[2], sys.argv[3], sys.argv[4])
+        pmc(sys.argv[2], sys.argv[3], sys.argv[4], sys.argv[5] if len(sys.argv) > 5 else None)
