@@ -8,9 +8,9 @@ round driver and synthetic workloads.  There is no CPU solve path here.
 from ._lib import (CMPC_MAX_ITER_REACHED, CMPC_SOLVED, CMPC_SOLVED_INACCURATE, CMPC_UNSOLVED, CmpcError,
                    Context, default_context, load)
 from .planner import PlannerLPV, PlannerLPVBatch, feasible_of, unpack
-from .qp import osqp_solve_qp, quadprog
+from .qp import osqp_solve_qp, osqp_solve_qp_batch, quadprog
 from .solver import nz_of, selftest_mfma, solve_mpc, solve_mpc_dev
 
 __all__ = ["Context", "CmpcError", "default_context", "load", "PlannerLPV", "PlannerLPVBatch", "feasible_of",
-           "unpack", "quadprog", "osqp_solve_qp", "solve_mpc", "solve_mpc_dev", "nz_of", "selftest_mfma", "CMPC_SOLVED",
+           "unpack", "quadprog", "osqp_solve_qp", "osqp_solve_qp_batch", "solve_mpc", "solve_mpc_dev", "nz_of", "selftest_mfma", "CMPC_SOLVED",
            "CMPC_SOLVED_INACCURATE", "CMPC_MAX_ITER_REACHED", "CMPC_UNSOLVED"]

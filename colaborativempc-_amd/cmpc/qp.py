@@ -96,23 +96,72 @@ def quadprog(H, f, A=None, b=None, Aeq=None, beq=None, lb=None, ub=None, ctx=Non
     return res
 
 
+def _osqp_result(x, status_val, text, iters, obj, kkt, pri_res, path):
+    res = SimpleNamespace(x=x, y=None, info=SimpleNamespace(status_val=status_val, status=text, iter=iters,
+                                                           obj_val=obj, kkt=kkt, pri_res=pri_res, solver=path))
+    feasible = 1 if status_val in (1, 2, -2) else 0   # LPV_Planner.py:243-249
+    if status_val != 1:
+        print("OSQP exited with status '%s'" % text)
+    return res, feasible
+
+
+def _pri_res(z, G, h, A, b):
+    """Reference-form primal residual max(|A z - b|, max(G z - h, 0)) (OSQP's pri_res, inf-norm)."""
+    r = 0.0
+    if A is not None and b is not None:
+        r = max(r, float(np.abs(A @ z - np.asarray(b, float).ravel()).max(initial=0.0)))
+    if G is not None and h is not None:
+        r = max(r, float(np.maximum(G @ z - np.asarray(h, float).ravel(), 0.0).max(initial=0.0)))
+    return r
+
+
+def osqp_solve_qp_batch(qps, ctx=None, tol=None, max_iter=None, structured=True):
+    """Many ``osqp_solve_qp`` calls in as few GPU launches as possible: ``qps`` is a list of
+    (P, q, G, h, A, b) tuples.  Every QP that ``structure.recognize`` identifies as a
+    reference-form agent QP (LPV_Planner.py:156-157) joins one structured batch per distinct
+    shared part (cmpc_solve_mpc_batch: one wavefront per agent); the others go through the
+    dense kernel (cmpc_solve_qp_batch; ``structured=False`` sends every QP there).  Returns a
+    list of (res, feasible)."""
+    from . import structure as St
+    from .solver import solve_mpc
+
+    recs = [St.recognize(*qp[:6]) if structured else None for qp in qps]
+    out = [None] * len(qps)
+    groups = {}
+    for i, p in enumerate(recs):
+        if p is not None:
+            groups.setdefault(St.shared_key(p), []).append(i)
+    for idx in groups.values():
+        batch = St.stack([recs[i] for i in idx])
+        z, kkt, it, st = solve_mpc(batch, ctx, tol=tol, max_iter=max_iter)
+        for a, i in enumerate(idx):
+            P, q, G, h, A, b = qps[i][:6]
+            x = z[a]
+            obj = float(0.5 * x @ (P @ x) + np.asarray(q, float) @ x)
+            out[i] = _osqp_result(x, int(st[a]), L.STATUS_TEXT.get(int(st[a]), "unsolved"), int(it[a]), obj,
+                                  float(kkt[a]), _pri_res(x, G, h, A, b), "structured")
+    for i, p in enumerate(recs):
+        if p is not None:
+            continue
+        P, q, G, h, A, b = qps[i][:6]
+        r = quadprog(P, q, G, h, A, b, ctx=ctx, tol=tol, max_iter=max_iter)
+        sv, text = _OSQP_OF_FLAG.get(int(r["exitflag"]), (-10, "unsolved"))
+        x = r["x"]
+        Gs = None if G is None else (G if hasattr(G, "toarray") else np.asarray(G, float))
+        As = None if A is None else (A if hasattr(A, "toarray") else np.asarray(A, float))
+        out[i] = _osqp_result(x, sv, text, int(r["iterations"]), float(r["fval"]), float(r["residual"]),
+                              _pri_res(x, Gs, h, As, b), "dense")
+    return out
+
+
 def osqp_solve_qp(P, q, G=None, h=None, A=None, b=None, initvals=None, ctx=None):
     """Drop-in for the reference's ``osqp_solve_qp`` (LPV_Planner.py:192-249): the same QP
-    (min 1/2 x'Px + q'x s.t. G x <= h, A x = b) solved on the GPU.  ``initvals`` is accepted
+    (min 1/2 x'Px + q'x s.t. G x <= h, A x = b) solved on the GPU, returning (res, feasible)
+    with ``res.x``, ``res.info.status_val`` / ``.status`` (OSQP codes), ``.obj_val``, ``.iter``,
+    plus ``.pri_res`` (reference-form primal residual), ``.kkt`` (the solver's scaled KKT
+    residual) and ``.solver`` ("structured" when the QP is recognised as the PlannerLPV agent
+    QP and solved by the structured kernels, "dense" otherwise).  ``initvals`` is accepted
     but unused: the reference passes it to ``osqp.warm_start`` (:237-238), while the
     interior-point method here starts from its own interior point (the caller in the
-    reference, PlannerLPV.solve :156-157, never passes it).  Returns (res, feasible)."""
-    r = quadprog(P, q, G, h, A, b, ctx=ctx)
-    flags = np.atleast_1d(r["exitflag"])
-    out = []
-    for i, fl in enumerate(flags):
-        sv, text = _OSQP_OF_FLAG.get(int(fl), (-10, "unsolved"))
-        x = np.atleast_2d(r["x"])[i]
-        res = SimpleNamespace(x=x, y=None, info=SimpleNamespace(status_val=sv, status=text,
-                                                                   iter=int(np.atleast_1d(r["iterations"])[i]),
-                                                                   obj_val=float(np.atleast_1d(r["fval"])[i])))
-        feasible = 1 if sv in (1, 2, -2) else 0   # LPV_Planner.py:243-249
-        if sv != 1:
-            print("OSQP exited with status '%s'" % text)
-        out.append((res, feasible))
-    return out[0] if np.ndim(r["exitflag"]) == 0 else out
+    reference, PlannerLPV.solve :156-157, never passes it)."""
+    return osqp_solve_qp_batch([(P, q, G, h, A, b)], ctx=ctx)[0]

@@ -1,0 +1,209 @@
+"""Recognition of the PlannerLPV QP structure at the ``osqp_solve_qp`` boundary.
+
+The reference hands OSQP one sparse QP per agent and control step
+(planner/lib/plan_lib/distributedPlanner/LPV_Planner.py:156-157 -> :192-249):
+
+    z = [xi_0 .. xi_N | u_0 .. u_{N-1} | du_0 .. du_{N-1}],   xi_k = [x_k (nx) | s_k (ns)]
+    P = 2 blkdiag((Q (+) Qs)^(N+1), R^N, dR^N)                                   (:382-427)
+    q = 2 [p_0 .. p_N (state part only), 0, 0]
+    G z <= h: stage rows C_{k,r} x_k + sign_r s_k[slack_r] <= h_{k,r}, k = 1..N   (:251-380)
+              then per stage [u_i <= ub_i; -u_i <= -lb_i] for every input i
+    A z = b:  x_0 = x0;  x_k - A_{k-1} x_{k-1} - B_{k-1} u_{k-1} = 0;  0 = 0 on the slack rows;
+              u_0 - du_0 = u_prev;  u_{k-1} - u_k + du_k = 0                        (:429-475)
+
+``recognize`` reads every structured quantity (A_k, B_k, x0, u_prev, Q, R, dR, Qs, p_k,
+C_k, h_k, input bounds, the slack pattern) out of such a QP, rebuilds the QP from them
+(``reference_form``) and accepts only when the rebuilt matrices and vectors are equal to
+the given ones entry for entry.  An accepted QP is therefore *identical* to the structured
+problem the one-wavefront-per-agent solvers take (cmpc_solve_mpc_batch), and the adapter
+solves it there instead of through the generic dense kernel.  Anything else returns None.
+"""
+from __future__ import annotations
+
+import numpy as np
+import scipy.sparse as sp
+
+LPV_LAYOUT = (9, 3, 2)   # PlannerLPV: n_s = 9 states, 3 slacks, n_u = 2 inputs (LPV_Planner.py:31-33)
+
+
+def _csr(a):
+    m = sp.csr_matrix(a, dtype=np.float64)
+    m.sum_duplicates()
+    m.eliminate_zeros()
+    return m
+
+
+def dims_of(nz, m_ineq, m_eq, layout=LPV_LAYOUT):
+    """(N, mc) of a reference-form QP with layout (nx, ns, nu), or None."""
+    nx, ns, nu = layout
+    ne = nx + ns
+    if (nz - ne) % (ne + 2 * nu):
+        return None
+    N = (nz - ne) // (ne + 2 * nu)
+    if N < 1 or m_eq != ne * (N + 1) + nu * N or (m_ineq - 2 * nu * N) % N:
+        return None
+    mc = (m_ineq - 2 * nu * N) // N
+    return (N, mc) if mc >= 0 else None
+
+
+def reference_form(p, a=0):
+    """Sparse reference-form QP (P, q, G, h, Aeq, beq) of agent ``a`` of a structured problem
+    dict (the keys of include/cmpc.h; row_slack / row_sign give the slack pattern)."""
+    nx, nu, N, ns, mc = (int(p[k]) for k in ("nx", "nu", "N", "ns", "mc"))
+    ne = nx + ns
+    nz = ne * (N + 1) + 2 * nu * N
+    cu, cd = ne * (N + 1), ne * (N + 1) + nu * N
+    # cost
+    Qt = np.zeros((ne, ne))
+    Qt[:nx, :nx] = p["Q"]
+    Qt[nx:, nx:] = np.diag(np.asarray(p["Qs"], float))
+    P = sp.block_diag([Qt] * (N + 1) + [np.asarray(p["R"], float)] * N + [np.asarray(p["dR"], float)] * N,
+                      format="csr") * 2.0
+    q = np.zeros(nz)
+    q[: ne * (N + 1)].reshape(N + 1, ne)[:, :nx] = 2.0 * np.asarray(p["qlin"][a], float)
+    # inequalities: stage rows, then input rows
+    k = np.arange(1, N + 1)
+    r_st = (k - 1)[:, None, None] * mc + np.arange(mc)[None, :, None]          # (N, mc, 1)
+    c_st = k[:, None, None] * ne + np.arange(nx)[None, None, :]               # (N, 1, nx)
+    C = np.asarray(p["C"][a], float)
+    rows = [np.broadcast_to(r_st, C.shape).ravel()]
+    cols = [np.broadcast_to(c_st, C.shape).ravel()]
+    vals = [C.ravel()]
+    sl = np.asarray(p["row_slack"])
+    sg = np.asarray(p["row_sign"], float)
+    has = np.nonzero(sl >= 0)[0]
+    if has.size:
+        rows.append(((k - 1)[:, None] * mc + has[None, :]).ravel())
+        cols.append((k[:, None] * ne + nx + sl[has][None, :]).ravel())
+        vals.append(np.broadcast_to(sg[has], (N, has.size)).ravel())
+    ms = N * mc
+    ku = np.arange(N)[:, None]
+    iu = np.arange(nu)[None, :]
+    ru = ms + (ku * nu + iu) * 2
+    cu_i = cu + ku * nu + iu
+    rows += [ru.ravel(), (ru + 1).ravel()]
+    cols += [cu_i.ravel(), cu_i.ravel()]
+    vals += [np.ones(N * nu), -np.ones(N * nu)]
+    G = sp.csr_matrix((np.concatenate(vals), (np.concatenate(rows), np.concatenate(cols))),
+                      shape=(ms + 2 * nu * N, nz))
+    h = np.concatenate([np.asarray(p["h"][a], float).ravel(),
+                        np.stack([np.broadcast_to(np.asarray(p["u_ub"], float), (N, nu)),
+                                  np.broadcast_to(-np.asarray(p["u_lb"], float), (N, nu))], -1).ravel()])
+    # equalities
+    ke = np.arange(N + 1)
+    rows = [(ke[:, None] * ne + np.arange(nx)).ravel()]
+    cols = [(ke[:, None] * ne + np.arange(nx)).ravel()]
+    vals = [np.ones((N + 1) * nx)]
+    kd = np.arange(1, N + 1)[:, None, None]
+    s_ = np.arange(nx)[None, :, None]
+    rows.append(np.broadcast_to(kd * ne + s_, (N, nx, nx)).ravel())
+    cols.append(np.broadcast_to((kd - 1) * ne + np.arange(nx)[None, None, :], (N, nx, nx)).ravel())
+    vals.append(-np.asarray(p["A"][a], float).ravel())
+    rows.append(np.broadcast_to(kd * ne + s_, (N, nx, nu)).ravel())
+    cols.append(np.broadcast_to(cu + (kd - 1) * nu + np.arange(nu)[None, None, :], (N, nx, nu)).ravel())
+    vals.append(-np.asarray(p["B"][a], float).ravel())
+    r0 = ne * (N + 1)
+    i = np.arange(N)[:, None]
+    j = np.arange(nu)[None, :]
+    rr = (r0 + i * nu + j).ravel()
+    first = (i == 0).repeat(nu, 1).ravel()
+    rows += [rr, rr, rr[~first]]
+    cols += [(cu + i * nu + j).ravel(), (cd + i * nu + j).ravel(), (cu + (i - 1) * nu + j).ravel()[~first]]
+    vals += [np.where(first, 1.0, -1.0), np.where(first, -1.0, 1.0), np.ones((~first).sum())]
+    Aeq = sp.csr_matrix((np.concatenate(vals), (np.concatenate(rows), np.concatenate(cols))),
+                        shape=(ne * (N + 1) + nu * N, nz))
+    beq = np.zeros(Aeq.shape[0])
+    beq[:nx] = p["x0"][a]
+    beq[r0:r0 + nu] = p["u_prev"][a]
+    return _csr(P), q, _csr(G), h, _csr(Aeq), beq
+
+
+def _same(X, Y):
+    return X.shape == Y.shape and (X != Y).nnz == 0
+
+
+def recognize(P, q, G, h, A, b, layout=LPV_LAYOUT):
+    """Structured single-agent problem dict (batch axis of 1) if (P, q, G, h, A, b) is exactly
+    a reference-form agent QP of the given layout, else None."""
+    if G is None or A is None or h is None or b is None:
+        return None
+    nx, ns, nu = layout
+    ne = nx + ns
+    P, G, A = _csr(P), _csr(G), _csr(A)
+    q, h, b = (np.asarray(v, dtype=np.float64).ravel() for v in (q, h, b))
+    nz = P.shape[1]
+    if P.shape != (nz, nz) or G.shape[1] != nz or A.shape[1] != nz or q.size != nz or \
+            h.size != G.shape[0] or b.size != A.shape[0]:
+        return None
+    d = dims_of(nz, G.shape[0], A.shape[0], layout)
+    if d is None:
+        return None
+    N, mc = d
+    cu, cd = ne * (N + 1), ne * (N + 1) + nu * N
+    if not (np.isfinite(q).all() and np.isfinite(b).all()) or np.isnan(h).any():
+        return None
+    # cost (P / 2 and q / 2 are exact in binary floating point)
+    Pd = P[:ne, :ne].toarray() / 2.0
+    Q, Qs = Pd[:nx, :nx], np.diag(Pd[nx:, nx:]).copy()
+    R = P[cu:cu + nu, cu:cu + nu].toarray() / 2.0
+    dR = P[cd:cd + nu, cd:cd + nu].toarray() / 2.0
+    if ns and not (Qs > 0).all():
+        return None
+    qlin = q[: ne * (N + 1)].reshape(N + 1, ne)[:, :nx] / 2.0
+    # dynamics from the equality rows
+    Ac = A.tocoo()
+    r, c, v = Ac.row, Ac.col, Ac.data
+    kr, sr = r // ne, r % ne
+    dyn = (r < ne * (N + 1)) & (kr >= 1) & (sr < nx)
+    Am = np.zeros((N, nx, nx))
+    Bm = np.zeros((N, nx, nu))
+    mx = dyn & (c < ne * (N + 1)) & (c // ne == kr - 1) & (c % ne < nx)
+    Am[kr[mx] - 1, sr[mx], c[mx] % ne] = -v[mx]
+    mu_ = dyn & (c >= cu) & (c < cd) & ((c - cu) // nu == kr - 1)
+    Bm[kr[mu_] - 1, sr[mu_], (c[mu_] - cu) % nu] = -v[mu_]
+    x0 = b[:nx].copy()
+    u_prev = b[ne * (N + 1): ne * (N + 1) + nu].copy()
+    # stage rows and input bounds from the inequality rows
+    Gc = G.tocoo()
+    r, c, v = Gc.row, Gc.col, Gc.data
+    ms = N * mc
+    st = (r < ms) & (c // ne == r // mc + 1) & (c < ne * (N + 1))
+    Cm = np.zeros((N, mc, nx))
+    sx = st & (c % ne < nx)
+    Cm[r[sx] // mc, r[sx] % mc, c[sx] % ne] = v[sx]
+    row_slack = -np.ones(mc, np.int32)
+    row_sign = np.ones(mc, np.int32)
+    ss = st & (c % ne >= nx) & (r < mc)   # slack pattern from stage 1; the rebuild checks all stages
+    for rr_, cc_, vv_ in zip(r[ss], c[ss], v[ss]):
+        if row_slack[rr_] >= 0 or vv_ not in (1.0, -1.0):
+            return None
+        row_slack[rr_] = cc_ % ne - nx
+        row_sign[rr_] = int(vv_)
+    hh = h[:ms].reshape(N, mc).copy()
+    hu = h[ms:].reshape(N, nu, 2)
+    u_ub, u_lb = hu[0, :, 0].copy(), -hu[0, :, 1]
+    prob = dict(nx=nx, nu=nu, N=N, ns=ns, mc=mc, Q=Q, R=R, dR=dR, Qs=Qs, u_ub=u_ub, u_lb=u_lb,
+                row_slack=row_slack, row_sign=row_sign, A=Am[None], B=Bm[None], x0=x0[None], u_prev=u_prev[None],
+                qlin=qlin[None], C=Cm[None], h=hh[None])
+    P2, q2, G2, h2, A2, b2 = reference_form(prob, 0)
+    if not (_same(P, P2) and _same(G, G2) and _same(A, A2) and np.array_equal(q, q2) and np.array_equal(b, b2)
+            and np.array_equal(h, h2)):
+        return None
+    return prob
+
+
+def shared_key(p):
+    """Hashable key of the batch-shared part of a structured problem (problems with equal keys
+    can share one cmpc_solve_mpc_batch launch)."""
+    return (p["nx"], p["nu"], p["N"], p["ns"], p["mc"]) + tuple(
+        np.asarray(p[k], float).tobytes() for k in ("Q", "R", "dR", "Qs", "u_ub", "u_lb")) + (
+        np.asarray(p["row_slack"]).tobytes(), np.asarray(p["row_sign"]).tobytes())
+
+
+def stack(probs):
+    """One structured batch from single-agent problems with equal shared_key."""
+    out = {k: probs[0][k] for k in ("nx", "nu", "N", "ns", "mc", "Q", "R", "dR", "Qs", "u_ub", "u_lb",
+                                     "row_slack", "row_sign")}
+    for k in ("A", "B", "x0", "u_prev", "qlin", "C", "h"):
+        out[k] = np.concatenate([p[k] for p in probs])
+    return out

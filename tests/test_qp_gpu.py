@@ -6,7 +6,7 @@ a QP captured from the reference's own PlannerLPV (tests/golden)."""
 import numpy as np
 import pytest
 
-from conftest import lpv_qps
+from conftest import LPV_CASES, lpv_qps
 
 pytestmark = pytest.mark.gpu
 
@@ -70,22 +70,62 @@ def test_random_qps_match_certified_oracle(gpu_ctx, seed, n, mi, me):
         assert np.abs(r["x"][k] - ref.x).max() < X_TOL
 
 
-@pytest.mark.parametrize("name", ["lpv_n10_a2", "lpv_n30_a3"])
+def _osqp_args(c):
+    """(P, q, G, h, A, b) exactly as PlannerLPV.solve passes them (LPV_Planner.py:156-157): csr
+    matrices, G = F, h = b, A = G_eq, b = E x0 + Eu uOld (recovered from OSQP's stacked form)."""
+    import scipy.sparse as sp
+
+    Aall, l, u = c["A"], c["l"], c["u"]
+    eq = np.isfinite(l) & (l == u)
+    return (sp.csr_matrix(c["P"]), c["q"], sp.csr_matrix(Aall[~eq]), u[~eq], sp.csr_matrix(Aall[eq]), u[eq])
+
+
+@pytest.mark.parametrize("name", LPV_CASES)
 def test_osqp_adapter_on_reference_captured_qp(gpu_ctx, name):
-    """The reference's own QPs, handed to osqp_solve_qp exactly as PlannerLPV.solve does
-    (LPV_Planner.py:156-157): P, q, G=F, h=b, A=G_eq, b=E x0 + Eu uOld.  This generic dense
-    path does not see the stage structure: the reduced Hessian's condition number is ~1e8
-    (Qs = 1e7), so the bar on z is 1e-4 (OSQP's own default eps is 1e-3) and
-    the optimal value must agree to 1e-7 relative (multipliers reach 1e7, so a 1e-12 feasibility
-    difference moves it by ~1e-5); the structured path holds 1e-6 on z."""
+    """Every captured reference QP of every golden file through osqp_solve_qp, called exactly as
+    PlannerLPV.solve calls it.  The adapter recognises the agent-QP structure (an exact
+    rebuild, cmpc.structure) and solves it on the structured kernels: z within 1e-6 of the
+    KKT-certified optimum, the solver's KKT residual and the reference-form primal residual
+    both <= 1e-6, OSQP status 'solved'."""
+    import cmpc
+
+    for j, c in lpv_qps(name):
+        res, feasible = cmpc.osqp_solve_qp(*_osqp_args(c), ctx=gpu_ctx)
+        assert res.info.solver == "structured"
+        assert feasible == 1 and res.info.status_val == 1, (j, res.info.status)
+        assert res.info.kkt <= 1e-6 and res.info.pri_res <= 1e-6, (res.info.kkt, res.info.pri_res)
+        assert np.abs(res.x - c["z"]).max() < 1e-6, (j, np.abs(res.x - c["z"]).max())
+        fz = 0.5 * c["z"] @ c["P"] @ c["z"] + c["q"] @ c["z"]
+        assert abs(res.info.obj_val - fz) <= 1e-9 * max(1.0, abs(fz))
+
+
+def test_osqp_adapter_batch_groups_reference_qps(gpu_ctx):
+    """All captured QPs of the 3-agent N=30 case in one osqp_solve_qp_batch call (one
+    structured launch) give the same answers as one call per QP."""
+    import cmpc
+
+    cs = [c for _, c in lpv_qps("lpv_n30_a3")]
+    out = cmpc.osqp_solve_qp_batch([_osqp_args(c) for c in cs], ctx=gpu_ctx)
+    for c, (res, feasible) in zip(cs, out):
+        one, _ = cmpc.osqp_solve_qp(*_osqp_args(c), ctx=gpu_ctx)
+        assert feasible == 1 and res.info.solver == "structured"
+        assert np.array_equal(res.x, one.x)
+        assert np.abs(res.x - c["z"]).max() < 1e-6
+
+
+@pytest.mark.parametrize("name", ["lpv_n10_a2", "lpv_n30_a3"])
+def test_dense_path_on_reference_captured_qp(gpu_ctx, name):
+    """The generic dense kernel (structure recognition off) on the reference's own QPs.  It does
+    not see the stage structure and works on the reduced Hessian, whose condition number is ~1e8
+    (Qs = 1e7): the bar on z is 1e-4 (OSQP's own default eps is 1e-3) and the
+    optimal value agrees to 1e-7 relative; the structured path above holds 1e-6."""
     import cmpc
 
     for j, c in lpv_qps(name):
         if c["step"] > 1:
             continue
-        Aall, l, u = c["A"], c["l"], c["u"]
-        eq = np.isfinite(l) & (l == u)
-        res, feasible = cmpc.osqp_solve_qp(c["P"], c["q"], Aall[~eq], u[~eq], Aall[eq], u[eq], ctx=gpu_ctx)
+        res, feasible = cmpc.osqp_solve_qp_batch([_osqp_args(c)], ctx=gpu_ctx, structured=False)[0]
+        assert res.info.solver == "dense"
         assert feasible == 1 and res.info.status_val == 1
         fz = 0.5 * c["z"] @ c["P"] @ c["z"] + c["q"] @ c["z"]
         assert abs(res.info.obj_val - fz) <= 1e-7 * max(1.0, abs(fz))

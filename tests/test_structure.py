@@ -1,0 +1,71 @@
+"""CPU checks of the osqp_solve_qp structure recogniser (cmpc.structure): every QP captured
+from the reference's PlannerLPV (tests/golden, oracle/gen_fixtures.py) is recognised, the
+recovered structured problem is the oracle builder's for the same inputs, and QPs that differ
+from the pattern in any entry are refused (they go to the dense kernel)."""
+import numpy as np
+import pytest
+import scipy.sparse as sp
+
+from conftest import LPV_CASES, lpv_qps
+
+from cmpc import structure as St
+
+
+def _args(c):
+    Aall, l, u = c["A"], c["l"], c["u"]
+    eq = np.isfinite(l) & (l == u)
+    return sp.csr_matrix(c["P"]), c["q"], sp.csr_matrix(Aall[~eq]), u[~eq], sp.csr_matrix(Aall[eq]), u[eq]
+
+
+@pytest.mark.parametrize("name", LPV_CASES)
+def test_every_captured_qp_is_recognised(name):
+    from oracle import lpv_ref as L
+
+    g = L.paper_gains()
+    for j, c in lpv_qps(name):
+        p = St.recognize(*_args(c))
+        assert p is not None, (name, j)
+        N = c["N"]
+        nb = c["x_agents"].shape[1]
+        assert p["N"] == N and p["mc"] == 4 + nb
+        np.testing.assert_array_equal(p["Q"], g["Q"])
+        np.testing.assert_array_equal(p["Qs"], np.diag(g["Qs"]))
+        np.testing.assert_array_equal(p["dR"], g["dR"])
+        np.testing.assert_array_equal(p["x0"][0], c["x0"])
+        np.testing.assert_array_equal(p["u_prev"][0], c["u_old"])
+        assert list(p["row_slack"]) == [-1, 0, 1, 1] + [2] * nb
+        assert list(p["row_sign"]) == [1, 1, 1, 1] + [-1] * nb
+        # rebuilt reference form == the captured one (the acceptance test itself, restated)
+        P2, q2, G2, h2, A2, b2 = St.reference_form(p)
+        P, q, G, h, A, b = _args(c)
+        assert (P != P2).nnz == 0 and (G != G2).nnz == 0 and (A != A2).nnz == 0
+        assert np.array_equal(q, q2) and np.array_equal(h, h2) and np.array_equal(b, b2)
+
+
+def test_perturbed_qps_are_refused():
+    _, c = next(iter(lpv_qps("lpv_n10_a2")))
+    P, q, G, h, A, b = _args(c)
+    assert St.recognize(P, q, G, h, A, b) is not None
+    P2 = P.tolil()
+    P2[0, 1] = 1e-3                                      # x-x cross term the stage form lacks
+    assert St.recognize(P2, q, G, h, A, b) is None
+    q2 = q.copy()
+    q2[-1] = 1.0                                         # linear cost on a rate
+    assert St.recognize(P, q2, G, h, A, b) is None
+    h2 = h.copy()
+    h2[-1] += 1.0                                        # input bound differing between stages
+    assert St.recognize(P, q, G, h2, A, b) is None
+    A2 = A.tolil()
+    A2[20, 30] = 0.5                                     # a coupling outside the dynamics pattern
+    assert St.recognize(P, q, G, h, A2, b) is None
+    assert St.recognize(P, q, G[:-1], h[:-1], A, b) is None   # wrong row count
+    assert St.recognize(P, q, None, None, A, b) is None
+
+
+def test_stack_and_shared_key():
+    cs = [c for _, c in lpv_qps("lpv_n30_a3")]
+    ps = [St.recognize(*_args(c)) for c in cs]
+    keys = {St.shared_key(p) for p in ps}
+    assert len(keys) == 1
+    s = St.stack(ps)
+    assert s["A"].shape == (len(cs), 30, 9, 9) and s["C"].shape[0] == len(cs)
