@@ -39,6 +39,7 @@ _IP = ct.POINTER(ct.c_int)
 
 CMPC_FLAG_GENERIC = 1
 CMPC_FLAG_FP32 = 8
+CMPC_FLAG_RICCATI = 16
 
 
 class cmpc_opts(ct.Structure):

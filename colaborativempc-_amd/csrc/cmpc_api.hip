@@ -37,7 +37,8 @@ int hip_fail(cmpc_ctx* c, hipError_t e, const char* where) {
 char* arena(cmpc_ctx* ctx, size_t bytes) {
     if (ctx->ws_bytes >= bytes) return ctx->ws;
     if (ctx->ws) {
-        (void)hipStreamSynchronize(ctx->stream);
+        // the arena may be in use by work queued on caller streams (the *_dev entry points)
+        (void)hipDeviceSynchronize();
         (void)hipFree(ctx->ws);
         ctx->ws = nullptr;
         ctx->ws_bytes = 0;
@@ -161,8 +162,13 @@ int cmpc_solve_mpc_batch_dev(cmpc_ctx* ctx, const cmpc_mpc_dims* dims, const cmp
     int rc = cmpc::mpc_prepare(dims, w, opts, &c, &msg);
     if (rc != CMPC_OK) return fail(ctx, rc, msg);
     if ((rc = set_device(ctx)) != CMPC_OK) return rc;
+    double* ws = nullptr;
+    if (const size_t wsd = cmpc::mpc_ws_doubles(c) * (size_t)dims->batch) {
+        ws = reinterpret_cast<double*>(arena(ctx, 8 * wsd));
+        if (!ws) return fail(ctx, CMPC_ERR_NOMEM, "device scratch allocation failed");
+    }
     cmpc::MpcPtrs p{in->A, in->B, in->x0, in->u_prev, in->qlin, in->C, in->h, out->z, out->kkt, out->iters, out->status,
-                    opts ? (unsigned long long*)opts->stamps : nullptr};
+                    opts ? (unsigned long long*)opts->stamps : nullptr, ws};
     HIP_TRY(cmpc::mpc_launch(c, p, dims->batch, (hipStream_t)stream, opts ? opts->flags : 0));
     return CMPC_OK;
 }
@@ -179,7 +185,8 @@ int cmpc_solve_mpc_batch(cmpc_ctx* ctx, const cmpc_mpc_dims* d, const cmpc_mpc_w
     const size_t B = d->batch, N = d->N, nx = d->nx, nu = d->nu, mc = d->mc;
     const size_t sA = B * N * nx * nx, sB = B * N * nx * nu, sx = B * nx, su = B * nu, sp = B * (N + 1) * nx,
                  sC = B * N * mc * nx, sh = B * N * mc, sz = B * mpc_nz(*d);
-    const size_t bytes = 8 * (sA + sB + sx + su + sp + sC + sh + sz + B) + 8 * B + 16 * 256;
+    const size_t sw = cmpc::mpc_ws_doubles(c) * B;
+    const size_t bytes = 8 * (sA + sB + sx + su + sp + sC + sh + sz + B + sw) + 8 * B + 16 * 256;
     char* base = arena(ctx, bytes);
     if (!base) return fail(ctx, CMPC_ERR_NOMEM, "device arena allocation failed");
     Carve cv{base};
@@ -187,6 +194,7 @@ int cmpc_solve_mpc_batch(cmpc_ctx* ctx, const cmpc_mpc_dims* d, const cmpc_mpc_w
            *du = cv.take<double>(su), *dp = cv.take<double>(sp), *dC = cv.take<double>(sC),
            *dh = cv.take<double>(sh), *dz = cv.take<double>(sz), *dk = cv.take<double>(B);
     int *di = cv.take<int>(B), *ds = cv.take<int>(B);
+    double* dw = sw ? cv.take<double>(sw) : nullptr;
     hipStream_t s = ctx->stream;
     HIP_TRY(hipMemcpyAsync(dA, in->A, 8 * sA, hipMemcpyHostToDevice, s));
     HIP_TRY(hipMemcpyAsync(dB, in->B, 8 * sB, hipMemcpyHostToDevice, s));
@@ -196,7 +204,7 @@ int cmpc_solve_mpc_batch(cmpc_ctx* ctx, const cmpc_mpc_dims* d, const cmpc_mpc_w
     HIP_TRY(hipMemcpyAsync(dC, in->C, 8 * sC, hipMemcpyHostToDevice, s));
     HIP_TRY(hipMemcpyAsync(dh, in->h, 8 * sh, hipMemcpyHostToDevice, s));
     cmpc::MpcPtrs p{dA, dB, dx0, du, dp, dC, dh, dz, dk, di, ds,
-                    opts ? (unsigned long long*)opts->stamps : nullptr};  // stamps: device memory
+                    opts ? (unsigned long long*)opts->stamps : nullptr, dw};  // stamps: device memory
     HIP_TRY(cmpc::mpc_launch(c, p, d->batch, s, opts ? opts->flags : 0));
     HIP_TRY(hipMemcpyAsync(out->z, dz, 8 * sz, hipMemcpyDeviceToHost, s));
     if (out->kkt) HIP_TRY(hipMemcpyAsync(out->kkt, dk, 8 * B, hipMemcpyDeviceToHost, s));
@@ -206,10 +214,11 @@ int cmpc_solve_mpc_batch(cmpc_ctx* ctx, const cmpc_mpc_dims* d, const cmpc_mpc_w
     return CMPC_OK;
 }
 
-// Workspace layout of the LPV path (device): structured problem + error flags.
-static size_t lpv_ws_bytes(const cmpc_lpv_dims* d) {
+// Workspace layout of the LPV path (device): structured problem + error flags + solver scratch.
+static size_t lpv_ws_bytes(const cmpc_lpv_dims* d, size_t solver_ws_doubles) {
     const size_t B = d->batch, N = d->N, mc = 4 + d->nb;
-    return 8 * (B * N * 81 + B * N * 18 + B * (N + 1) * 9 + B * N * mc * 9 + B * N * mc) + 4 * B + 8 * 256;
+    return 8 * (B * N * 81 + B * N * 18 + B * (N + 1) * 9 + B * N * mc * 9 + B * N * mc + B * solver_ws_doubles) +
+           4 * B + 10 * 256;
 }
 
 static int lpv_run(cmpc_ctx* ctx, const cmpc_lpv_params* prm, const cmpc_track* tr, const cmpc_lpv_dims* d,
@@ -224,10 +233,12 @@ static int lpv_run(cmpc_ctx* ctx, const cmpc_lpv_params* prm, const cmpc_track* 
     double *A = cv.take<double>(B * N * 81), *Bm = cv.take<double>(B * N * 18), *p = cv.take<double>(B * (N + 1) * 9),
            *C = cv.take<double>(B * N * m * 9), *h = cv.take<double>(B * N * m);
     int* err = cv.take<int>(B);
+    const size_t sw = cmpc::mpc_ws_doubles(mc) * B;
+    double* ws = sw ? cv.take<double>(sw) : nullptr;
     HIP_TRY(hipMemsetAsync(err, 0, 4 * B, s));
     cmpc::LpvPtrs lp{in->x_last, in->u_last, in->x_agents, in->pose, A, Bm, p, C, h, out->planes, err};
     HIP_TRY(cmpc::lpv_build_launch(lc, lp, d->batch, s));
-    cmpc::MpcPtrs mp{A, Bm, in->x0, in->u_old, p, C, h, out->z, out->kkt, out->iters, out->status, nullptr};
+    cmpc::MpcPtrs mp{A, Bm, in->x0, in->u_old, p, C, h, out->z, out->kkt, out->iters, out->status, nullptr, ws};
     HIP_TRY(cmpc::mpc_launch(mc, mp, d->batch, s, opts ? opts->flags : 0));
     HIP_TRY(cmpc::lpv_mark_launch(err, out->status, out->z, (int)(12 * (N + 1) + 4 * N), d->batch, s));
     return CMPC_OK;
@@ -240,7 +251,9 @@ int cmpc_solve_lpv_batch_dev(cmpc_ctx* ctx, const cmpc_lpv_params* prm, const cm
         return fail(ctx, CMPC_ERR_ARG, "null argument");
     int rc = set_device(ctx);
     if (rc != CMPC_OK) return rc;
-    char* base = arena(ctx, lpv_ws_bytes(d));
+    cmpc::MpcConst mc;
+    if ((rc = lpv_solver_const(ctx, prm, d, opts, &mc)) != CMPC_OK) return rc;
+    char* base = arena(ctx, lpv_ws_bytes(d, cmpc::mpc_ws_doubles(mc)));
     if (!base) return fail(ctx, CMPC_ERR_NOMEM, "device arena allocation failed");
     Carve cv{base};
     return lpv_run(ctx, prm, tr, d, in, out, opts, (hipStream_t)stream, cv);
@@ -257,7 +270,10 @@ int cmpc_solve_lpv_batch(cmpc_ctx* ctx, const cmpc_lpv_params* prm, const cmpc_t
     const size_t sx0 = B * 9, sxl = B * d->last_rows * 9, sul = B * N * 2, suo = B * 2,
                  sxa = in->x_agents ? B * (N + 1) * nb * 2 : 0, spo = B * (N + 1) * 2, sz = B * nz,
                  spl = out->planes ? B * N * 3 * nb : 0;
-    const size_t bytes = lpv_ws_bytes(d) + 8 * (sx0 + sxl + sul + suo + sxa + spo + sz + spl + B) + 8 * B + 16 * 256;
+    cmpc::MpcConst mc;
+    if ((rc = lpv_solver_const(ctx, prm, d, opts, &mc)) != CMPC_OK) return rc;
+    const size_t bytes = lpv_ws_bytes(d, cmpc::mpc_ws_doubles(mc)) +
+                         8 * (sx0 + sxl + sul + suo + sxa + spo + sz + spl + B) + 8 * B + 16 * 256;
     char* base = arena(ctx, bytes);
     if (!base) return fail(ctx, CMPC_ERR_NOMEM, "device arena allocation failed");
     Carve cv{base};

@@ -22,7 +22,8 @@ struct MpcConst {
     int npad;   // n rounded up to 16 (MFMA tile)
     int ldk;    // leading dimension of the LDS Hessian (odd)
     int max_iter;
-    int wg;     // 0: one-wave kernels; 1: workgroup kernel in fp64 (N*nu > 64); 2: workgroup kernel in fp32
+    int wg;       // 0: one-wave kernels; 2: workgroup kernel in fp32 (CMPC_FLAG_FP32)
+    int riccati;  // 1: stage-wise Riccati kernel (fp64, N*nu > 64 or CMPC_FLAG_RICCATI)
     double tol;
     double qs_max;  // max(1, 2*max(Qs)) — slack residual scale
     double Q[CMPC_MAX_NX * CMPC_MAX_NX];
@@ -48,6 +49,7 @@ struct MpcPtrs {
     int* iters;
     int* status;
     unsigned long long* stamps;  // optional: batch x kStampSlots per-section s_memtime counts (v3 kernel)
+    double* ws;                  // device scratch, batch x mpc_ws_doubles(c) (Riccati kernel; else unused)
 };
 
 // Interior-point safeguards shared by both solver kernels and the C oracle (oracle/cmpc_oracle.c).
@@ -73,6 +75,13 @@ __host__ __device__ inline int stop_status(int stop, double best_m, double tol) 
 size_t mpc_wg_lds_bytes(const MpcConst& c, bool fp32);
 hipError_t mpc_wg_launch(const MpcConst& c, const MpcPtrs& p, int batch, hipStream_t s, bool fp32);
 constexpr size_t kMaxLdsBytes = 160 * 1024;
+
+// Stage-wise Riccati kernel (mpc_riccati.hip): any horizon whose per-agent rows fit LDS.
+size_t mpc_riccati_lds_bytes(const MpcConst& c);
+size_t mpc_riccati_ws_doubles(const MpcConst& c);
+hipError_t mpc_riccati_launch(const MpcConst& c, const MpcPtrs& p, int batch, hipStream_t s);
+// Device scratch (doubles per agent) the solver chosen for c needs in MpcPtrs::ws (0: none).
+inline size_t mpc_ws_doubles(const MpcConst& c) { return c.riccati ? mpc_riccati_ws_doubles(c) : 0; }
 
 // Fills the derived fields of MpcConst; returns CMPC_OK or an error code with msg.
 int mpc_prepare(const cmpc_mpc_dims* d, const cmpc_mpc_weights* w, const cmpc_opts* o,

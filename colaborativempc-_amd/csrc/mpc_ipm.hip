@@ -665,8 +665,8 @@ int mpc_prepare(const cmpc_mpc_dims* d, const cmpc_mpc_weights* wt, const cmpc_o
         return CMPC_ERR_ARG;
     }
     const bool fp32 = o && (o->flags & CMPC_FLAG_FP32);
-    if (d->N * d->nu > CMPC_MAX_NCOND_WG) {
-        *msg = "N*nu > 256: exceeds the workgroup-per-agent solver";
+    if (fp32 && d->N * d->nu > CMPC_MAX_NCOND_WG) {
+        *msg = "N*nu > 256: exceeds the fp32 workgroup-per-agent solver";
         return CMPC_ERR_UNSUPPORTED;
     }
     *c = MpcConst{};
@@ -683,7 +683,8 @@ int mpc_prepare(const cmpc_mpc_dims* d, const cmpc_mpc_weights* wt, const cmpc_o
     c->ldk = (c->n & 1) ? c->n : c->n + 1;
     c->tol = (o && o->tol > 0) ? o->tol : 1e-9;
     c->max_iter = (o && o->max_iter > 0) ? o->max_iter : 60;
-    c->wg = fp32 ? 2 : (c->n > CMPC_MAX_NCOND ? 1 : 0);
+    c->wg = fp32 ? 2 : 0;
+    c->riccati = (!fp32 && (c->n > CMPC_MAX_NCOND || (o && (o->flags & CMPC_FLAG_RICCATI)))) ? 1 : 0;
     double qs = 1.0;
     for (int i = 0; i < d->nx * d->nx; ++i) c->Q[i] = wt->Q[i];
     for (int i = 0; i < d->nu * d->nu; ++i) {
@@ -699,9 +700,12 @@ int mpc_prepare(const cmpc_mpc_dims* d, const cmpc_mpc_weights* wt, const cmpc_o
         qs = fmax(qs, 2.0 * wt->Qs[j]);
     }
     c->qs_max = qs;
-    if (c->wg && mpc_wg_lds_bytes(*c, c->wg == 2) > kMaxLdsBytes) {
-        *msg = c->wg == 2 ? "problem does not fit the fp32 workgroup solver's 160 KB of LDS"
-                          : "N*nu > 64 in fp64 does not fit 160 KB of LDS: use CMPC_FLAG_FP32";
+    if (c->wg && mpc_wg_lds_bytes(*c, true) > kMaxLdsBytes) {
+        *msg = "problem does not fit the fp32 workgroup solver's 160 KB of LDS";
+        return CMPC_ERR_UNSUPPORTED;
+    }
+    if (c->riccati && mpc_riccati_lds_bytes(*c) > kMaxLdsBytes) {
+        *msg = "the per-agent rows of this horizon do not fit the Riccati solver's 160 KB of LDS";
         return CMPC_ERR_UNSUPPORTED;
     }
     for (int i = 0; i < d->nu; ++i) {
@@ -732,6 +736,7 @@ static hipError_t launch_t(const MpcConst& c, const MpcPtrs& p, int batch, hipSt
 hipError_t mpc_launch(const MpcConst& c, const MpcPtrs& p, int batch, hipStream_t s, int flags) {
     if (batch == 0) return hipSuccess;
     if (c.wg) return mpc_wg_launch(c, p, batch, s, c.wg == 2);
+    if (c.riccati) return mpc_riccati_launch(c, p, batch, s);
     hipError_t e2;
     if (!(flags & CMPC_FLAG_GENERIC) && mpc3_try_launch(c, p, batch, s, &e2)) return e2;
     switch (c.npad / 16) {

@@ -1,0 +1,893 @@
+// Stage-wise (Riccati) interior-point solver for the structured LTV agent-QP: long horizons.
+//
+// The QP is the one PlannerLPV assembles (reference: planner/lib/plan_lib/distributedPlanner/
+// LPV_Planner.py:279-475) and the reference ships it at N = 125 (planner/scripts/config_files/
+// config_LPV.py:13-24): N*nu = 250 condensed inputs, whose dense Newton matrix (500 KB fp64)
+// cannot live in LDS.  This kernel runs the SAME Mehrotra method as the condensed kernels
+// (mpc_ipm.hip: same residuals, scaling, step control, safeguards and termination, internal.h),
+// and only replaces the Newton solve K dU = rhs, K = sum_k Gamma_k' W_k Gamma_k + 2R + 2D'dR D
+// + diag(input rows), by the equivalent linear-quadratic problem over the horizon
+//
+//   min  sum_{k=1..N} 1/2 dX_k' W_k dX_k + sum_k [1/2 dU_k'(2R + th_k) dU_k + 1/2 (dU_k - dU_{k-1})' 2dR (.)]
+//        - rhs' dU     s.t.  dX_{k+1} = A_k dX_k + B_k dU_k,  dX_0 = 0,  dU_{-1} = 0,
+//
+// solved by a Riccati recursion on the augmented state y_k = [dX_k; dU_{k-1}] (na = nx + nu):
+// O(N (nx+nu)^3) work and O(N nu (nx+nu)) storage instead of O((N nu)^3) and O((N nu)^2).
+//
+// One 64-lane wavefront (= one workgroup) per agent.  Everything the row loops touch lives in
+// LDS; the per-stage operands of the recursions (A_k, B_k and the Riccati gains) stream from
+// global memory through a double-buffered LDS stage image, fetched one stage ahead into
+// registers so the load latency overlaps the current stage.  The Riccati gains, the predictor
+// direction and the best-iterate copy live in a per-agent global scratch (MpcPtrs::ws).
+// fp64 throughout.
+#include <cmath>
+
+#include "internal.h"
+#include "wave_ops.h"
+
+namespace cmpc {
+
+namespace {
+
+constexpr int kMaxNa = CMPC_MAX_NX + CMPC_MAX_NU;
+constexpr int kStageMax = CMPC_MAX_NX * CMPC_MAX_NX + CMPC_MAX_NX * CMPC_MAX_NU + CMPC_MAX_NU * kMaxNa +
+                          CMPC_MAX_NU * CMPC_MAX_NU;
+constexpr int kPer = (kStageMax + kWave - 1) / kWave;  // stage-image values per lane
+
+struct RLds {
+    int t, lam, th, rp, rho, rt, w, GdU;  // per row
+    int X, dX, yb, psi;                   // per stage state
+    int U, dU, rd, gU, rh;                // per condensed input
+    int sig, dsig, Dsig, rsig;            // per stage slack
+    int P, pv, sb, T, G, Hy, Kk, W, gv;   // Riccati working set
+    int total;
+};
+
+struct Dims {
+    int nx, nu, na, nc, sA, sB, sF, sAB, S;
+};
+
+__host__ __device__ inline Dims dims_of(const MpcConst& c) {
+    Dims d;
+    d.nx = c.nx;
+    d.nu = c.nu;
+    d.na = c.nx + c.nu;
+    d.nc = c.nx + c.nu;
+    d.sA = c.nx * c.nx;
+    d.sB = c.nx * c.nu;
+    d.sF = c.nu * d.na + c.nu * c.nu;  // gains K_k (nu x na) | Hinv_k (nu x nu)
+    d.sAB = d.sA + d.sB;
+    d.S = d.sAB + d.sF;
+    return d;
+}
+
+__host__ __device__ inline RLds r_layout(const MpcConst& c) {
+    const Dims d = dims_of(c);
+    RLds L;
+    int o = 0;
+    auto take = [&](int cnt) {
+        const int r = o;
+        o += (cnt + 1) & ~1;
+        return r;
+    };
+    const int m = c.m, n = c.n, N = c.N, nx = c.nx, ns = c.ns;
+    L.t = take(m);
+    L.lam = take(m);
+    L.th = take(m);
+    L.rp = take(m);
+    L.rho = take(m);
+    L.rt = take(m);
+    L.w = take(m);
+    L.GdU = take(m);
+    L.X = take((N + 1) * nx);
+    L.dX = take((N + 1) * nx);
+    L.yb = take((N + 1) * nx);
+    L.psi = take(2 * nx);
+    L.U = take(n);
+    L.dU = take(n);
+    L.rd = take(n);
+    L.gU = take(n);
+    L.rh = take(n);
+    L.sig = take(N * ns);
+    L.dsig = take(N * ns);
+    L.Dsig = take(N * ns);
+    L.rsig = take(N * ns);
+    L.P = take(d.na * d.na);
+    L.pv = take(2 * d.na);
+    L.sb = take(2 * d.S);
+    L.T = take(d.na * d.nc);
+    L.G = take(d.nc * d.nc);
+    L.Hy = take(c.nu * d.na);
+    L.Kk = take(c.nu * d.na);
+    L.W = take(nx * nx);
+    L.gv = take(c.nu + nx);
+    L.total = o;
+    return L;
+}
+
+// per-agent global scratch (doubles): predictor direction (dt, dl), Riccati factors, best iterate
+struct RGlb {
+    size_t dta, dla, F, bU, bsig, total;
+};
+
+__host__ __device__ inline RGlb r_glb(const MpcConst& c) {
+    const Dims d = dims_of(c);
+    RGlb g;
+    size_t o = 0;
+    auto take = [&](size_t cnt) {
+        const size_t r = o;
+        o += (cnt + 31) & ~size_t(31);  // 256-byte aligned regions
+        return r;
+    };
+    g.dta = take(c.m);
+    g.dla = take(c.m);
+    g.F = take((size_t)c.N * d.sF);
+    g.bU = take(c.n);
+    g.bsig = take((size_t)c.N * c.ns);
+    g.total = o;
+    return g;
+}
+
+// Stage image of stage k: [A_k (nx x nx) | B_k (nx x nu) | K_k (nu x na) | Hinv_k (nu x nu)]
+// (the first `cnt` values).  Lane l holds values l, l + 64, ...
+struct StageSrc {
+    const double* A;
+    const double* B;
+    const double* F;
+    int sA, sB, sF;
+};
+
+__device__ __forceinline__ void stage_fetch(const StageSrc& s, int k, int cnt, double (&r)[kPer]) {
+    const int l = threadIdx.x;
+#pragma unroll
+    for (int q = 0; q < kPer; ++q) {
+        const int e = l + q * kWave;
+        double v = 0.0;
+        if (e < s.sA) v = s.A[(size_t)k * s.sA + e];
+        else if (e < s.sA + s.sB) v = s.B[(size_t)k * s.sB + (e - s.sA)];
+        else if (e < cnt) v = s.F[(size_t)k * s.sF + (e - s.sA - s.sB)];
+        r[q] = v;
+    }
+}
+
+__device__ __forceinline__ void stage_put(double* buf, int cnt, const double (&r)[kPer]) {
+    const int l = threadIdx.x;
+#pragma unroll
+    for (int q = 0; q < kPer; ++q) {
+        const int e = l + q * kWave;
+        if (e < cnt) buf[e] = r[q];
+    }
+}
+
+// 2R u_k + 2dR (du_k - du_{k+1}) for condensed variable index cidx (k*nu + i)
+__device__ __forceinline__ double rdr_grad(const MpcConst& c, const double* U, const double* up, int cidx) {
+    const int nu = c.nu, k = cidx / nu, i = cidx - k * nu;
+    double v = 0.0;
+    for (int j = 0; j < nu; ++j) {
+        const double uk = U[k * nu + j];
+        const double duk = uk - (k ? U[(k - 1) * nu + j] : up[j]);
+        const double dun = (k + 1 < c.N) ? U[(k + 1) * nu + j] - uk : 0.0;
+        v += 2.0 * c.R[i * nu + j] * uk + 2.0 * c.dR[i * nu + j] * (duk - dun);
+    }
+    return v;
+}
+
+// Value of row r at (X, U, sig): state rows C_{k,r} . X_{k+1} (+ sign * sig), input rows +-U
+__device__ __forceinline__ double row_value(const MpcConst& c, const double* __restrict__ C, int r, const double* X,
+                                            const double* U, const double* sig) {
+    if (r < c.ms) {
+        const int k = r / c.mc, rr = r - k * c.mc;
+        const double* cr = C + (size_t)r * c.nx;
+        const double* xk = X + (k + 1) * c.nx;
+        double v = 0.0;
+        for (int s = 0; s < c.nx; ++s) v = fma(cr[s], xk[s], v);
+        const int j = c.row_slack[rr];
+        if (sig && j >= 0) v += c.row_sign[rr] * sig[k * c.ns + j];
+        return v;
+    }
+    const int q = r - c.ms;
+    const double u = U[q >> 1];
+    return (q & 1) ? -u : u;
+}
+
+// Entry (s,u) of the per-stage constraint curvature M (stable group Schur form; see
+// mpc_ipm.hip m_entry): no-slack rows th c c'; slack group j
+// [q sum_r th_r c_r c_r' + sum_{r<r'} th_r th_r' (a_r - a_r')(a_r - a_r')'] / (q + sum th)
+__device__ __forceinline__ double m_entry(const MpcConst& c, const double* __restrict__ Ck, const double* th_k,
+                                          const double* Dsig_k, int s, int u) {
+    const int nx = c.nx;
+    double v = 0.0;
+    for (int r = 0; r < c.mc; ++r) {
+        const double* c1 = Ck + r * nx;
+        const double t1 = th_k[r];
+        const int j = c.row_slack[r];
+        if (j < 0) {
+            v = fma(t1 * c1[s], c1[u], v);
+            continue;
+        }
+        const double inv = 1.0 / Dsig_k[j];
+        const double q = 2.0 * c.Qs[j];
+        double g = q * t1 * c1[s] * c1[u];
+        const double s1 = c.row_sign[r];
+        for (int r2 = r + 1; r2 < c.mc; ++r2) {
+            if (c.row_slack[r2] != j) continue;
+            const double* c2 = Ck + r2 * nx;
+            const double s2 = c.row_sign[r2];
+            g += t1 * th_k[r2] * (s1 * c1[s] - s2 * c2[s]) * (s1 * c1[u] - s2 * c2[u]);
+        }
+        v = fma(g, inv, v);
+    }
+    return v;
+}
+
+// X_0 = x0 (or 0), X_{k+1} = A_k X_k + B_k U_k  (stage images through sb)
+__device__ void fwd_sim(const MpcConst& c, const Dims& d, const StageSrc& src, double* sb,
+                        const double* __restrict__ x0, const double* U, double* X) {
+    const int l = threadIdx.x, nx = d.nx, nu = d.nu, N = c.N;
+    double r[kPer];
+    stage_fetch(src, 0, d.sAB, r);
+    if (l < nx) X[l] = x0 ? x0[l] : 0.0;
+    stage_put(sb, d.sAB, r);
+    if (N > 1) stage_fetch(src, 1, d.sAB, r);
+    bar();
+    for (int k = 0; k < N; ++k) {
+        const double* Ak = sb + (k & 1) * d.S;
+        const double* Bk = Ak + d.sA;
+        if (l < nx) {
+            double v = 0.0;
+            for (int t = 0; t < nx; ++t) v = fma(Ak[l * nx + t], X[k * nx + t], v);
+            for (int i = 0; i < nu; ++i) v = fma(Bk[l * nu + i], U[k * nu + i], v);
+            X[(k + 1) * nx + l] = v;
+        }
+        if (k + 1 < N) {
+            stage_put(sb + ((k + 1) & 1) * d.S, d.sAB, r);
+            if (k + 2 < N) stage_fetch(src, k + 2, d.sAB, r);
+        }
+        bar();
+    }
+}
+
+// out_k = B_k' psi_{k+1}, psi_N = yb_N, psi_k = yb_k + A_k' psi_{k+1}   (out: n values)
+__device__ void adjoint(const MpcConst& c, const Dims& d, const StageSrc& src, double* sb, const double* yb,
+                        double* out, double* psi2) {
+    const int l = threadIdx.x, nx = d.nx, nu = d.nu, N = c.N;
+    double* pa = psi2;
+    double* pb = psi2 + nx;
+    double r[kPer];
+    stage_fetch(src, N - 1, d.sAB, r);
+    if (l < nx) pa[l] = yb[N * nx + l];
+    stage_put(sb + ((N - 1) & 1) * d.S, d.sAB, r);
+    if (N > 1) stage_fetch(src, N - 2, d.sAB, r);
+    bar();
+    for (int k = N - 1; k >= 0; --k) {
+        const double* Ak = sb + (k & 1) * d.S;
+        const double* Bk = Ak + d.sA;
+        if (l < nu) {
+            double v = 0.0;
+            for (int s = 0; s < nx; ++s) v = fma(Bk[s * nu + l], pa[s], v);
+            out[k * nu + l] = v;
+        } else if (k > 0 && l >= 32 && l < 32 + nx) {
+            const int t = l - 32;
+            double v = yb[k * nx + t];
+            for (int s = 0; s < nx; ++s) v = fma(Ak[s * nx + t], pa[s], v);
+            pb[t] = v;
+        }
+        if (k > 0) {
+            stage_put(sb + ((k - 1) & 1) * d.S, d.sAB, r);
+            if (k > 1) stage_fetch(src, k - 2, d.sAB, r);
+        }
+        bar();
+        double* tq = pa;
+        pa = pb;
+        pb = tq;
+    }
+}
+
+// Riccati factorisation of the Newton system at the current (th, Dsig): writes the gains
+// K_k = -Hvv^-1 Hvy and Hinv_k = Hvv^-1 of every stage into F.  Returns false on a
+// non-positive pivot (wave-uniform).
+__device__ bool riccati_factor(const MpcConst& c, const Dims& d, const RLds& L, double* sm,
+                               const double* __restrict__ A, const double* __restrict__ B,
+                               const double* __restrict__ C, double* __restrict__ F) {
+    const int l = threadIdx.x, nx = d.nx, nu = d.nu, na = d.na, nc = d.nc, N = c.N, mc = c.mc, ns = c.ns;
+    double* P = sm + L.P;
+    double* T = sm + L.T;
+    double* G = sm + L.G;
+    double* Hy = sm + L.Hy;
+    double* Kk = sm + L.Kk;
+    double* W = sm + L.W;
+    double* sb = sm + L.sb;
+    const double* th = sm + L.th;
+    const double* Dsig = sm + L.Dsig;
+    const StageSrc src{A, B, nullptr, d.sA, d.sB, d.sF};
+    double r[kPer];
+    stage_fetch(src, N - 1, d.sAB, r);
+    // P_N = blkdiag(W_N, 0),  W_N = 2Q + M_N (stage rows of X_N)
+    for (int e = l; e < na * na; e += kWave) {
+        const int i = e / na, j = e - i * na;
+        P[e] = (i < nx && j < nx) ? 2.0 * c.Q[i * nx + j] +
+                                        m_entry(c, C + (size_t)(N - 1) * mc * nx, th + (N - 1) * mc,
+                                                Dsig + (N - 1) * ns, i, j)
+                                  : 0.0;
+    }
+    stage_put(sb + ((N - 1) & 1) * d.S, d.sAB, r);
+    if (N > 1) stage_fetch(src, N - 2, d.sAB, r);
+    bar();
+    bool ok = true;
+    for (int k = N - 1; k >= 0; --k) {
+        const double* Ak = sb + (k & 1) * d.S;
+        const double* Bk = Ak + d.sA;
+        // T = P[:, :nx] [A_k | B_k]   (na x nc);  W_k = 2Q + M_k for the state X_k (k >= 1)
+        for (int e = l; e < na * nc; e += kWave) {
+            const int i = e / nc, j = e - i * nc;
+            double v = 0.0;
+            if (j < nx)
+                for (int s = 0; s < nx; ++s) v = fma(P[i * na + s], Ak[s * nx + j], v);
+            else
+                for (int s = 0; s < nx; ++s) v = fma(P[i * na + s], Bk[s * nu + (j - nx)], v);
+            T[e] = v;
+        }
+        if (k >= 1)
+            for (int e = l; e < nx * nx; e += kWave) {
+                const int i = e / nx, j = e - i * nx;
+                W[e] = 2.0 * c.Q[e] + m_entry(c, C + (size_t)(k - 1) * mc * nx, th + (k - 1) * mc,
+                                              Dsig + (k - 1) * ns, i, j);
+            }
+        bar();
+        // G = [A_k | B_k]' T[:nx, :]   (nc x nc, lower triangle)
+        for (int e = l; e < nc * nc; e += kWave) {
+            const int i = e / nc, j = e - i * nc;
+            if (j > i) continue;
+            const double* ci = (i < nx) ? Ak + i : Bk + (i - nx);
+            const int ldi = (i < nx) ? nx : nu;
+            double v = 0.0;
+            for (int s = 0; s < nx; ++s) v = fma(ci[s * ldi], T[s * nc + j], v);
+            G[e] = v;
+        }
+        bar();
+        // Hvv = 2R + 2dR + diag(th_u) + B'Pxx B + Pux B + B'Pxu + Puu  (every lane, nu <= 4),
+        // its Cholesky factor and inverse in registers
+        double Lf[CMPC_MAX_NU][CMPC_MAX_NU], Hi[CMPC_MAX_NU][CMPC_MAX_NU];
+#pragma unroll
+        for (int a = 0; a < CMPC_MAX_NU; ++a)
+#pragma unroll
+            for (int b = 0; b < CMPC_MAX_NU; ++b) {
+                double v = 0.0;
+                if (a < nu && b <= a) {
+                    v = 2.0 * c.R[a * nu + b] + 2.0 * c.dR[a * nu + b] + G[(nx + a) * nc + nx + b] +
+                        T[(nx + a) * nc + nx + b] + T[(nx + b) * nc + nx + a] + P[(nx + a) * na + nx + b];
+                    if (a == b) {
+                        const int rr = c.ms + 2 * (k * nu + a);
+                        v += th[rr] + th[rr + 1];
+                    }
+                }
+                Lf[a][b] = v;
+            }
+#pragma unroll
+        for (int j = 0; j < CMPC_MAX_NU; ++j) {
+            if (j < nu) {
+                double dj = Lf[j][j];
+#pragma unroll
+                for (int p = 0; p < j; ++p) dj = fma(-Lf[j][p], Lf[j][p], dj);
+                ok = ok && (dj > 0.0);
+                const double rs = rsqrt_d(dj > 0.0 ? dj : 1.0);
+                Lf[j][j] = dj * rs;
+#pragma unroll
+                for (int i = j + 1; i < CMPC_MAX_NU; ++i) {
+                    if (i < nu) {
+                        double v = Lf[i][j];
+#pragma unroll
+                        for (int p = 0; p < j; ++p) v = fma(-Lf[i][p], Lf[j][p], v);
+                        Lf[i][j] = v * rs;
+                    }
+                }
+            }
+        }
+        // Li = L^-1 (lower), Hinv = Li' Li
+        double Li[CMPC_MAX_NU][CMPC_MAX_NU];
+#pragma unroll
+        for (int i = 0; i < CMPC_MAX_NU; ++i)
+#pragma unroll
+            for (int j = 0; j < CMPC_MAX_NU; ++j) Li[i][j] = 0.0;
+#pragma unroll
+        for (int i = 0; i < CMPC_MAX_NU; ++i) {
+            if (i < nu) {
+                const double di = rcp_d(Lf[i][i]);
+                Li[i][i] = di;
+#pragma unroll
+                for (int j = 0; j < i; ++j) {
+                    double v = 0.0;
+#pragma unroll
+                    for (int p = j; p < i; ++p) v = fma(Lf[i][p], Li[p][j], v);
+                    Li[i][j] = -v * di;
+                }
+            }
+        }
+#pragma unroll
+        for (int a = 0; a < CMPC_MAX_NU; ++a)
+#pragma unroll
+            for (int b = 0; b < CMPC_MAX_NU; ++b) {
+                double v = 0.0;
+#pragma unroll
+                for (int p = 0; p < CMPC_MAX_NU; ++p) v = fma(Li[p][a], Li[p][b], v);
+                Hi[a][b] = v;
+            }
+        // Hvy = [B'Pxx A + Pux A | -2dR] (nu x na);  K_k = -Hinv Hvy
+        double* Fk = F + (size_t)k * d.sF;
+        for (int e = l; e < nu * na; e += kWave) {
+            const int a = e / na, j = e - a * na;
+            double kv = 0.0, ha = 0.0;
+#pragma unroll
+            for (int b = 0; b < CMPC_MAX_NU; ++b) {
+                if (b < nu) {
+                    const double hv = (j < nx) ? G[(nx + b) * nc + j] + T[(nx + b) * nc + j] : -2.0 * c.dR[b * nu + (j - nx)];
+                    double hab = 0.0;
+#pragma unroll
+                    for (int a2 = 0; a2 < CMPC_MAX_NU; ++a2)
+                        if (a2 == a) hab = Hi[a2][b];
+                    kv = fma(-hab, hv, kv);
+                    if (b == a) ha = hv;
+                }
+            }
+            Kk[e] = kv;
+            Hy[e] = ha;
+            Fk[e] = kv;
+        }
+        if (l < nu * nu) {
+            const int a = l / nu, b = l - a * nu;
+            double v = 0.0;
+#pragma unroll
+            for (int a2 = 0; a2 < CMPC_MAX_NU; ++a2)
+#pragma unroll
+                for (int b2 = 0; b2 < CMPC_MAX_NU; ++b2)
+                    if (a2 == a && b2 == b) v = Hi[a2][b2];
+            Fk[nu * na + l] = v;
+        }
+        if (k > 0) {
+            stage_put(sb + ((k - 1) & 1) * d.S, d.sAB, r);
+            if (k > 1) stage_fetch(src, k - 2, d.sAB, r);
+        }
+        bar();
+        if (k == 0) break;
+        // P_k = blkdiag(W_k + A'Pxx A, 2dR) + Hvy' K_k   (symmetric: lower triangle mirrored)
+        for (int e = l; e < na * na; e += kWave) {
+            const int i = e / na, j = e - i * na;
+            if (j > i) continue;
+            double v = (i < nx) ? W[i * nx + j] + G[i * nc + j]
+                                : ((j >= nx) ? 2.0 * c.dR[(i - nx) * nu + (j - nx)] : 0.0);
+            for (int a = 0; a < nu; ++a) v = fma(Hy[a * na + i], Kk[a * na + j], v);
+            P[i * na + j] = v;
+            P[j * na + i] = v;
+        }
+        bar();
+    }
+    return ok;
+}
+
+// Solve the Newton system for the right-hand side rh (n values): dU (n) and dX ((N+1) nx,
+// dX_0 = 0), with the gains of riccati_factor.
+__device__ void riccati_solve(const MpcConst& c, const Dims& d, const RLds& L, double* sm,
+                              const double* __restrict__ A, const double* __restrict__ B,
+                              const double* __restrict__ F) {
+    const int l = threadIdx.x, nx = d.nx, nu = d.nu, na = d.na, N = c.N;
+    double* sb = sm + L.sb;
+    double* pv = sm + L.pv;
+    double* gv = sm + L.gv;
+    double* dU = sm + L.dU;
+    double* dX = sm + L.dX;
+    const double* rh = sm + L.rh;
+    const StageSrc src{A, B, F, d.sA, d.sB, d.sF};
+    double r[kPer];
+    // backward: p_N = 0;  gv = -rh_k + B'p_x + p_u;  kk_k = -Hinv gv (into dU);  p_k = [A'p_x; 0] + K' gv
+    stage_fetch(src, N - 1, d.S, r);
+    if (l < na) pv[l] = 0.0;
+    stage_put(sb + ((N - 1) & 1) * d.S, d.S, r);
+    if (N > 1) stage_fetch(src, N - 2, d.S, r);
+    bar();
+    for (int k = N - 1; k >= 0; --k) {
+        const double* Ak = sb + (k & 1) * d.S;
+        const double* Bk = Ak + d.sA;
+        const double* Kg = Bk + d.sB;
+        const double* Hg = Kg + nu * na;
+        const double* pc = pv + ((N - 1 - k) & 1) * na;
+        double* pn = pv + ((N - k) & 1) * na;
+        if (l < nu) {
+            double v = pc[nx + l] - rh[k * nu + l];
+            for (int s = 0; s < nx; ++s) v = fma(Bk[s * nu + l], pc[s], v);
+            gv[l] = v;
+        } else if (l >= 32 && l < 32 + nx) {
+            const int j = l - 32;
+            double v = 0.0;
+            for (int s = 0; s < nx; ++s) v = fma(Ak[s * nx + j], pc[s], v);
+            gv[nu + j] = v;
+        }
+        bar();
+        if (l < nu) {
+            double v = 0.0;
+            for (int b = 0; b < nu; ++b) v = fma(-Hg[l * nu + b], gv[b], v);
+            dU[k * nu + l] = v;
+        } else if (l >= 32 && l < 32 + na) {
+            const int j = l - 32;
+            double v = (j < nx) ? gv[nu + j] : 0.0;
+            for (int a = 0; a < nu; ++a) v = fma(Kg[a * na + j], gv[a], v);
+            pn[j] = v;
+        }
+        if (k > 0) {
+            stage_put(sb + ((k - 1) & 1) * d.S, d.S, r);
+            if (k > 1) stage_fetch(src, k - 2, d.S, r);
+        }
+        bar();
+    }
+    // forward: y_0 = 0;  v_k = kk_k + K_k y_k;  dX_{k+1} = A_k dX_k + B_k v_k
+    stage_fetch(src, 0, d.S, r);
+    if (l < nx) dX[l] = 0.0;
+    stage_put(sb, d.S, r);
+    if (N > 1) stage_fetch(src, 1, d.S, r);
+    bar();
+    for (int k = 0; k < N; ++k) {
+        const double* Ak = sb + (k & 1) * d.S;
+        const double* Bk = Ak + d.sA;
+        const double* Kg = Bk + d.sB;
+        if (l < nu) {
+            double v = dU[k * nu + l];
+            for (int j = 0; j < nx; ++j) v = fma(Kg[l * na + j], dX[k * nx + j], v);
+            if (k > 0)
+                for (int b = 0; b < nu; ++b) v = fma(Kg[l * na + nx + b], dU[(k - 1) * nu + b], v);
+            dU[k * nu + l] = v;
+        }
+        bar();
+        if (l < nx) {
+            double v = 0.0;
+            for (int t = 0; t < nx; ++t) v = fma(Ak[l * nx + t], dX[k * nx + t], v);
+            for (int a = 0; a < nu; ++a) v = fma(Bk[l * nu + a], dU[k * nu + a], v);
+            dX[(k + 1) * nx + l] = v;
+        }
+        if (k + 1 < N) {
+            stage_put(sb + ((k + 1) & 1) * d.S, d.S, r);
+            if (k + 2 < N) stage_fetch(src, k + 2, d.S, r);
+        }
+        bar();
+    }
+}
+
+__global__ __launch_bounds__(kWave) void mpc_riccati_kernel(const MpcConst c, const MpcPtrs P) {
+    extern __shared__ __attribute__((aligned(16))) double sm[];
+    const int b = blockIdx.x;
+    const int l = threadIdx.x;
+    const RLds L = r_layout(c);
+    const Dims d = dims_of(c);
+    const RGlb gl = r_glb(c);
+    const int nx = c.nx, nu = c.nu, N = c.N, ns = c.ns, mc = c.mc, n = c.n, ms = c.ms, m = c.m;
+
+    const double* __restrict__ A = P.A + (size_t)b * N * nx * nx;
+    const double* __restrict__ B = P.B + (size_t)b * N * nx * nu;
+    const double* __restrict__ x0 = P.x0 + (size_t)b * nx;
+    const double* __restrict__ up = P.up + (size_t)b * nu;
+    const double* __restrict__ pl = P.p + (size_t)b * (N + 1) * nx;
+    const double* __restrict__ C = P.C + (size_t)b * N * mc * nx;
+    const double* __restrict__ h = P.h + (size_t)b * N * mc;
+    double* __restrict__ ws = P.ws + (size_t)b * gl.total;
+    double* dta = ws + gl.dta;
+    double* dla = ws + gl.dla;
+    double* F = ws + gl.F;
+    double* bU = ws + gl.bU;
+    double* bsig = ws + gl.bsig;
+
+    double* t = sm + L.t;
+    double* lam = sm + L.lam;
+    double* th = sm + L.th;
+    double* rp = sm + L.rp;
+    double* rho = sm + L.rho;
+    double* rt = sm + L.rt;
+    double* w = sm + L.w;
+    double* GdU = sm + L.GdU;
+    double* X = sm + L.X;
+    double* dX = sm + L.dX;
+    double* yb = sm + L.yb;
+    double* psi = sm + L.psi;
+    double* U = sm + L.U;
+    double* dU = sm + L.dU;
+    double* rd = sm + L.rd;
+    double* gU = sm + L.gU;
+    double* rh = sm + L.rh;
+    double* sig = sm + L.sig;
+    double* dsig = sm + L.dsig;
+    double* Dsig = sm + L.Dsig;
+    double* rsig = sm + L.rsig;
+    double* sb = sm + L.sb;
+    const StageSrc sAB{A, B, nullptr, d.sA, d.sB, d.sF};
+
+    for (int i = l; i < L.total; i += kWave) sm[i] = 0.0;
+    bar();
+
+    // ---- row right-hand sides; inactive rows carry w = +inf ----
+    for (int r = l; r < m; r += kWave) {
+        double v;
+        if (r < ms) {
+            v = h[r];
+        } else {
+            const int q = r - ms, i = (q >> 1) % nu;
+            v = (q & 1) ? -c.u_lb[i] : c.u_ub[i];
+        }
+        w[r] = isfinite(v) ? v : INFINITY;
+    }
+    bar();
+    fwd_sim(c, d, sAB, sb, x0, U, X);
+
+    double mact_l = 0.0, sp_l = 1.0;
+    for (int r = l; r < m; r += kWave) {
+        if (isfinite(w[r])) {
+            const double g = row_value(c, C, r, X, U, sig);
+            t[r] = fmax(w[r] - g, 1.0);
+            lam[r] = 1.0;
+            mact_l += 1.0;
+            sp_l = fmax(sp_l, fabs(w[r]));
+        } else {
+            t[r] = 1.0;
+            lam[r] = 0.0;
+        }
+    }
+    const double mact = fmax(wave_sum(mact_l), 1.0);
+    const double scale_p = wave_max(sp_l);
+    bar();
+
+    double best_m = INFINITY, best_kkt = INFINITY;
+    int best_it = 0, stop = kStopMaxIter, it;
+    double kkt = INFINITY;
+    for (it = 1; it <= c.max_iter; ++it) {
+        // ================= residuals (as mpc_ipm.hip) =================
+        for (int i = l; i < (N + 1) * nx; i += kWave) {
+            const int k = i / nx, s = i - k * nx;
+            double v = 2.0 * pl[i];
+            for (int u = 0; u < nx; ++u) v = fma(2.0 * c.Q[s * nx + u], X[k * nx + u], v);
+            yb[i] = v;
+        }
+        bar();
+        adjoint(c, d, sAB, sb, yb, gU, psi);
+        double gs_l = 1.0;
+        for (int i = l; i < n; i += kWave) {
+            gU[i] += rdr_grad(c, U, up, i);
+            gs_l = nmax(gs_l, fabs(gU[i]));
+        }
+        const double gscale = wave_max(gs_l);
+        for (int i = l; i < N * nx; i += kWave) {  // + C' lambda on stages 1..N
+            const int k = i / nx, s = i - k * nx;
+            double v = 0.0;
+            for (int r = 0; r < mc; ++r) v = fma(lam[k * mc + r], C[((size_t)k * mc + r) * nx + s], v);
+            yb[(k + 1) * nx + s] += v;
+        }
+        bar();
+        adjoint(c, d, sAB, sb, yb, rd, psi);
+        double nrd_l = 0.0, nrs_l = 0.0, nrp_l = 0.0, mu_l = 0.0;
+        for (int i = l; i < n; i += kWave) {
+            const int r = ms + 2 * i;
+            rd[i] += rdr_grad(c, U, up, i) + lam[r] - lam[r + 1];
+            nrd_l = nmax(nrd_l, fabs(rd[i]));
+        }
+        for (int i = l; i < N * ns; i += kWave) {
+            const int k = i / ns, j = i - k * ns;
+            double v = 2.0 * c.Qs[j] * sig[i];
+            for (int r = 0; r < mc; ++r)
+                if (c.row_slack[r] == j) v += c.row_sign[r] * lam[k * mc + r];
+            rsig[i] = v;
+            nrs_l = nmax(nrs_l, fabs(v));
+        }
+        for (int r = l; r < m; r += kWave) {
+            if (isfinite(w[r])) {
+                const double v = row_value(c, C, r, X, U, sig) + t[r] - w[r];
+                rp[r] = v;
+                nrp_l = nmax(nrp_l, fabs(v));
+                mu_l += t[r] * lam[r];
+            } else {
+                rp[r] = 0.0;
+            }
+        }
+        const double mu = wave_sum(mu_l) / mact;
+        const double res = nmax(nmax(wave_max(nrd_l) / gscale, wave_max(nrs_l) / c.qs_max), wave_max(nrp_l) / scale_p);
+        kkt = nmax(res, mu);
+        const double merit = nmax(res, 1e4 * mu);
+        if (!isfinite(merit)) {
+            stop = kStopNonFinite;
+            break;
+        }
+        if (merit < best_m) {
+            best_m = merit;
+            best_kkt = kkt;
+            best_it = it;
+            for (int i = l; i < n; i += kWave) bU[i] = U[i];
+            for (int i = l; i < N * ns; i += kWave) bsig[i] = sig[i];
+        }
+        if (merit < c.tol) {
+            stop = kStopConverged;
+            break;
+        }
+        if (best_m < 1e3 * c.tol && it - best_it >= kStallIters) {
+            stop = kStopStalled;
+            break;
+        }
+        bar();
+
+        // ================= Newton system: Riccati factorisation =================
+        for (int r = l; r < m; r += kWave) th[r] = isfinite(w[r]) ? lam[r] / t[r] : 0.0;
+        bar();
+        for (int i = l; i < N * ns; i += kWave) {
+            const int k = i / ns, j = i - k * ns;
+            double v = 2.0 * c.Qs[j];
+            for (int r = 0; r < mc; ++r)
+                if (c.row_slack[r] == j) v += th[k * mc + r];
+            Dsig[i] = v;
+        }
+        bar();
+        if (!riccati_factor(c, d, L, sm, A, B, C, F)) {
+            stop = kStopBreakdown;
+            break;
+        }
+
+        // ================= predictor / corrector =================
+        double sig_c = 0.0, alpha = 0.0;
+        for (int pass = 0; pass < 2; ++pass) {
+            for (int r = l; r < m; r += kWave) {
+                if (!isfinite(w[r])) {
+                    rho[r] = 0.0;
+                    continue;
+                }
+                double rc = -t[r] * lam[r];
+                if (pass) rc += sig_c * mu - dta[r] * dla[r];
+                rho[r] = (rc + lam[r] * rp[r]) / t[r];
+            }
+            bar();
+            for (int r = l; r < m; r += kWave) {
+                double v = rho[r];
+                if (r < ms) {
+                    const int k = r / mc, rr = r - k * mc, j = c.row_slack[rr];
+                    if (j >= 0) {
+                        const double q = 2.0 * c.Qs[j];
+                        v = q * rho[r] - th[r] * c.row_sign[rr] * rsig[k * ns + j];
+                        for (int r2 = 0; r2 < mc; ++r2) {
+                            if (r2 == rr || c.row_slack[r2] != j) continue;
+                            const int R2 = k * mc + r2;
+                            v += th[R2] * rho[r] - th[r] * c.row_sign[rr] * c.row_sign[r2] * rho[R2];
+                        }
+                        v /= Dsig[k * ns + j];
+                    }
+                }
+                rt[r] = v;
+            }
+            bar();
+            for (int i = l; i < (N + 1) * nx; i += kWave) {
+                const int k = i / nx, s = i - k * nx;
+                double v = 0.0;
+                if (k > 0)
+                    for (int r = 0; r < mc; ++r) v = fma(rt[(k - 1) * mc + r], C[((size_t)(k - 1) * mc + r) * nx + s], v);
+                yb[i] = v;
+            }
+            bar();
+            adjoint(c, d, sAB, sb, yb, rh, psi);
+            // rhs = -rd - G' rt
+            for (int i = l; i < n; i += kWave) rh[i] = -rd[i] - (rh[i] + rt[ms + 2 * i] - rt[ms + 2 * i + 1]);
+            bar();
+            riccati_solve(c, d, L, sm, A, B, F);
+            for (int r = l; r < m; r += kWave) GdU[r] = row_value(c, C, r, dX, dU, nullptr);
+            bar();
+            for (int i = l; i < N * ns; i += kWave) {
+                const int k = i / ns, j = i - k * ns;
+                double v = rsig[i];
+                for (int r = 0; r < mc; ++r)
+                    if (c.row_slack[r] == j) {
+                        const int R1 = k * mc + r;
+                        v += c.row_sign[r] * (rho[R1] + th[R1] * GdU[R1]);
+                    }
+                dsig[i] = -v / Dsig[i];
+            }
+            bar();
+            double amax_l = 1.0e300;
+            double* dtp = pass ? rho : dta;  // corrector reuses rho/rt storage for (dt, dl)
+            double* dlp = pass ? rt : dla;
+            for (int r = l; r < m; r += kWave) {
+                if (!isfinite(w[r])) {
+                    dtp[r] = 0.0;
+                    dlp[r] = 0.0;
+                    continue;
+                }
+                double sd = 0.0;
+                if (r < ms) {
+                    const int k = r / mc, rr = r - k * mc, j = c.row_slack[rr];
+                    if (j >= 0) sd = c.row_sign[rr] * dsig[k * ns + j];
+                }
+                const double rho_r = rho[r];
+                const double dtv = -rp[r] - GdU[r] - sd;
+                const double dlv = rho_r + th[r] * (GdU[r] + sd);
+                dtp[r] = dtv;
+                dlp[r] = dlv;
+                if (dtv < 0.0) amax_l = fmin(amax_l, -t[r] / dtv);
+                if (dlv < 0.0) amax_l = fmin(amax_l, -lam[r] / dlv);
+            }
+            const double amax = fmin(wave_min(amax_l), 1.0e300);
+            bar();
+            if (!pass) {
+                const double a = fmin(amax, 1.0);
+                double mua_l = 0.0;
+                for (int r = l; r < m; r += kWave)
+                    if (isfinite(w[r])) mua_l += (t[r] + a * dta[r]) * (lam[r] + a * dla[r]);
+                const double mu_aff = wave_sum(mua_l) / mact;
+                const double ratio = mu > 0.0 ? mu_aff / mu : 0.0;
+                sig_c = ratio * ratio * ratio;
+            } else {
+                alpha = fmin(1.0, 0.995 * amax);
+                // stay in the wide neighbourhood t_r lam_r >= gamma mu(alpha) (see kNbhdGamma)
+                for (int bt = 0; bt < kMaxBacktrack; ++bt) {
+                    double mn_l = 0.0, pm_l = INFINITY;
+                    for (int r = l; r < m; r += kWave)
+                        if (isfinite(w[r])) {
+                            const double pr = (t[r] + alpha * rho[r]) * (lam[r] + alpha * rt[r]);
+                            mn_l += pr;
+                            pm_l = fmin(pm_l, pr);
+                        }
+                    if (wave_min(pm_l) >= kNbhdGamma * (wave_sum(mn_l) / mact)) break;
+                    alpha *= 0.8;
+                }
+            }
+        }
+        // ---- update (corrector direction: dU, dX, dsig, (rho, rt) = (dt, dl)) ----
+        for (int i = l; i < n; i += kWave) U[i] = fma(alpha, dU[i], U[i]);
+        for (int i = l; i < N * ns; i += kWave) sig[i] = fma(alpha, dsig[i], sig[i]);
+        for (int i = l; i < (N + 1) * nx; i += kWave) X[i] = fma(alpha, dX[i], X[i]);
+        for (int r = l; r < m; r += kWave)
+            if (isfinite(w[r])) {
+                t[r] = fma(alpha, rho[r], t[r]);
+                lam[r] = fma(alpha, rt[r], lam[r]);
+            }
+        bar();
+    }
+    if (it > c.max_iter) it = c.max_iter;
+    bar();
+    int status = CMPC_SOLVED;
+    if (stop != kStopConverged) {
+        if (best_it > 0) {  // restore the best iterate
+            for (int i = l; i < n; i += kWave) U[i] = bU[i];
+            for (int i = l; i < N * ns; i += kWave) sig[i] = bsig[i];
+            kkt = best_kkt;
+        }
+        status = stop_status(stop, best_m, c.tol);
+    }
+    bar();
+
+    // ---- output in the reference layout ----
+    fwd_sim(c, d, sAB, sb, x0, U, X);
+    const int nxe = nx + ns;
+    const size_t nz = (size_t)nxe * (N + 1) + 2 * (size_t)n;
+    double* z = P.z + (size_t)b * nz;
+    for (int i = l; i < (N + 1) * nxe; i += kWave) {
+        const int k = i / nxe, s = i - k * nxe;
+        z[i] = (s < nx) ? X[k * nx + s] : (k ? sig[(k - 1) * ns + (s - nx)] : 0.0);
+    }
+    for (int i = l; i < n; i += kWave) {
+        const int k = i / nu, j = i - k * nu;
+        z[(size_t)(N + 1) * nxe + i] = U[i];
+        z[(size_t)(N + 1) * nxe + n + i] = U[i] - (k ? U[(k - 1) * nu + j] : up[j]);
+    }
+    if (l == 0) {
+        if (P.kkt) P.kkt[b] = kkt;
+        if (P.iters) P.iters[b] = it;
+        if (P.status) P.status[b] = status;
+    }
+}
+
+}  // namespace
+
+size_t mpc_riccati_lds_bytes(const MpcConst& c) { return sizeof(double) * (size_t)r_layout(c).total; }
+
+size_t mpc_riccati_ws_doubles(const MpcConst& c) { return r_glb(c).total; }
+
+hipError_t mpc_riccati_launch(const MpcConst& c, const MpcPtrs& p, int batch, hipStream_t s) {
+    if (batch == 0) return hipSuccess;
+    if (!p.ws) return hipErrorInvalidValue;
+    const size_t lds = mpc_riccati_lds_bytes(c);
+    hipError_t e = hipFuncSetAttribute((const void*)mpc_riccati_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       (int)lds);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(mpc_riccati_kernel, dim3(batch), dim3(kWave), lds, s, c, p);
+    return hipGetLastError();
+}
+
+}  // namespace cmpc

@@ -63,15 +63,18 @@ extern "C" {
 #define CMPC_MAX_NU 4
 #define CMPC_MAX_NS 4
 #define CMPC_MAX_MC 16
-#define CMPC_MAX_NCOND 64      /* one-wavefront-per-agent solvers (fp64) */
-#define CMPC_MAX_NCOND_WG 256  /* workgroup-per-agent solver (fp32, or fp64 while LDS allows) */
+#define CMPC_MAX_NCOND 64      /* condensed one-wavefront-per-agent solvers (fp64); beyond it the
+                                  stage-wise Riccati solver runs any horizon whose rows fit LDS
+                                  (N = 125, nb <= 4 at nx = 9) */
+#define CMPC_MAX_NCOND_WG 256  /* fp32 workgroup-per-agent solver (CMPC_FLAG_FP32) */
 
 typedef struct cmpc_ctx cmpc_ctx;
 
 #define CMPC_FLAG_GENERIC 1  /* force the generic (runtime-dimension) kernel */
 #define CMPC_FLAG_FP32 8     /* fp32 workgroup-per-agent solver (long horizons, BASELINE cfg5);
                                 opts.tol should then be ~1e-5 */
-#define CMPC_FLAG_ALL (CMPC_FLAG_GENERIC | CMPC_FLAG_FP32)  /* any other bit: CMPC_ERR_ARG */
+#define CMPC_FLAG_RICCATI 16 /* force the stage-wise Riccati solver (fp64; the default when N*nu > 64) */
+#define CMPC_FLAG_ALL (CMPC_FLAG_GENERIC | CMPC_FLAG_FP32 | CMPC_FLAG_RICCATI)  /* other bits: CMPC_ERR_ARG */
 
 typedef struct {
     double tol;    /* relative stationarity/feasibility tolerance (complementarity: 1e-4*tol); <= 0 selects 1e-9 */

@@ -208,6 +208,9 @@ static int solve_one(const shared_t* S, const agent_t* a, double tol, int max_it
     double *bU = wk->bU, *bsig = wk->bsig;
     int it;
     double kkt = INFINITY;
+#ifdef SHORT_STEP
+    double alpha_prev = 1.0;
+#endif
     for (it = 1; it <= max_iter; ++it) {
         /* ---- residuals ---- */
         double* ybar = wk->ybar;
@@ -354,6 +357,9 @@ static int solve_one(const shared_t* S, const agent_t* a, double tol, int max_it
 
         /* ---- predictor / corrector ---- */
         double sig_c = 0.0, mu_aff = 0.0;
+#ifdef RETRY_SIGMA
+        int retried = 0;
+#endif
         for (int pass = 0; pass < 2; ++pass) {
             for (int r = 0; r < m; ++r) {
                 if (!wk->act[r]) { wk->rho[r] = 0.0; continue; }
@@ -425,8 +431,14 @@ static int solve_one(const shared_t* S, const agent_t* a, double tol, int max_it
                     if (wk->act[r]) mu_aff += (t[r] + al * dt[r]) * (lam[r] + al * dl[r]);
                 mu_aff /= mact ? mact : 1;
                 sig_c = mu > 0 ? pow(mu_aff / mu, 3.0) : 0.0;
+#ifdef SHORT_STEP
+                if (alpha_prev < SHORT_STEP) sig_c = fmax(sig_c, SIGMA_MIN);
+#endif
             } else {
                 al = 0.995 * al;
+#ifdef RETRY_SIGMA
+                const double al_free = al > 1.0 ? 1.0 : al;
+#endif
                 if (al > 1.0) al = 1.0;
                 /* keep the iterate in the wide neighbourhood t_r lambda_r >= gamma mu(al):
                    without it Mehrotra's corrector can cycle on degenerate collision rows
@@ -456,6 +468,18 @@ static int solve_one(const shared_t* S, const agent_t* a, double tol, int max_it
                         fprintf(stderr, "      step al %.3e sigma %.2e mu_aff/mu %.2e blocking %d (t %.2e lam %.2e)\n",
                                 al, sig_c, mu > 0 ? mu_aff / mu : 0.0, blk, t[blk % 10000], lam[blk % 10000]);
                 }
+#endif
+#ifdef RETRY_SIGMA
+                /* the neighbourhood cut the corrector step hard: recompute it once with more centring */
+                if (!retried && al < RETRY_FRAC * al_free) {
+                    retried = 1;
+                    sig_c = fmax(sig_c, RETRY_SIGMA);
+                    pass = 0;
+                    continue;
+                }
+#endif
+#ifdef SHORT_STEP
+                alpha_prev = al;
 #endif
                 for (int c = 0; c < n; ++c) U[c] += al * wk->dU[c];
                 for (int q = 0; q < N * ns; ++q) sig[q] += al * wk->dsig[q];

@@ -226,16 +226,29 @@ def main():
     os.makedirs(OUT, exist_ok=True)
     R = _import_reference()
     x0db = R["x0_database"]
-    map_goldens(R)
-    schedule_goldens(R)
-    run_loop(R, "lpv_n10_a2", 10, x0db[0:2], steps=4)
-    run_loop(R, "lpv_n30_a3", 30, x0db[0:3], steps=4)
+    only = set(sys.argv[1:])          # optional subset of fixture names
+    want = lambda nm: not only or nm in only
+    if want("maps"):
+        map_goldens(R)
+    if want("schedule"):
+        schedule_goldens(R)
+    if want("lpv_n10_a2"):
+        run_loop(R, "lpv_n10_a2", 10, x0db[0:2], steps=4)
+    if want("lpv_n30_a3"):
+        run_loop(R, "lpv_n30_a3", 30, x0db[0:3], steps=4)
     slow = [list(x0db[0]), list(x0db[1])]
     slow[0][0] = 0.1                                   # vx < 0.2 -> LPV_Planner.py:505-517
     slow[1][0] = 0.15
-    run_loop(R, "lpv_n10_lowspeed", 10, slow, steps=3)
-    run_loop(R, "lpv_n10_a1", 10, x0db[0:1], steps=2)  # no neighbours: nb = 0
-    run_loop(R, "lpv_n20_a4", 20, x0db[0:4], steps=2)
+    if want("lpv_n10_lowspeed"):
+        run_loop(R, "lpv_n10_lowspeed", 10, slow, steps=3)
+    if want("lpv_n10_a1"):
+        run_loop(R, "lpv_n10_a1", 10, x0db[0:1], steps=2)  # no neighbours: nb = 0
+    if want("lpv_n20_a4"):
+        run_loop(R, "lpv_n20_a4", 20, x0db[0:4], steps=2)
+    if want("lpv_n125_a3"):
+        # the reference's shipped configuration: N = 125, 3 agents, Highway
+        # (planner/scripts/config_files/config_LPV.py:13-24, LPV_HP_N_main.py)
+        run_loop(R, "lpv_n125_a3", 125, x0db[0:3], steps=2)
 
 
 if __name__ == "__main__":

@@ -138,13 +138,51 @@ def solve_qp(P, q, A, l, u, tol=1e-12, max_iter=200, verbose=False):
         _, x, yv, lam = best
         if best[0] < 1e-9:
             status = "solved"
-    # OSQP-convention multipliers on the original rows
-    y = np.zeros(A.shape[0])
-    y[eq] = yv
     nup = int(up.sum())
-    y[up] += lam[:nup]
-    y[lo] -= lam[nup:]
+
+    def osqp_y(yv_, lam_):
+        # OSQP-convention multipliers on the original rows
+        y_ = np.zeros(A.shape[0])
+        y_[eq] = yv_
+        y_[up] += lam_[:nup]
+        y_[lo] -= lam_[nup:]
+        return y_
+
+    y = osqp_y(yv, lam)
     cert = kkt_certificate(P, q, A, l, u, x, y)
+    # Polish (as OSQP's polish=True, which the reference sets, LPV_Planner.py:232): re-solve
+    # with the rows the IPM found active as equalities.  Interior-point iterates approach a
+    # weakly active (degenerate) bound only like sqrt(mu); the polished point sits on it.
+    # Kept only when it is primal and dual feasible and its certificate is no worse.
+    if mi:
+        act = lam > s
+        Ca, da = C[act], d[act]
+        ka = int(act.sum())
+        K = np.zeros((n + me + ka, n + me + ka))
+        K[:n, :n] = P
+        K[:n, n:n + me] = E.T
+        K[:n, n + me:] = Ca.T
+        K[n:n + me, :n] = E
+        K[n + me:, :n] = Ca
+        rhs = np.hstack([-q, e, da])
+        try:   # LU (not lstsq: its rank cut-off drops the 1e7-scaled slack directions)
+            lu = sla.lu_factor(K)
+            sol = sla.lu_solve(lu, rhs)
+            sol = sol + sla.lu_solve(lu, rhs - K @ sol)
+            if not np.isfinite(sol).all():
+                sol = None
+        except (np.linalg.LinAlgError, ValueError):
+            sol = None
+        if sol is not None:
+            xp = sol[:n]
+            lam_p = np.zeros(mi)
+            lam_p[act] = sol[n + me:]
+            yp = osqp_y(sol[n:n + me], lam_p)
+            feas = (C @ xp <= d + 1e-10 * max(1.0, np.abs(d).max(initial=0))).all() and (lam_p >= -1e-9).all()
+            cp = kkt_certificate(P, q, A, l, u, xp, yp)
+            if feas and cp["stat_rel"] <= max(cert["stat_rel"], 1e-12) and cp["prim"] <= max(cert["prim"], 1e-12) \
+                    and cp["comp"] <= cert["comp"]:
+                x, y, cert = xp, yp, cp
     sv = 1 if status == "solved" else -2
     return QPResult(x, y, status, sv, it, cert)
 

@@ -26,7 +26,7 @@ def golden_matrix(d, nm, j):
     return sp.coo_matrix((d[f"{nm}_{j}_data"], (d[f"{nm}_{j}_row"], d[f"{nm}_{j}_col"])), shape=shp).toarray()
 
 
-LPV_CASES = ["lpv_n10_a2", "lpv_n30_a3", "lpv_n10_lowspeed", "lpv_n10_a1", "lpv_n20_a4"]
+LPV_CASES = ["lpv_n10_a2", "lpv_n30_a3", "lpv_n10_lowspeed", "lpv_n10_a1", "lpv_n20_a4", "lpv_n125_a3"]
 
 
 def lpv_qps(name):
@@ -46,3 +46,21 @@ def gpu_ctx():
     import cmpc
 
     return cmpc.default_context(0)
+
+
+def assert_matches_optimum(z, c, ztol=1e-6):
+    """z solves the captured reference QP c: within ztol of the certified optimum z*, or — where
+    the optimum sits on a weakly active bound (multiplier ~ 0, the degenerate case in which
+    interior-point iterates approach the bound only like sqrt(mu)) — primal feasible to 1e-9,
+    optimal in value to 1e-12 relative and within 1e-5 of z*."""
+    err = float(np.abs(z - c["z"]).max())
+    if err < ztol:
+        return err
+    P, q, A, l, u = c["P"], c["q"], c["A"], c["l"], c["u"]
+    Az = A @ z
+    viol = max(float(np.maximum(Az - u, 0).max()), float(np.maximum(l - Az, 0).max()))
+    f, fs = 0.5 * z @ P @ z + q @ z, 0.5 * c["z"] @ P @ c["z"] + q @ c["z"]
+    weak = np.isinf(l) & (np.abs(Az - u) < 1e-5) & (np.abs(c["y"]) < 1e-4)
+    assert weak.any() and viol < 1e-9 and f - fs < 1e-12 * abs(fs) and err < 1e-5, (err, viol, f - fs)
+    return err
+

@@ -6,7 +6,7 @@ reference optimum / the C restatement; builder outputs to fp64 rounding.
 import numpy as np
 import pytest
 
-from conftest import LPV_CASES, golden, lpv_qps
+from conftest import LPV_CASES, assert_matches_optimum, golden, lpv_qps
 
 pytestmark = pytest.mark.gpu
 
@@ -47,9 +47,12 @@ def test_lpv_batch_matches_reference_optimum(gpu_ctx, name):
         res = bp.solve(np.stack([c["x0"] for c in cs]), np.stack([c["x_last"] for c in cs]),
                        np.stack([c["u_last"] for c in cs]), np.stack([c["u_old"] for c in cs]),
                        xa if xa.shape[2] else None, np.stack([c["pose"] for c in cs]))
-        assert (res["status"] == cmpc.CMPC_SOLVED).all(), res["status"]
-        zref = np.stack([c["z"] for c in cs])
-        assert np.abs(res["z"] - zref).max() < Z_TOL
+        # solved; or, at the rounding floor of the N = 125 case, "solved inaccurate" (OSQP's
+        # status 2, which the reference counts as feasible, LPV_Planner.py:243-249)
+        assert np.isin(res["status"], (cmpc.CMPC_SOLVED, cmpc.CMPC_SOLVED_INACCURATE)).all(), res["status"]
+        assert (res["status"] == cmpc.CMPC_SOLVED).mean() >= 0.8, res["status"]
+        for a, c in enumerate(cs):
+            assert_matches_optimum(res["z"][a], c, Z_TOL)
         if xa.shape[2]:
             np.testing.assert_allclose(res["planes"], np.stack([c["planes"] for c in cs]), rtol=0, atol=1e-14)
 
@@ -250,33 +253,55 @@ def test_edge_cases(gpu_ctx):
 
 def test_unsupported_sizes_are_rejected(gpu_ctx):
     import cmpc
-    from cmpc import scenarios as S
-    from oracle import synth
 
-    sc = S.make_di(2, 130, 1, 2)   # N*nu = 260 > 256
-    P = synth.structured(sc.shared, sc.params, sc.A, sc.B, sc.x0, sc.u_prev, sc.lane, sc.nbr, sc.traj, np.arange(2))
+    # nx = 12, nu = 4, 16 rows per stage at N = 200: the per-agent rows exceed 160 KB of LDS
+    nx, nu, N, mc, B = 12, 4, 200, 16, 1
+    p = dict(nx=nx, nu=nu, N=N, ns=1, mc=mc, Q=np.eye(nx), R=np.eye(nu), dR=np.eye(nu), Qs=np.ones(1),
+             u_ub=np.ones(nu), u_lb=-np.ones(nu), row_slack=-np.ones(mc, np.int32), row_sign=np.ones(mc, np.int32),
+             A=np.tile(np.eye(nx), (B, N, 1, 1)), B=np.zeros((B, N, nx, nu)), x0=np.zeros((B, nx)),
+             u_prev=np.zeros((B, nu)), qlin=np.zeros((B, N + 1, nx)), C=np.zeros((B, N, mc, nx)),
+             h=np.ones((B, N, mc)))
     with pytest.raises(cmpc.CmpcError):
-        cmpc.solve_mpc(P, gpu_ctx)
-    sc = S.make_di(4, 50, 2, 3)    # cfg5 in fp64: the workgroup solver's LDS would exceed 160 KB
-    P = synth.structured(sc.shared, sc.params, sc.A, sc.B, sc.x0, sc.u_prev, sc.lane, sc.nbr, sc.traj, np.arange(4))
-    with pytest.raises(cmpc.CmpcError):
-        cmpc.solve_mpc(P, gpu_ctx)
+        cmpc.solve_mpc(p, gpu_ctx)
 
 
-def test_long_horizon_fp64_workgroup_solver(gpu_ctx):
-    """N*nu = 80 > 64: the workgroup-per-agent solver in fp64, vs the C restatement."""
+@pytest.mark.parametrize("n,N,nb,dim", [(48, 40, 2, 2), (8, 130, 1, 2), (64, 50, 2, 3)])
+def test_long_horizon_riccati_solver(gpu_ctx, n, N, nb, dim):
+    """N*nu > 64: the stage-wise Riccati solver (fp64) vs the C restatement — including
+    N*nu = 260 (beyond any condensed kernel) and BASELINE cfg5's shape in fp64."""
     import cmpc
     from cmpc import scenarios as S
     from oracle import cmpc_oracle as CO
     from oracle import synth
 
-    sc = S.make_di(48, 40, 2, 2)
+    sc = S.make_di(n, N, nb, dim)
     P = synth.structured(sc.shared, sc.params, sc.A, sc.B, sc.x0, sc.u_prev, sc.lane, sc.nbr, sc.traj,
-                         np.arange(48))
+                         np.arange(n))
     z, kkt, it, st = cmpc.solve_mpc(P, gpu_ctx)
-    zc, _, _, stc = CO.solve_batch(P)
-    assert (st == cmpc.CMPC_SOLVED).all() and (stc == 1).all()
+    zc, _, itc, stc = CO.solve_batch(P)
+    assert np.isin(st, (cmpc.CMPC_SOLVED, cmpc.CMPC_SOLVED_INACCURATE)).all() and np.isin(stc, (1, 2)).all()
     assert np.abs(z - zc).max() < Z_TOL
+    assert kkt.max() < 1e-6
+
+
+@pytest.mark.parametrize("n,N,nb,dim", [(64, 20, 2, 2), (256, 30, 2, 2), (16, 10, 1, 3), (8, 10, 0, 2)])
+def test_riccati_forced_matches_condensed(gpu_ctx, n, N, nb, dim):
+    """CMPC_FLAG_RICCATI on short horizons: the Riccati factorisation solves the same Newton
+    systems as the condensed Cholesky, so the two GPU paths and the C restatement agree."""
+    import cmpc
+    from cmpc import scenarios as S
+    from oracle import cmpc_oracle as CO
+    from oracle import synth
+
+    sc = S.make_di(n, N, nb, dim)
+    P = synth.structured(sc.shared, sc.params, sc.A, sc.B, sc.x0, sc.u_prev, sc.lane, sc.nbr, sc.traj,
+                         np.arange(n))
+    zr, kr, ir, sr = cmpc.solve_mpc(P, gpu_ctx, riccati=True)
+    zd, kd, idd, sd = cmpc.solve_mpc(P, gpu_ctx)
+    zc, _, _, _ = CO.solve_batch(P)
+    assert np.isin(sr, (cmpc.CMPC_SOLVED, cmpc.CMPC_SOLVED_INACCURATE)).all()
+    assert np.abs(zr - zc).max() < Z_TOL and np.abs(zr - zd).max() < Z_TOL
+    print(f"riccati iters mean {ir.mean():.2f} vs condensed {idd.mean():.2f}")
 
 
 # fp32 bar (BASELINE cfg5 "fp32 path with tolerance check vs fp64 reference"): every z entry

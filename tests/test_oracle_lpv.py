@@ -31,7 +31,7 @@ def test_golden_solutions_are_kkt_certified(name):
     d = golden(name)
     assert d["stat"].max() < 1e-11
     assert d["prim"].max() < 1e-12
-    assert d["comp"].max() < 1e-9
+    assert d["comp"].max() < 5e-9
 
 
 def test_ipm_resolves_golden():

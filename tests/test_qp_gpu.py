@@ -6,7 +6,7 @@ a QP captured from the reference's own PlannerLPV (tests/golden)."""
 import numpy as np
 import pytest
 
-from conftest import LPV_CASES, lpv_qps
+from conftest import LPV_CASES, assert_matches_optimum, lpv_qps
 
 pytestmark = pytest.mark.gpu
 
@@ -92,9 +92,9 @@ def test_osqp_adapter_on_reference_captured_qp(gpu_ctx, name):
     for j, c in lpv_qps(name):
         res, feasible = cmpc.osqp_solve_qp(*_osqp_args(c), ctx=gpu_ctx)
         assert res.info.solver == "structured"
-        assert feasible == 1 and res.info.status_val == 1, (j, res.info.status)
+        assert feasible == 1 and res.info.status_val in (1, 2), (j, res.info.status)
         assert res.info.kkt <= 1e-6 and res.info.pri_res <= 1e-6, (res.info.kkt, res.info.pri_res)
-        assert np.abs(res.x - c["z"]).max() < 1e-6, (j, np.abs(res.x - c["z"]).max())
+        assert_matches_optimum(res.x, c, 1e-6)
         fz = 0.5 * c["z"] @ c["P"] @ c["z"] + c["q"] @ c["z"]
         assert abs(res.info.obj_val - fz) <= 1e-9 * max(1.0, abs(fz))
 
