@@ -17,11 +17,20 @@
 // One 64-lane wavefront (= one workgroup) per agent.  Everything the row loops touch lives in
 // LDS; the per-stage operands of the recursions (A_k, B_k and the Riccati gains) stream from
 // global memory through a double-buffered LDS stage image, fetched one stage ahead into
-// registers so the load latency overlaps the current stage.  The Riccati gains, the predictor
-// direction and the best-iterate copy live in a per-agent global scratch (MpcPtrs::ws).
-// fp64 throughout.
+// registers so the load latency overlaps the current stage.  The Riccati gains, the stage
+// weights W_k, the predictor direction and the best-iterate copy live in a per-agent global
+// scratch (MpcPtrs::ws).
+//
+// Precision.  fp64, except near the solution of hard agents: once max th = lam/t exceeds
+// kDdTh (rows pinned at t ~ 1e-13 with multipliers ~ 1e5, th -> 1e18..1e21 on the reference's
+// N = 125 case) the double recursion loses the small directions of the cost-to-go to
+// cancellation, and its Newton direction is off by O(1) where the condensed Cholesky is
+// still usable.  Those iterations factor in double-double (dd.h) and refine the direction
+// against the Newton residual evaluated in double-double (up to kRefineMax steps), which
+// restores the exact direction (tools/ipm_lab.py, oracle/cmpc_oracle.c newton = 3).
 #include <cmath>
 
+#include "dd.h"
 #include "internal.h"
 #include "wave_ops.h"
 
@@ -33,13 +42,16 @@ constexpr int kMaxNa = CMPC_MAX_NX + CMPC_MAX_NU;
 constexpr int kStageMax = CMPC_MAX_NX * CMPC_MAX_NX + CMPC_MAX_NX * CMPC_MAX_NU + CMPC_MAX_NU * kMaxNa +
                           CMPC_MAX_NU * CMPC_MAX_NU;
 constexpr int kPer = (kStageMax + kWave - 1) / kWave;  // stage-image values per lane
+constexpr double kDdTh = 1e10;   // max th above which an iteration runs in double-double
+constexpr int kRefineMax = 6;    // refinement steps of a double-double iteration's direction
 
 struct RLds {
     int t, lam, th, rp, rho, rt, w, GdU;  // per row
-    int X, dX, yb, psi;                   // per stage state
-    int U, dU, rd, gU, rh;                // per condensed input
+    int X, dX, yb, yb2, psi;              // per stage state (yb | yb2: the dd states of kres_dd)
+    int U, dU, rd, gU, rh, cr;            // per condensed input
     int sig, dsig, Dsig, rsig;            // per stage slack
-    int P, pv, sb, T, G, Hy, Kk, W, gv;   // Riccati working set
+    int P, pv, sb, T, G, Hy, Kk, gv, xpp; // Riccati working set
+    int Pd, PAd, PBd, Hd, Hyd, Kd, psid;  // double-double working set
     int total;
 };
 
@@ -82,12 +94,14 @@ __host__ __device__ inline RLds r_layout(const MpcConst& c) {
     L.X = take((N + 1) * nx);
     L.dX = take((N + 1) * nx);
     L.yb = take((N + 1) * nx);
+    L.yb2 = take((N + 1) * nx);  // must follow yb: [yb, yb2) holds (N+1)*nx dd values
     L.psi = take(2 * nx);
     L.U = take(n);
     L.dU = take(n);
     L.rd = take(n);
     L.gU = take(n);
     L.rh = take(n);
+    L.cr = take(n);
     L.sig = take(N * ns);
     L.dsig = take(N * ns);
     L.Dsig = take(N * ns);
@@ -99,15 +113,23 @@ __host__ __device__ inline RLds r_layout(const MpcConst& c) {
     L.G = take(d.nc * d.nc);
     L.Hy = take(c.nu * d.na);
     L.Kk = take(c.nu * d.na);
-    L.W = take(nx * nx);
     L.gv = take(c.nu + nx);
+    L.xpp = take(2 * nx);
+    L.Pd = take(2 * d.na * d.na);
+    L.PAd = take(2 * d.na * nx);
+    L.PBd = take(2 * d.na * c.nu);
+    L.Hd = take(2 * c.nu * c.nu);
+    L.Hyd = take(2 * c.nu * d.na);
+    L.Kd = take(2 * c.nu * d.na);
+    L.psid = take(4 * nx);
     L.total = o;
     return L;
 }
 
-// per-agent global scratch (doubles): predictor direction (dt, dl), Riccati factors, best iterate
+// per-agent global scratch (doubles): predictor direction (dt, dl), Riccati factors, stage
+// weights W_k = 2Q + M_k of the state X_{k+1}, best iterate
 struct RGlb {
-    size_t dta, dla, F, bU, bsig, total;
+    size_t dta, dla, F, Wk, bU, bsig, total;
 };
 
 __host__ __device__ inline RGlb r_glb(const MpcConst& c) {
@@ -122,6 +144,7 @@ __host__ __device__ inline RGlb r_glb(const MpcConst& c) {
     g.dta = take(c.m);
     g.dla = take(c.m);
     g.F = take((size_t)c.N * d.sF);
+    g.Wk = take((size_t)c.N * c.nx * c.nx);
     g.bU = take(c.n);
     g.bsig = take((size_t)c.N * c.ns);
     g.total = o;
@@ -283,32 +306,39 @@ __device__ void adjoint(const MpcConst& c, const Dims& d, const StageSrc& src, d
     }
 }
 
-// Riccati factorisation of the Newton system at the current (th, Dsig): writes the gains
-// K_k = -Hvv^-1 Hvy and Hinv_k = Hvv^-1 of every stage into F.  Returns false on a
-// non-positive pivot (wave-uniform).
+// W_k = 2Q + M_k of the state X_{k+1} for every block k (global scratch, one pass of all lanes)
+__device__ void stage_weights(const MpcConst& c, const RLds& L, const double* sm, const double* __restrict__ C,
+                              double* __restrict__ Wg) {
+    const int nx = c.nx, nx2 = nx * nx, mc = c.mc, ns = c.ns;
+    const double* th = sm + L.th;
+    const double* Dsig = sm + L.Dsig;
+    for (int e = threadIdx.x; e < c.N * nx2; e += kWave) {
+        const int k = e / nx2, q = e - k * nx2, i = q / nx, j = q - i * nx;
+        Wg[e] = 2.0 * c.Q[q] + m_entry(c, C + (size_t)k * mc * nx, th + k * mc, Dsig + k * ns, i, j);
+    }
+}
+
+// Riccati factorisation of the Newton system at the current (th, Dsig), with the stage weights
+// Wg of stage_weights: writes the gains K_k = -Hvv^-1 Hvy and Hinv_k = Hvv^-1 of every stage
+// into F.  Returns false on a non-positive pivot (wave-uniform).
 __device__ bool riccati_factor(const MpcConst& c, const Dims& d, const RLds& L, double* sm,
                                const double* __restrict__ A, const double* __restrict__ B,
-                               const double* __restrict__ C, double* __restrict__ F) {
-    const int l = threadIdx.x, nx = d.nx, nu = d.nu, na = d.na, nc = d.nc, N = c.N, mc = c.mc, ns = c.ns;
+                               const double* __restrict__ Wg, double* __restrict__ F) {
+    const int l = threadIdx.x, nx = d.nx, nu = d.nu, na = d.na, nc = d.nc, N = c.N;
     double* P = sm + L.P;
     double* T = sm + L.T;
     double* G = sm + L.G;
     double* Hy = sm + L.Hy;
     double* Kk = sm + L.Kk;
-    double* W = sm + L.W;
     double* sb = sm + L.sb;
     const double* th = sm + L.th;
-    const double* Dsig = sm + L.Dsig;
     const StageSrc src{A, B, nullptr, d.sA, d.sB, d.sF};
     double r[kPer];
     stage_fetch(src, N - 1, d.sAB, r);
     // P_N = blkdiag(W_N, 0),  W_N = 2Q + M_N (stage rows of X_N)
     for (int e = l; e < na * na; e += kWave) {
         const int i = e / na, j = e - i * na;
-        P[e] = (i < nx && j < nx) ? 2.0 * c.Q[i * nx + j] +
-                                        m_entry(c, C + (size_t)(N - 1) * mc * nx, th + (N - 1) * mc,
-                                                Dsig + (N - 1) * ns, i, j)
-                                  : 0.0;
+        P[e] = (i < nx && j < nx) ? Wg[(size_t)(N - 1) * nx * nx + i * nx + j] : 0.0;
     }
     stage_put(sb + ((N - 1) & 1) * d.S, d.sAB, r);
     if (N > 1) stage_fetch(src, N - 2, d.sAB, r);
@@ -327,12 +357,6 @@ __device__ bool riccati_factor(const MpcConst& c, const Dims& d, const RLds& L, 
                 for (int s = 0; s < nx; ++s) v = fma(P[i * na + s], Bk[s * nu + (j - nx)], v);
             T[e] = v;
         }
-        if (k >= 1)
-            for (int e = l; e < nx * nx; e += kWave) {
-                const int i = e / nx, j = e - i * nx;
-                W[e] = 2.0 * c.Q[e] + m_entry(c, C + (size_t)(k - 1) * mc * nx, th + (k - 1) * mc,
-                                              Dsig + (k - 1) * ns, i, j);
-            }
         bar();
         // G = [A_k | B_k]' T[:nx, :]   (nc x nc, lower triangle)
         for (int e = l; e < nc * nc; e += kWave) {
@@ -453,7 +477,7 @@ __device__ bool riccati_factor(const MpcConst& c, const Dims& d, const RLds& L, 
         for (int e = l; e < na * na; e += kWave) {
             const int i = e / na, j = e - i * na;
             if (j > i) continue;
-            double v = (i < nx) ? W[i * nx + j] + G[i * nc + j]
+            double v = (i < nx) ? Wg[(size_t)(k - 1) * nx * nx + i * nx + j] + G[i * nc + j]
                                 : ((j >= nx) ? 2.0 * c.dR[(i - nx) * nu + (j - nx)] : 0.0);
             for (int a = 0; a < nu; ++a) v = fma(Hy[a * na + i], Kk[a * na + j], v);
             P[i * na + j] = v;
@@ -464,18 +488,192 @@ __device__ bool riccati_factor(const MpcConst& c, const Dims& d, const RLds& L, 
     return ok;
 }
 
-// Solve the Newton system for the right-hand side rh (n values): dU (n) and dX ((N+1) nx,
-// dX_0 = 0), with the gains of riccati_factor.
+// riccati_factor in double-double (standard form: P_k = blkdiag(W_k + A'Pxx A, 2dR) + Hvy'K_k),
+// for the iterations whose th span defeats fp64 (kDdTh).  The gains are rounded to double
+// into F; the refinement against the double-double residual (kres_dd) absorbs that rounding.
+__device__ __noinline__ bool riccati_factor_dd(const MpcConst& c, const Dims& d, const RLds& L, double* sm,
+                                  const double* __restrict__ A, const double* __restrict__ B,
+                                  const double* __restrict__ Wg, double* __restrict__ F) {
+    const int l = threadIdx.x, nx = d.nx, nu = d.nu, na = d.na, N = c.N;
+    double* P = sm + L.Pd;
+    double* PA = sm + L.PAd;
+    double* PB = sm + L.PBd;
+    double* H = sm + L.Hd;
+    double* Hy = sm + L.Hyd;
+    double* Kk = sm + L.Kd;
+    double* sb = sm + L.sb;
+    const double* th = sm + L.th;
+    const StageSrc src{A, B, nullptr, d.sA, d.sB, d.sF};
+    double r[kPer];
+    stage_fetch(src, N - 1, d.sAB, r);
+    for (int e = l; e < na * na; e += kWave) {
+        const int i = e / na, j = e - i * na;
+        st_dd(P, e, dd_of((i < nx && j < nx) ? Wg[(size_t)(N - 1) * nx * nx + i * nx + j] : 0.0));
+    }
+    stage_put(sb + ((N - 1) & 1) * d.S, d.sAB, r);
+    if (N > 1) stage_fetch(src, N - 2, d.sAB, r);
+    bar();
+    bool ok = true;
+    for (int k = N - 1; k >= 0; --k) {
+        const double* Ak = sb + (k & 1) * d.S;
+        const double* Bk = Ak + d.sA;
+        // PA = P[:, :nx] A_k (na x nx);  PB = P [B_k; I] (na x nu)
+        for (int e = l; e < na * (nx + nu); e += kWave) {
+            if (e < na * nx) {
+                const int i = e / nx, j = e - i * nx;
+                dd v = dd_of(0.0);
+                for (int s2 = 0; s2 < nx; ++s2) v = dd_fmad(v, ld_dd(P, i * na + s2), Ak[s2 * nx + j]);
+                st_dd(PA, e, v);
+            } else {
+                const int e2 = e - na * nx, i = e2 / nu, cc = e2 - i * nu;
+                dd v = ld_dd(P, i * na + nx + cc);
+                for (int s2 = 0; s2 < nx; ++s2) v = dd_fmad(v, ld_dd(P, i * na + s2), Bk[s2 * nu + cc]);
+                st_dd(PB, e2, v);
+            }
+        }
+        bar();
+        // Hvy = [B'PA + PA_u | -2dR] (nu x na);  Hvv = 2R + 2dR + diag(th_u) + B'PB + PB_u (nu x nu)
+        for (int e = l; e < nu * na + nu * nu; e += kWave) {
+            if (e < nu * na) {
+                const int cc = e / na, j = e - cc * na;
+                dd v;
+                if (j < nx) {
+                    v = ld_dd(PA, (nx + cc) * nx + j);
+                    for (int s2 = 0; s2 < nx; ++s2) v = dd_fmad(v, ld_dd(PA, s2 * nx + j), Bk[s2 * nu + cc]);
+                } else {
+                    v = dd_of(-2.0 * c.dR[cc * nu + (j - nx)]);
+                }
+                st_dd(Hy, e, v);
+            } else {
+                const int e2 = e - nu * na, cc = e2 / nu, ee = e2 - cc * nu;
+                dd v = dd_add(dd_ts(2.0 * c.R[cc * nu + ee], 2.0 * c.dR[cc * nu + ee]), ld_dd(PB, (nx + cc) * nu + ee));
+                for (int s2 = 0; s2 < nx; ++s2) v = dd_fmad(v, ld_dd(PB, s2 * nu + ee), Bk[s2 * nu + cc]);
+                if (cc == ee) {
+                    const int rr = c.ms + 2 * (k * nu + cc);
+                    v = dd_add(v, dd_ts(th[rr], th[rr + 1]));
+                }
+                st_dd(H, e2, v);
+            }
+        }
+        bar();
+        // Cholesky of Hvv and its inverse, in registers (every lane; nu <= 4)
+        dd Lf[CMPC_MAX_NU][CMPC_MAX_NU], Hi[CMPC_MAX_NU][CMPC_MAX_NU];
+#pragma unroll
+        for (int a = 0; a < CMPC_MAX_NU; ++a)
+#pragma unroll
+            for (int b = 0; b < CMPC_MAX_NU; ++b) Lf[a][b] = (a < nu && b <= a) ? ld_dd(H, a * nu + b) : dd_of(0.0);
+#pragma unroll
+        for (int j = 0; j < CMPC_MAX_NU; ++j) {
+            if (j < nu) {
+                dd dj = Lf[j][j];
+#pragma unroll
+                for (int p = 0; p < j; ++p) dj = dd_sub(dj, dd_mul(Lf[j][p], Lf[j][p]));
+                ok = ok && (dj.hi > 0.0);
+                if (!(dj.hi > 0.0)) dj = dd_of(1.0);
+                dj = dd_sqrt(dj);
+                Lf[j][j] = dj;
+#pragma unroll
+                for (int i = j + 1; i < CMPC_MAX_NU; ++i) {
+                    if (i < nu) {
+                        dd v = Lf[i][j];
+#pragma unroll
+                        for (int p = 0; p < j; ++p) v = dd_sub(v, dd_mul(Lf[i][p], Lf[j][p]));
+                        Lf[i][j] = dd_div(v, dj);
+                    }
+                }
+            }
+        }
+#pragma unroll
+        for (int col = 0; col < CMPC_MAX_NU; ++col) {
+            dd e[CMPC_MAX_NU];
+#pragma unroll
+            for (int i = 0; i < CMPC_MAX_NU; ++i) e[i] = dd_of(i == col ? 1.0 : 0.0);
+#pragma unroll
+            for (int i = 0; i < CMPC_MAX_NU; ++i) {
+                if (i < nu) {
+                    dd v = e[i];
+#pragma unroll
+                    for (int p = 0; p < i; ++p) v = dd_sub(v, dd_mul(Lf[i][p], e[p]));
+                    e[i] = dd_div(v, Lf[i][i]);
+                }
+            }
+#pragma unroll
+            for (int i = CMPC_MAX_NU - 1; i >= 0; --i) {
+                if (i < nu) {
+                    dd v = e[i];
+#pragma unroll
+                    for (int p = i + 1; p < CMPC_MAX_NU; ++p)
+                        if (p < nu) v = dd_sub(v, dd_mul(Lf[p][i], e[p]));
+                    e[i] = dd_div(v, Lf[i][i]);
+                }
+            }
+#pragma unroll
+            for (int i = 0; i < CMPC_MAX_NU; ++i) Hi[i][col] = e[i];
+        }
+        // K_k = -Hinv Hvy (nu x na) into LDS (dd) and F (double);  Hinv into F
+        double* Fk = F + (size_t)k * d.sF;
+        for (int e = l; e < nu * na; e += kWave) {
+            const int a = e / na, j = e - a * na;
+            dd v = dd_of(0.0);
+#pragma unroll
+            for (int b = 0; b < CMPC_MAX_NU; ++b) {
+                if (b < nu) {
+                    dd hab = dd_of(0.0);
+#pragma unroll
+                    for (int a2 = 0; a2 < CMPC_MAX_NU; ++a2)
+                        if (a2 == a) hab = Hi[a2][b];
+                    v = dd_sub(v, dd_mul(hab, ld_dd(Hy, b * na + j)));
+                }
+            }
+            st_dd(Kk, e, v);
+            Fk[e] = v.hi;
+        }
+        if (l < nu * nu) {
+            const int a = l / nu, b = l - a * nu;
+            double v = 0.0;
+#pragma unroll
+            for (int a2 = 0; a2 < CMPC_MAX_NU; ++a2)
+#pragma unroll
+                for (int b2 = 0; b2 < CMPC_MAX_NU; ++b2)
+                    if (a2 == a && b2 == b) v = Hi[a2][b2].hi;
+            Fk[nu * na + l] = v;
+        }
+        if (k > 0) {
+            stage_put(sb + ((k - 1) & 1) * d.S, d.sAB, r);
+            if (k > 1) stage_fetch(src, k - 2, d.sAB, r);
+        }
+        bar();
+        if (k == 0) break;
+        // P_k = blkdiag(W_k + A'Pxx A, 2dR) + Hvy'K_k  (A_k still in the other half of sb)
+        for (int e = l; e < na * na; e += kWave) {
+            const int i = e / na, j = e - i * na;
+            if (j > i) continue;
+            dd v;
+            if (i < nx) {
+                v = dd_of(Wg[(size_t)(k - 1) * nx * nx + i * nx + j]);
+                for (int s2 = 0; s2 < nx; ++s2) v = dd_fmad(v, ld_dd(PA, s2 * nx + j), Ak[s2 * nx + i]);
+            } else {
+                v = dd_of((j >= nx) ? 2.0 * c.dR[(i - nx) * nu + (j - nx)] : 0.0);
+            }
+            for (int a = 0; a < nu; ++a) v = dd_fma(v, ld_dd(Hy, a * na + i), ld_dd(Kk, a * na + j));
+            st_dd(P, i * na + j, v);
+            st_dd(P, j * na + i, v);
+        }
+        bar();
+    }
+    return ok;
+}
+
+// Solve the Newton system for the right-hand side rh (n values): dU (n) and, when dX is not
+// null, dX ((N+1) nx, dX_0 = 0), with the gains of riccati_factor.
 __device__ void riccati_solve(const MpcConst& c, const Dims& d, const RLds& L, double* sm,
                               const double* __restrict__ A, const double* __restrict__ B,
-                              const double* __restrict__ F) {
+                              const double* __restrict__ F, const double* rh, double* dU, double* dX) {
     const int l = threadIdx.x, nx = d.nx, nu = d.nu, na = d.na, N = c.N;
     double* sb = sm + L.sb;
     double* pv = sm + L.pv;
     double* gv = sm + L.gv;
-    double* dU = sm + L.dU;
-    double* dX = sm + L.dX;
-    const double* rh = sm + L.rh;
+    double* xb = sm + L.xpp;  // dX_k, ping-pong
     const StageSrc src{A, B, F, d.sA, d.sB, d.sF};
     double r[kPer];
     // backward: p_N = 0;  gv = -rh_k + B'p_x + p_u;  kk_k = -Hinv gv (into dU);  p_k = [A'p_x; 0] + K' gv
@@ -520,7 +718,10 @@ __device__ void riccati_solve(const MpcConst& c, const Dims& d, const RLds& L, d
     }
     // forward: y_0 = 0;  v_k = kk_k + K_k y_k;  dX_{k+1} = A_k dX_k + B_k v_k
     stage_fetch(src, 0, d.S, r);
-    if (l < nx) dX[l] = 0.0;
+    if (l < nx) {
+        xb[l] = 0.0;
+        if (dX) dX[l] = 0.0;
+    }
     stage_put(sb, d.S, r);
     if (N > 1) stage_fetch(src, 1, d.S, r);
     bar();
@@ -528,9 +729,10 @@ __device__ void riccati_solve(const MpcConst& c, const Dims& d, const RLds& L, d
         const double* Ak = sb + (k & 1) * d.S;
         const double* Bk = Ak + d.sA;
         const double* Kg = Bk + d.sB;
+        const double* xc = xb + (k & 1) * nx;
         if (l < nu) {
             double v = dU[k * nu + l];
-            for (int j = 0; j < nx; ++j) v = fma(Kg[l * na + j], dX[k * nx + j], v);
+            for (int j = 0; j < nx; ++j) v = fma(Kg[l * na + j], xc[j], v);
             if (k > 0)
                 for (int b = 0; b < nu; ++b) v = fma(Kg[l * na + nx + b], dU[(k - 1) * nu + b], v);
             dU[k * nu + l] = v;
@@ -538,15 +740,95 @@ __device__ void riccati_solve(const MpcConst& c, const Dims& d, const RLds& L, d
         bar();
         if (l < nx) {
             double v = 0.0;
-            for (int t = 0; t < nx; ++t) v = fma(Ak[l * nx + t], dX[k * nx + t], v);
+            for (int t = 0; t < nx; ++t) v = fma(Ak[l * nx + t], xc[t], v);
             for (int a = 0; a < nu; ++a) v = fma(Bk[l * nu + a], dU[k * nu + a], v);
-            dX[(k + 1) * nx + l] = v;
+            xb[((k + 1) & 1) * nx + l] = v;
+            if (dX) dX[(k + 1) * nx + l] = v;
         }
         if (k + 1 < N) {
             stage_put(sb + ((k + 1) & 1) * d.S, d.S, r);
             if (k + 2 < N) stage_fetch(src, k + 2, d.S, r);
         }
         bar();
+    }
+}
+
+// out = rhs - K v with the product evaluated in double-double (the refinement residual of a
+// double-double iteration):  K v = sum_k Gamma_k' W_k Gamma_k v + (2R + 2D'dR D + diag(th_u)) v,
+// through the stage recursions (dd states in [yb, yb2), dd adjoint in psid).
+__device__ __noinline__ void kres_dd(const MpcConst& c, const Dims& d, const RLds& L, double* sm, const double* __restrict__ A,
+                        const double* __restrict__ B, const double* __restrict__ Wg, const double* v,
+                        const double* rhs, double* out) {
+    const int l = threadIdx.x, nx = d.nx, nu = d.nu, N = c.N, nx2 = nx * nx;
+    double* Xd = sm + L.yb;
+    double* sb = sm + L.sb;
+    const double* th = sm + L.th;
+    double* pa = sm + L.psid;
+    double* pb = pa + 2 * nx;
+    const StageSrc src{A, B, nullptr, d.sA, d.sB, d.sF};
+    double r[kPer];
+    // forward: X_0 = 0, X_{k+1} = A_k X_k + B_k v_k
+    stage_fetch(src, 0, d.sAB, r);
+    if (l < nx) st_dd(Xd, l, dd_of(0.0));
+    stage_put(sb, d.sAB, r);
+    if (N > 1) stage_fetch(src, 1, d.sAB, r);
+    bar();
+    for (int k = 0; k < N; ++k) {
+        const double* Ak = sb + (k & 1) * d.S;
+        const double* Bk = Ak + d.sA;
+        if (l < nx) {
+            dd acc = dd_of(0.0);
+            for (int t = 0; t < nx; ++t) acc = dd_fmad(acc, ld_dd(Xd, k * nx + t), Ak[l * nx + t]);
+            for (int i = 0; i < nu; ++i) acc = dd_fmadd(acc, Bk[l * nu + i], v[k * nu + i]);
+            st_dd(Xd, (k + 1) * nx + l, acc);
+        }
+        if (k + 1 < N) {
+            stage_put(sb + ((k + 1) & 1) * d.S, d.sAB, r);
+            if (k + 2 < N) stage_fetch(src, k + 2, d.sAB, r);
+        }
+        bar();
+    }
+    // adjoint: psi_N = W X_N, psi_k = W X_k + A_k' psi_{k+1};  out_k = rhs_k - B_k' psi_{k+1} - (...)
+    stage_fetch(src, N - 1, d.sAB, r);
+    if (l < nx) {
+        dd acc = dd_of(0.0);
+        for (int u = 0; u < nx; ++u) acc = dd_fmad(acc, ld_dd(Xd, N * nx + u), Wg[(size_t)(N - 1) * nx2 + l * nx + u]);
+        st_dd(pa, l, acc);
+    }
+    stage_put(sb + ((N - 1) & 1) * d.S, d.sAB, r);
+    if (N > 1) stage_fetch(src, N - 2, d.sAB, r);
+    bar();
+    for (int k = N - 1; k >= 0; --k) {
+        const double* Ak = sb + (k & 1) * d.S;
+        const double* Bk = Ak + d.sA;
+        if (l < nu) {
+            dd acc = dd_of(0.0);
+            for (int s2 = 0; s2 < nx; ++s2) acc = dd_fmad(acc, ld_dd(pa, s2), Bk[s2 * nu + l]);
+            for (int j = 0; j < nu; ++j) {
+                const double vk = v[k * nu + j];
+                const dd dk = dd_ts(vk, k ? -v[(k - 1) * nu + j] : 0.0);
+                const dd dn = (k + 1 < N) ? dd_ts(v[(k + 1) * nu + j], -vk) : dd_of(0.0);
+                acc = dd_fmadd(acc, 2.0 * c.R[l * nu + j], vk);
+                acc = dd_fmad(acc, dd_sub(dk, dn), 2.0 * c.dR[l * nu + j]);
+            }
+            const int rr = c.ms + 2 * (k * nu + l);
+            acc = dd_fmad(acc, dd_ts(th[rr], th[rr + 1]), v[k * nu + l]);
+            out[k * nu + l] = dd_sub(dd_of(rhs[k * nu + l]), acc).hi;
+        } else if (k > 0 && l >= 32 && l < 32 + nx) {
+            const int t = l - 32;
+            dd acc = dd_of(0.0);
+            for (int u = 0; u < nx; ++u) acc = dd_fmad(acc, ld_dd(Xd, k * nx + u), Wg[(size_t)(k - 1) * nx2 + t * nx + u]);
+            for (int s2 = 0; s2 < nx; ++s2) acc = dd_fmad(acc, ld_dd(pa, s2), Ak[s2 * nx + t]);
+            st_dd(pb, t, acc);
+        }
+        if (k > 0) {
+            stage_put(sb + ((k - 1) & 1) * d.S, d.sAB, r);
+            if (k > 1) stage_fetch(src, k - 2, d.sAB, r);
+        }
+        bar();
+        double* tq = pa;
+        pa = pb;
+        pb = tq;
     }
 }
 
@@ -572,6 +854,7 @@ __global__ __launch_bounds__(kWave) void mpc_riccati_kernel(const MpcConst c, co
     double* F = ws + gl.F;
     double* bU = ws + gl.bU;
     double* bsig = ws + gl.bsig;
+    double* Wg = ws + gl.Wk;
 
     double* t = sm + L.t;
     double* lam = sm + L.lam;
@@ -590,6 +873,7 @@ __global__ __launch_bounds__(kWave) void mpc_riccati_kernel(const MpcConst c, co
     double* rd = sm + L.rd;
     double* gU = sm + L.gU;
     double* rh = sm + L.rh;
+    double* cr = sm + L.cr;
     double* sig = sm + L.sig;
     double* dsig = sm + L.dsig;
     double* Dsig = sm + L.Dsig;
@@ -718,7 +1002,12 @@ __global__ __launch_bounds__(kWave) void mpc_riccati_kernel(const MpcConst c, co
             Dsig[i] = v;
         }
         bar();
-        if (!riccati_factor(c, d, L, sm, A, B, C, F)) {
+        stage_weights(c, L, sm, C, Wg);
+        double thm_l = 0.0;
+        for (int r = l; r < m; r += kWave) thm_l = fmax(thm_l, th[r]);
+        const bool hp = wave_max(thm_l) > kDdTh;  // wave-uniform
+        bar();
+        if (!(hp ? riccati_factor_dd(c, d, L, sm, A, B, Wg, F) : riccati_factor(c, d, L, sm, A, B, Wg, F))) {
             stop = kStopBreakdown;
             break;
         }
@@ -766,7 +1055,25 @@ __global__ __launch_bounds__(kWave) void mpc_riccati_kernel(const MpcConst c, co
             // rhs = -rd - G' rt
             for (int i = l; i < n; i += kWave) rh[i] = -rd[i] - (rh[i] + rt[ms + 2 * i] - rt[ms + 2 * i + 1]);
             bar();
-            riccati_solve(c, d, L, sm, A, B, F);
+            riccati_solve(c, d, L, sm, A, B, F, rh, dU, dX);
+            if (hp) {
+                // refinement: dU += M^-1 (rhs - K dU), residual in double-double (gU, cr: free here)
+                for (int ir = 0; ir < kRefineMax; ++ir) {
+                    kres_dd(c, d, L, sm, A, B, Wg, dU, rh, gU);
+                    riccati_solve(c, d, L, sm, A, B, F, gU, cr, nullptr);
+                    double cn_l = 0.0, un_l = 0.0;
+                    for (int i = l; i < n; i += kWave) {
+                        const double u = dU[i] + cr[i];
+                        dU[i] = u;
+                        cn_l = nmax(cn_l, fabs(cr[i]));
+                        un_l = fmax(un_l, fabs(u));
+                    }
+                    const double cn = wave_max(cn_l), un = wave_max(un_l);
+                    bar();
+                    if (!(cn > 1e-16 * un)) break;
+                }
+                fwd_sim(c, d, sAB, sb, nullptr, dU, dX);
+            }
             for (int r = l; r < m; r += kWave) GdU[r] = row_value(c, C, r, dX, dU, nullptr);
             bar();
             for (int i = l; i < N * ns; i += kWave) {

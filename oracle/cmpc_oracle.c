@@ -17,7 +17,7 @@
  * (oracle/qp_ipm.py) on QPs captured from the reference (tests/golden).
  */
 #include <math.h>
-#ifdef ORACLE_TRACE
+#if defined(ORACLE_TRACE) || defined(RIC_DEBUG)
 #include <stdio.h>
 #endif
 #include <stdlib.h>
@@ -30,6 +30,8 @@ typedef struct {
     int nx, nu, N, ns, mc;
     const double *Q, *R, *dR, *Qs, *u_ub, *u_lb;
     const int *row_slack, *row_sign;
+    int newton, refine; /* refine: iterative-refinement steps of the Riccati solve */
+    /* newton: 0 condensed Cholesky; 1 Riccati (P = Qyy + A'PA + Hvy'K); 2 Riccati, Joseph form */
 } shared_t;
 
 typedef struct {
@@ -113,6 +115,753 @@ static void chol_solve(const double* L, int n, double* b) {
     }
 }
 
+
+#ifdef RIC_DEBUG
+#define NEWTON_C 0
+#else
+#define NEWTON_C (S->newton)
+#endif
+/* ---- stage-wise Riccati Newton solve (mirrors colaborativempc-_amd/csrc/mpc_riccati.hip) ----
+ * The condensed Newton system K dU = rhs is the LQ problem
+ *   min sum_{k>=1} 1/2 dX_k'W_k dX_k + sum_k 1/2 v_k'(2R + th_k) v_k + 1/2 (v_k - v_{k-1})'2dR(.) - rhs'v
+ *   s.t. dX_{k+1} = A_k dX_k + B_k v_k, dX_0 = 0, v_{-1} = 0,
+ * solved on the augmented state y_k = [dX_k; v_{k-1}] (na = nx + nu). */
+#define NA_MAX 16
+#define NU_MAX 4
+
+/* W = 2Q + M (stable group Schur form) for the stage rows of block k (rows of X_{k+1}) */
+static void stage_w(const shared_t* S, const agent_t* a, const double* th, const double* Dsig, int k, double* W) {
+    const int nx = S->nx, mc = S->mc, ns = S->ns;
+    for (int s = 0; s < nx * nx; ++s) W[s] = 2.0 * S->Q[s];
+    for (int r = 0; r < mc; ++r) {
+        const double* c1 = a->C + ((size_t)k * mc + r) * nx;
+        double th1 = th[k * mc + r];
+        int j = S->row_slack[r];
+        if (j < 0) {
+            for (int s = 0; s < nx; ++s) for (int u = 0; u < nx; ++u) W[s * nx + u] += th1 * c1[s] * c1[u];
+            continue;
+        }
+        double inv = 1.0 / Dsig[k * ns + j], q = 2.0 * S->Qs[j];
+        for (int s = 0; s < nx; ++s) for (int u = 0; u < nx; ++u) W[s * nx + u] += q * th1 * c1[s] * c1[u] * inv;
+        for (int r2 = r + 1; r2 < mc; ++r2) {
+            if (S->row_slack[r2] != j) continue;
+            const double* c2 = a->C + ((size_t)k * mc + r2) * nx;
+            double th2 = th[k * mc + r2], s1 = S->row_sign[r], s2 = S->row_sign[r2];
+            for (int s = 0; s < nx; ++s)
+                for (int u = 0; u < nx; ++u)
+                    W[s * nx + u] += th1 * th2 * (s1 * c1[s] - s2 * c2[s]) * (s1 * c1[u] - s2 * c2[u]) * inv;
+        }
+    }
+}
+
+/* gains F_k = [K_k (nu x na) | Hinv_k (nu x nu)];  returns -1 on a non-positive pivot */
+static int ric_factor(const shared_t* S, const agent_t* a, const double* th, const double* Dsig, double* F) {
+    const int nx = S->nx, nu = S->nu, N = S->N, na = nx + nu, ms = N * S->mc, sF = nu * na + nu * nu;
+    double P[NA_MAX * NA_MAX], Pn[NA_MAX * NA_MAX], W[NA_MAX * NA_MAX], H[NU_MAX * NU_MAX], Hy[NU_MAX * NA_MAX];
+    double Lf[NU_MAX * NU_MAX], Hi[NU_MAX * NU_MAX], Acl[NA_MAX * NA_MAX], T[NA_MAX * NA_MAX];
+    memset(P, 0, sizeof P);
+    stage_w(S, a, th, Dsig, N - 1, W);
+    for (int i = 0; i < nx; ++i) for (int j = 0; j < nx; ++j) P[i * na + j] = W[i * nx + j];
+    for (int k = N - 1; k >= 0; --k) {
+        const double* Ak = a->A + (size_t)k * nx * nx;
+        const double* Bk = a->B + (size_t)k * nx * nu;
+        /* Bb = [B_k; I] (na x nu), Ab = [[A_k, 0], [0, 0]];  PB = P Bb */
+        double PB[NA_MAX * NU_MAX];
+        for (int i = 0; i < na; ++i)
+            for (int c = 0; c < nu; ++c) {
+                double v = P[i * na + nx + c];
+                for (int s = 0; s < nx; ++s) v += P[i * na + s] * Bk[s * nu + c];
+                PB[i * nu + c] = v;
+            }
+        /* Hvv = 2R + 2dR + diag(th_u) + Bb'P Bb */
+        for (int c = 0; c < nu; ++c)
+            for (int e = 0; e < nu; ++e) {
+                double v = 2.0 * S->R[c * nu + e] + 2.0 * S->dR[c * nu + e] + PB[(nx + c) * nu + e];
+                for (int s = 0; s < nx; ++s) v += Bk[s * nu + c] * PB[s * nu + e];
+                if (c == e) { int r = ms + 2 * (k * nu + c); v += th[r] + th[r + 1]; }
+                H[c * nu + e] = v;
+            }
+        /* Hvy = [Bb'P[:, :nx] A_k | -2dR] */
+        for (int c = 0; c < nu; ++c)
+            for (int j = 0; j < na; ++j) {
+                double v = 0.0;
+                if (j < nx)
+                    for (int s = 0; s < nx; ++s) v += PB[s * nu + c] * Ak[s * nx + j];
+                else
+                    v = -2.0 * S->dR[c * nu + (j - nx)];
+                Hy[c * na + j] = v;
+            }
+        /* Cholesky of Hvv and its inverse */
+        for (int j = 0; j < nu; ++j) {
+            double d = H[j * nu + j];
+            for (int p = 0; p < j; ++p) d -= Lf[j * nu + p] * Lf[j * nu + p];
+            if (!(d > 0.0)) return -1;
+            d = sqrt(d);
+            Lf[j * nu + j] = d;
+            for (int i = j + 1; i < nu; ++i) {
+                double v = H[i * nu + j];
+                for (int p = 0; p < j; ++p) v -= Lf[i * nu + p] * Lf[j * nu + p];
+                Lf[i * nu + j] = v / d;
+            }
+        }
+        for (int c = 0; c < nu; ++c) {
+            double e[NU_MAX];
+            for (int i = 0; i < nu; ++i) e[i] = (i == c) ? 1.0 : 0.0;
+            for (int i = 0; i < nu; ++i) {
+                double v = e[i];
+                for (int p = 0; p < i; ++p) v -= Lf[i * nu + p] * e[p];
+                e[i] = v / Lf[i * nu + i];
+            }
+            for (int i = nu - 1; i >= 0; --i) {
+                double v = e[i];
+                for (int p = i + 1; p < nu; ++p) v -= Lf[p * nu + i] * e[p];
+                e[i] = v / Lf[i * nu + i];
+            }
+            for (int i = 0; i < nu; ++i) Hi[i * nu + c] = e[i];
+        }
+        double* Fk = F + (size_t)k * sF;
+        for (int c = 0; c < nu; ++c)
+            for (int j = 0; j < na; ++j) {
+                double v = 0.0;
+                for (int e = 0; e < nu; ++e) v -= Hi[c * nu + e] * Hy[e * na + j];
+                Fk[c * na + j] = v;
+            }
+        for (int c = 0; c < nu * nu; ++c) Fk[nu * na + c] = Hi[c];
+        if (k == 0) break;
+        stage_w(S, a, th, Dsig, k - 1, W);
+        const double* Kk = Fk;
+        if (S->newton == 2) {
+            /* Joseph form: P_k = blkdiag(W_k, 0) + K'(2R + th)K + (K - E)'2dR(K - E) + Acl'P Acl,
+               Acl = Ab + Bb K, E = [0 | I]: a sum of PSD terms */
+            for (int i = 0; i < na; ++i)
+                for (int j = 0; j < na; ++j) {
+                    double v;
+                    if (i < nx) {
+                        v = (j < nx) ? Ak[i * nx + j] : 0.0;
+                        for (int c = 0; c < nu; ++c) v += Bk[i * nu + c] * Kk[c * na + j];
+                    } else {
+                        v = Kk[(i - nx) * na + j];
+                    }
+                    Acl[i * na + j] = v;
+                }
+            for (int i = 0; i < na; ++i)
+                for (int j = 0; j < na; ++j) {
+                    double v = 0.0;
+                    for (int s = 0; s < na; ++s) v += P[i * na + s] * Acl[s * na + j];
+                    T[i * na + j] = v;
+                }
+            for (int i = 0; i < na; ++i)
+                for (int j = 0; j <= i; ++j) {
+                    double v = (i < nx && j < nx) ? W[i * nx + j] : 0.0;
+                    for (int s = 0; s < na; ++s) v += Acl[s * na + i] * T[s * na + j];
+                    for (int c = 0; c < nu; ++c) {
+                        const double kc_i = Kk[c * na + i], kc_j = Kk[c * na + j];
+                        double ru = 0.0;
+                        for (int e = 0; e < nu; ++e) {
+                            const double ke_j = Kk[e * na + j];
+                            ru += 2.0 * S->R[c * nu + e] * ke_j;
+                            const double d_i = kc_i - ((i >= nx && i - nx == c) ? 1.0 : 0.0);
+                            const double d_j = ke_j - ((j >= nx && j - nx == e) ? 1.0 : 0.0);
+                            v += d_i * 2.0 * S->dR[c * nu + e] * d_j;
+                        }
+                        const int r = ms + 2 * (k * nu + c);
+                        v += kc_i * (ru + (th[r] + th[r + 1]) * kc_j);
+                    }
+                    Pn[i * na + j] = v;
+                    Pn[j * na + i] = v;
+                }
+        } else {
+            /* P_k = blkdiag(W_k + A'Pxx A, 2dR) + Hvy'K */
+            for (int i = 0; i < na; ++i)
+                for (int j = 0; j <= i; ++j) {
+                    double v;
+                    if (i < nx) {
+                        v = W[i * nx + j];
+                        for (int s = 0; s < nx; ++s) {
+                            double pa = 0.0;
+                            for (int t2 = 0; t2 < nx; ++t2) pa += P[s * na + t2] * Ak[t2 * nx + j];
+                            v += Ak[s * nx + i] * pa;
+                        }
+                    } else {
+                        v = (j >= nx) ? 2.0 * S->dR[(i - nx) * nu + (j - nx)] : 0.0;
+                    }
+                    for (int c = 0; c < nu; ++c) v += Hy[c * na + i] * Kk[c * na + j];
+                    Pn[i * na + j] = v;
+                    Pn[j * na + i] = v;
+                }
+        }
+        memcpy(P, Pn, sizeof(double) * na * na);
+    }
+    return 0;
+}
+
+#ifdef RIC_QUAD
+#include <quadmath.h>
+typedef __float128 RQ;
+/* gains F_k = [K_k (nu x na) | Hinv_k (nu x nu)];  returns -1 on a non-positive pivot */
+static int ric_factor_q(const shared_t* S, const agent_t* a, const double* th, const double* Dsig, double* F) {
+    const int nx = S->nx, nu = S->nu, N = S->N, na = nx + nu, ms = N * S->mc, sF = nu * na + nu * nu;
+    RQ P[NA_MAX * NA_MAX], Pn[NA_MAX * NA_MAX], H[NU_MAX * NU_MAX], Hy[NU_MAX * NA_MAX]; double W[NA_MAX * NA_MAX];
+    RQ Lf[NU_MAX * NU_MAX], Hi[NU_MAX * NU_MAX], Acl[NA_MAX * NA_MAX], T[NA_MAX * NA_MAX], Kq[NU_MAX * NA_MAX];
+    memset(P, 0, sizeof P);
+    stage_w(S, a, th, Dsig, N - 1, W);
+    for (int i = 0; i < nx; ++i) for (int j = 0; j < nx; ++j) P[i * na + j] = W[i * nx + j];
+    for (int k = N - 1; k >= 0; --k) {
+        const double* Ak = a->A + (size_t)k * nx * nx;
+        const double* Bk = a->B + (size_t)k * nx * nu;
+        /* Bb = [B_k; I] (na x nu), Ab = [[A_k, 0], [0, 0]];  PB = P Bb */
+        RQ PB[NA_MAX * NU_MAX];
+        for (int i = 0; i < na; ++i)
+            for (int c = 0; c < nu; ++c) {
+                RQ v = P[i * na + nx + c];
+                for (int s = 0; s < nx; ++s) v += P[i * na + s] * Bk[s * nu + c];
+                PB[i * nu + c] = v;
+            }
+        /* Hvv = 2R + 2dR + diag(th_u) + Bb'P Bb */
+        for (int c = 0; c < nu; ++c)
+            for (int e = 0; e < nu; ++e) {
+                RQ v = (RQ)(2.0 * S->R[c * nu + e] + 2.0 * S->dR[c * nu + e]) + PB[(nx + c) * nu + e];
+                for (int s = 0; s < nx; ++s) v += Bk[s * nu + c] * PB[s * nu + e];
+                if (c == e) { int r = ms + 2 * (k * nu + c); v += th[r] + th[r + 1]; }
+                H[c * nu + e] = v;
+            }
+        /* Hvy = [Bb'P[:, :nx] A_k | -2dR] */
+        for (int c = 0; c < nu; ++c)
+            for (int j = 0; j < na; ++j) {
+                RQ v = 0.0;
+                if (j < nx)
+                    for (int s = 0; s < nx; ++s) v += PB[s * nu + c] * Ak[s * nx + j];
+                else
+                    v = -2.0 * S->dR[c * nu + (j - nx)];
+                Hy[c * na + j] = v;
+            }
+        /* Cholesky of Hvv and its inverse */
+        for (int j = 0; j < nu; ++j) {
+            RQ d = H[j * nu + j];
+            for (int p = 0; p < j; ++p) d -= Lf[j * nu + p] * Lf[j * nu + p];
+            if (!(d > 0.0)) return -1;
+            d = sqrtq(d);
+            Lf[j * nu + j] = d;
+            for (int i = j + 1; i < nu; ++i) {
+                RQ v = H[i * nu + j];
+                for (int p = 0; p < j; ++p) v -= Lf[i * nu + p] * Lf[j * nu + p];
+                Lf[i * nu + j] = v / d;
+            }
+        }
+        for (int c = 0; c < nu; ++c) {
+            RQ e[NU_MAX];
+            for (int i = 0; i < nu; ++i) e[i] = (i == c) ? 1.0 : 0.0;
+            for (int i = 0; i < nu; ++i) {
+                RQ v = e[i];
+                for (int p = 0; p < i; ++p) v -= Lf[i * nu + p] * e[p];
+                e[i] = v / Lf[i * nu + i];
+            }
+            for (int i = nu - 1; i >= 0; --i) {
+                RQ v = e[i];
+                for (int p = i + 1; p < nu; ++p) v -= Lf[p * nu + i] * e[p];
+                e[i] = v / Lf[i * nu + i];
+            }
+            for (int i = 0; i < nu; ++i) Hi[i * nu + c] = e[i];
+        }
+        double* Fk = F + (size_t)k * sF;
+        for (int c = 0; c < nu; ++c)
+            for (int j = 0; j < na; ++j) {
+                RQ v = 0.0;
+                for (int e = 0; e < nu; ++e) v -= Hi[c * nu + e] * Hy[e * na + j];
+                Fk[c * na + j] = (double)v;
+                Kq[c * na + j] = v;
+            }
+        for (int c = 0; c < nu * nu; ++c) Fk[nu * na + c] = (double)Hi[c];
+        if (k == 0) break;
+        stage_w(S, a, th, Dsig, k - 1, W);
+        const RQ* Kk = Kq;
+        if (S->newton == 2) {
+            /* Joseph form: P_k = blkdiag(W_k, 0) + K'(2R + th)K + (K - E)'2dR(K - E) + Acl'P Acl,
+               Acl = Ab + Bb K, E = [0 | I]: a sum of PSD terms */
+            for (int i = 0; i < na; ++i)
+                for (int j = 0; j < na; ++j) {
+                    RQ v;
+                    if (i < nx) {
+                        v = (j < nx) ? Ak[i * nx + j] : 0.0;
+                        for (int c = 0; c < nu; ++c) v += Bk[i * nu + c] * Kk[c * na + j];
+                    } else {
+                        v = Kk[(i - nx) * na + j];
+                    }
+                    Acl[i * na + j] = v;
+                }
+            for (int i = 0; i < na; ++i)
+                for (int j = 0; j < na; ++j) {
+                    RQ v = 0.0;
+                    for (int s = 0; s < na; ++s) v += P[i * na + s] * Acl[s * na + j];
+                    T[i * na + j] = v;
+                }
+            for (int i = 0; i < na; ++i)
+                for (int j = 0; j <= i; ++j) {
+                    RQ v = (i < nx && j < nx) ? W[i * nx + j] : 0.0;
+                    for (int s = 0; s < na; ++s) v += Acl[s * na + i] * T[s * na + j];
+                    for (int c = 0; c < nu; ++c) {
+                        const RQ kc_i = Kk[c * na + i], kc_j = Kk[c * na + j];
+                        RQ ru = 0.0;
+                        for (int e = 0; e < nu; ++e) {
+                            const RQ ke_j = Kk[e * na + j];
+                            ru += 2.0 * S->R[c * nu + e] * ke_j;
+                            const RQ d_i = kc_i - ((i >= nx && i - nx == c) ? 1.0 : 0.0);
+                            const RQ d_j = ke_j - ((j >= nx && j - nx == e) ? 1.0 : 0.0);
+                            v += d_i * 2.0 * S->dR[c * nu + e] * d_j;
+                        }
+                        const int r = ms + 2 * (k * nu + c);
+                        v += kc_i * (ru + (th[r] + th[r + 1]) * kc_j);
+                    }
+                    Pn[i * na + j] = v;
+                    Pn[j * na + i] = v;
+                }
+        } else {
+            /* P_k = blkdiag(W_k + A'Pxx A, 2dR) + Hvy'K */
+            for (int i = 0; i < na; ++i)
+                for (int j = 0; j <= i; ++j) {
+                    RQ v;
+                    if (i < nx) {
+                        v = W[i * nx + j];
+                        for (int s = 0; s < nx; ++s) {
+                            RQ pa = 0.0;
+                            for (int t2 = 0; t2 < nx; ++t2) pa += P[s * na + t2] * Ak[t2 * nx + j];
+                            v += Ak[s * nx + i] * pa;
+                        }
+                    } else {
+                        v = (j >= nx) ? 2.0 * S->dR[(i - nx) * nu + (j - nx)] : 0.0;
+                    }
+                    for (int c = 0; c < nu; ++c) v += Hy[c * na + i] * Kk[c * na + j];
+                    Pn[i * na + j] = v;
+                    Pn[j * na + i] = v;
+                }
+        }
+        memcpy(P, Pn, sizeof(RQ) * na * na);
+    }
+    return 0;
+}
+
+#endif
+/* dU, dX for the right-hand side rhs with the gains F */
+static void ric_solve(const shared_t* S, const agent_t* a, const double* F, const double* rhs, double* dU, double* dX) {
+    const int nx = S->nx, nu = S->nu, N = S->N, na = nx + nu, sF = nu * na + nu * nu;
+    double p[NA_MAX], pn[NA_MAX], g[NA_MAX];
+    memset(p, 0, sizeof p);
+    for (int k = N - 1; k >= 0; --k) {
+        const double* Ak = a->A + (size_t)k * nx * nx;
+        const double* Bk = a->B + (size_t)k * nx * nu;
+        const double* Kg = F + (size_t)k * sF;
+        const double* Hg = Kg + nu * na;
+        for (int c = 0; c < nu; ++c) {
+            double v = p[nx + c] - rhs[k * nu + c];
+            for (int s = 0; s < nx; ++s) v += Bk[s * nu + c] * p[s];
+            g[c] = v;
+        }
+        for (int c = 0; c < nu; ++c) {
+            double v = 0.0;
+            for (int e = 0; e < nu; ++e) v -= Hg[c * nu + e] * g[e];
+            dU[k * nu + c] = v;
+        }
+        for (int j = 0; j < na; ++j) {
+            double v = 0.0;
+            if (j < nx)
+                for (int s = 0; s < nx; ++s) v += Ak[s * nx + j] * p[s];
+            for (int c = 0; c < nu; ++c) v += Kg[c * na + j] * g[c];
+            pn[j] = v;
+        }
+        memcpy(p, pn, sizeof(double) * na);
+    }
+    for (int s = 0; s < nx; ++s) dX[s] = 0.0;
+    for (int k = 0; k < N; ++k) {
+        const double* Ak = a->A + (size_t)k * nx * nx;
+        const double* Bk = a->B + (size_t)k * nx * nu;
+        const double* Kg = F + (size_t)k * sF;
+        for (int c = 0; c < nu; ++c) {
+            double v = dU[k * nu + c];
+            for (int j = 0; j < nx; ++j) v += Kg[c * na + j] * dX[k * nx + j];
+            if (k > 0)
+                for (int e = 0; e < nu; ++e) v += Kg[c * na + nx + e] * dU[(k - 1) * nu + e];
+            dU[k * nu + c] = v;
+        }
+        for (int s = 0; s < nx; ++s) {
+            double v = 0.0;
+            for (int t2 = 0; t2 < nx; ++t2) v += Ak[s * nx + t2] * dX[k * nx + t2];
+            for (int c = 0; c < nu; ++c) v += Bk[s * nu + c] * dU[k * nu + c];
+            dX[(k + 1) * nx + s] = v;
+        }
+    }
+}
+
+
+/* y = K v for the condensed Newton matrix K = sum_k Gamma_k'W_k Gamma_k + 2R + 2D'dR D + diag(th_u),
+   matrix-free through the stage recursions (dX = Gamma v, then the adjoint) */
+static void kmul(const shared_t* S, const agent_t* a, const double* th, const double* Dsig, const double* v, double* y,
+                 double* dX, double* yb, double* psi, double* tmp) {
+    const int nx = S->nx, nu = S->nu, N = S->N, ms = N * S->mc;
+    double W[NA_MAX * NA_MAX];
+    fwd_sim(S, a, NULL, v, dX);
+    for (int s = 0; s < nx; ++s) yb[s] = 0.0;
+    for (int k = 1; k <= N; ++k) {
+        stage_w(S, a, th, Dsig, k - 1, W);
+        for (int s = 0; s < nx; ++s) {
+            double acc = 0.0;
+            for (int u = 0; u < nx; ++u) acc += W[s * nx + u] * dX[k * nx + u];
+            yb[k * nx + s] = acc;
+        }
+    }
+    adjoint(S, a, yb, y, psi, tmp);
+    for (int k = 0; k < N; ++k)
+        for (int i = 0; i < nu; ++i) {
+            double acc = 0.0;
+            for (int j = 0; j < nu; ++j) {
+                const double vk = v[k * nu + j];
+                const double dk = vk - (k ? v[(k - 1) * nu + j] : 0.0);
+                const double dn = (k + 1 < N) ? v[(k + 1) * nu + j] - vk : 0.0;
+                acc += 2.0 * S->R[i * nu + j] * vk + 2.0 * S->dR[i * nu + j] * (dk - dn);
+            }
+            const int r = ms + 2 * (k * nu + i);
+            y[k * nu + i] += acc + (th[r] + th[r + 1]) * v[k * nu + i];
+        }
+}
+
+
+#ifdef RIC_QREF
+#include <quadmath.h>
+/* debug: the condensed Newton solve in quad precision (reference direction) */
+static void condensed_q(const shared_t* S, const agent_t* a, const double* th, const double* Dsig, const double* rhs,
+                        double* out) {
+    const int nx = S->nx, nu = S->nu, N = S->N, n = N * nu, mc = S->mc, ns = S->ns, ms = N * mc;
+    __float128* G = calloc((size_t)(N + 1) * nx * n, sizeof(__float128));
+    __float128* K = calloc((size_t)n * n, sizeof(__float128));
+    __float128 W[NA_MAX * NA_MAX];
+    for (int k = 0; k < N; ++k) {
+        const double* Ak = a->A + (size_t)k * nx * nx;
+        const double* Bk = a->B + (size_t)k * nx * nu;
+        for (int s = 0; s < nx; ++s)
+            for (int c = 0; c < n; ++c) {
+                __float128 v = 0;
+                for (int t = 0; t < nx; ++t) v += (__float128)Ak[s * nx + t] * G[((size_t)k * nx + t) * n + c];
+                if (c >= k * nu && c < (k + 1) * nu) v += Bk[s * nu + (c - k * nu)];
+                G[((size_t)(k + 1) * nx + s) * n + c] = v;
+            }
+    }
+    for (int k = 0; k < N; ++k) {
+        for (int s = 0; s < nx * nx; ++s) W[s] = 2.0 * S->Q[s];
+        for (int r = 0; r < mc; ++r) {
+            const double* c1 = a->C + ((size_t)k * mc + r) * nx;
+            __float128 th1 = th[k * mc + r];
+            int j = S->row_slack[r];
+            if (j < 0) { for (int s = 0; s < nx; ++s) for (int u = 0; u < nx; ++u) W[s * nx + u] += th1 * c1[s] * c1[u]; continue; }
+            __float128 D = 2.0 * S->Qs[j];
+            for (int r2 = 0; r2 < mc; ++r2) if (S->row_slack[r2] == j) D += th[k * mc + r2];
+            __float128 q = 2.0 * S->Qs[j];
+            for (int s = 0; s < nx; ++s) for (int u = 0; u < nx; ++u) W[s * nx + u] += q * th1 * c1[s] * c1[u] / D;
+            for (int r2 = r + 1; r2 < mc; ++r2) {
+                if (S->row_slack[r2] != j) continue;
+                const double* c2 = a->C + ((size_t)k * mc + r2) * nx;
+                __float128 th2 = th[k * mc + r2], s1 = S->row_sign[r], s2 = S->row_sign[r2];
+                for (int s = 0; s < nx; ++s) for (int u = 0; u < nx; ++u)
+                    W[s * nx + u] += th1 * th2 * (s1 * c1[s] - s2 * c2[s]) * (s1 * c1[u] - s2 * c2[u]) / D;
+            }
+        }
+        const __float128* Gk = G + (size_t)(k + 1) * nx * n;
+        const int ncol = (k + 1) * nu;
+        __float128* Y = calloc((size_t)nx * ncol, sizeof(__float128));
+        for (int s = 0; s < nx; ++s) for (int c2 = 0; c2 < ncol; ++c2) { __float128 y = 0; for (int u = 0; u < nx; ++u) y += W[s * nx + u] * Gk[u * n + c2]; Y[s * ncol + c2] = y; }
+        for (int c1 = 0; c1 < ncol; ++c1)
+            for (int c2 = 0; c2 <= c1; ++c2) {
+                __float128 v = 0;
+                for (int s = 0; s < nx; ++s) v += Gk[s * n + c1] * Y[s * ncol + c2];
+                K[(size_t)c1 * n + c2] += v;
+            }
+        free(Y);
+    }
+    for (int k = 0; k < N; ++k)
+        for (int i = 0; i < nu; ++i)
+            for (int j = 0; j < nu; ++j) {
+                int ci = k * nu + i, cj = k * nu + j;
+                __float128 v = 2.0 * S->R[i * nu + j] + 2.0 * S->dR[i * nu + j] * (k + 1 < N ? 2.0 : 1.0);
+                if (cj <= ci) K[(size_t)ci * n + cj] += v;
+                if (k > 0) K[(size_t)ci * n + (k - 1) * nu + j] += -2.0 * S->dR[i * nu + j];
+            }
+    for (int k = 0; k < N; ++k)
+        for (int i = 0; i < nu; ++i) { int r = ms + (k * nu + i) * 2; K[(size_t)(k * nu + i) * n + k * nu + i] += (__float128)th[r] + th[r + 1]; }
+    for (int j = 0; j < n; ++j) {
+        __float128 d = K[(size_t)j * n + j];
+        for (int p = 0; p < j; ++p) d -= K[(size_t)j * n + p] * K[(size_t)j * n + p];
+        d = sqrtq(d); K[(size_t)j * n + j] = d;
+        for (int i = j + 1; i < n; ++i) { __float128 v = K[(size_t)i * n + j]; for (int p = 0; p < j; ++p) v -= K[(size_t)i * n + p] * K[(size_t)j * n + p]; K[(size_t)i * n + j] = v / d; }
+    }
+    __float128* b = calloc(n, sizeof(__float128));
+    for (int i = 0; i < n; ++i) { __float128 v = rhs[i]; for (int p = 0; p < i; ++p) v -= K[(size_t)i * n + p] * b[p]; b[i] = v / K[(size_t)i * n + i]; }
+    for (int i = n - 1; i >= 0; --i) { __float128 v = b[i]; for (int p = i + 1; p < n; ++p) v -= K[(size_t)p * n + i] * b[p]; b[i] = v / K[(size_t)i * n + i]; }
+    for (int i = 0; i < n; ++i) out[i] = (double)b[i];
+    free(G); free(K); free(b); (void)Dsig; (void)ns;
+}
+#endif
+
+
+#ifdef KMUL_QUAD
+#include <quadmath.h>
+/* r = rhs - K v with the product in quad precision (residual for iterative refinement) */
+static void kres_q(const shared_t* S, const agent_t* a, const double* th, const double* Dsig, const double* v,
+                   const double* rhs, double* out) {
+    const int nx = S->nx, nu = S->nu, N = S->N, ms = N * S->mc;
+    double W[NA_MAX * NA_MAX];
+    __float128 X[(NA_MAX) * 256], Y[NA_MAX * 256], psi[NA_MAX], tmp[NA_MAX];
+    for (int s = 0; s < nx; ++s) X[s] = 0;
+    for (int k = 0; k < N; ++k) {
+        const double* Ak = a->A + (size_t)k * nx * nx;
+        const double* Bk = a->B + (size_t)k * nx * nu;
+        for (int s = 0; s < nx; ++s) {
+            __float128 acc = 0;
+            for (int t = 0; t < nx; ++t) acc += (__float128)Ak[s * nx + t] * X[k * nx + t];
+            for (int i = 0; i < nu; ++i) acc += (__float128)Bk[s * nu + i] * v[k * nu + i];
+            X[(k + 1) * nx + s] = acc;
+        }
+    }
+    for (int k = 1; k <= N; ++k) {
+        stage_w(S, a, th, Dsig, k - 1, W);
+        for (int s = 0; s < nx; ++s) {
+            __float128 acc = 0;
+            for (int u = 0; u < nx; ++u) acc += (__float128)W[s * nx + u] * X[k * nx + u];
+            Y[k * nx + s] = acc;
+        }
+    }
+    for (int s = 0; s < nx; ++s) psi[s] = Y[N * nx + s];
+    for (int k = N - 1; k >= 0; --k) {
+        const double* Ak = a->A + (size_t)k * nx * nx;
+        const double* Bk = a->B + (size_t)k * nx * nu;
+        for (int i = 0; i < nu; ++i) {
+            __float128 acc = 0;
+            for (int s = 0; s < nx; ++s) acc += (__float128)Bk[s * nu + i] * psi[s];
+            for (int j = 0; j < nu; ++j) {
+                const __float128 vk = v[k * nu + j];
+                const __float128 dk = vk - (k ? (__float128)v[(k - 1) * nu + j] : 0);
+                const __float128 dn = (k + 1 < N) ? (__float128)v[(k + 1) * nu + j] - vk : 0;
+                acc += 2.0 * S->R[i * nu + j] * vk + 2.0 * S->dR[i * nu + j] * (dk - dn);
+            }
+            const int r = ms + 2 * (k * nu + i);
+            acc += ((__float128)th[r] + th[r + 1]) * v[k * nu + i];
+            out[k * nu + i] = (double)((__float128)rhs[k * nu + i] - acc);
+        }
+        if (k > 0) {
+            for (int t = 0; t < nx; ++t) {
+                __float128 acc = Y[k * nx + t];
+                for (int s = 0; s < nx; ++s) acc += (__float128)Ak[s * nx + t] * psi[s];
+                tmp[t] = acc;
+            }
+            for (int t = 0; t < nx; ++t) psi[t] = tmp[t];
+        }
+    }
+}
+#endif
+
+
+/* ---- double-double arithmetic (hi + lo, |lo| <= ulp(hi)/2; fma-based, as the kernel's) ----
+ * The Riccati factor and the refinement residual switch to it once max th exceeds RIC_DD_TH:
+ * there the double recursion's error grows past what Newton can absorb (near the solution
+ * th -> 1e18..1e21 on saturated inputs and collision rows; SURVEY M4's 1e8 conditioning). */
+typedef struct { double hi, lo; } dd_t;
+static inline dd_t dd_qts(double a, double b) { double s = a + b; dd_t r = {s, b - (s - a)}; return r; }
+static inline dd_t dd_ts(double a, double b) {
+    double s = a + b, bb = s - a;
+    dd_t r = {s, (a - (s - bb)) + (b - bb)};
+    return r;
+}
+static inline dd_t dd_add(dd_t x, dd_t y) {
+    dd_t s = dd_ts(x.hi, y.hi);
+    return dd_qts(s.hi, s.lo + x.lo + y.lo);
+}
+static inline dd_t dd_mul(dd_t x, dd_t y) {
+    double p = x.hi * y.hi, e = fma(x.hi, y.hi, -p);
+    e = fma(x.hi, y.lo, fma(x.lo, y.hi, e));
+    return dd_qts(p, e);
+}
+static inline dd_t dd_muld(dd_t x, double y) {
+    double p = x.hi * y, e = fma(x.hi, y, -p);
+    e = fma(x.lo, y, e);
+    return dd_qts(p, e);
+}
+static inline dd_t dd_fma(dd_t acc, dd_t x, dd_t y) { return dd_add(acc, dd_mul(x, y)); }
+static inline dd_t dd_fmad(dd_t acc, dd_t x, double y) { return dd_add(acc, dd_muld(x, y)); }
+static inline dd_t dd_d(double a) { dd_t r = {a, 0.0}; return r; }
+static inline dd_t dd_neg(dd_t x) { dd_t r = {-x.hi, -x.lo}; return r; }
+static inline dd_t dd_div(dd_t x, dd_t y) {
+    double q1 = x.hi / y.hi;
+    dd_t r = dd_add(x, dd_neg(dd_muld(y, q1)));
+    double q2 = r.hi / y.hi;
+    r = dd_add(r, dd_neg(dd_muld(y, q2)));
+    double q3 = r.hi / y.hi;
+    dd_t q = dd_qts(q1, q2);
+    return dd_add(q, dd_d(q3));
+}
+static inline dd_t dd_sqrt(dd_t x) {
+    double s = sqrt(x.hi);
+    dd_t r = dd_add(x, dd_neg(dd_mul(dd_d(s), dd_d(s))));
+    return dd_qts(s, r.hi / (2.0 * s));
+}
+
+#ifndef RIC_DD_TH
+#define RIC_DD_TH 1e10
+#endif
+#define RIC_REFINE_MAX 6
+
+/* ric_factor in double-double (standard form); gains rounded to double */
+static int ric_factor_dd(const shared_t* S, const agent_t* a, const double* th, const double* Dsig, double* F) {
+    const int nx = S->nx, nu = S->nu, N = S->N, na = nx + nu, ms = N * S->mc, sF = nu * na + nu * nu;
+    dd_t P[NA_MAX * NA_MAX], Pn[NA_MAX * NA_MAX], H[NU_MAX * NU_MAX], Hy[NU_MAX * NA_MAX], Lf[NU_MAX * NU_MAX],
+        Hi[NU_MAX * NU_MAX], Kk[NU_MAX * NA_MAX], PB[NA_MAX * NU_MAX], PA[NA_MAX * NA_MAX];
+    double W[NA_MAX * NA_MAX];
+    for (int e = 0; e < na * na; ++e) P[e] = dd_d(0.0);
+    stage_w(S, a, th, Dsig, N - 1, W);
+    for (int i = 0; i < nx; ++i) for (int j = 0; j < nx; ++j) P[i * na + j] = dd_d(W[i * nx + j]);
+    for (int k = N - 1; k >= 0; --k) {
+        const double* Ak = a->A + (size_t)k * nx * nx;
+        const double* Bk = a->B + (size_t)k * nx * nu;
+        for (int i = 0; i < na; ++i)
+            for (int c = 0; c < nu; ++c) {
+                dd_t v = P[i * na + nx + c];
+                for (int s = 0; s < nx; ++s) v = dd_fmad(v, P[i * na + s], Bk[s * nu + c]);
+                PB[i * nu + c] = v;
+            }
+        for (int c = 0; c < nu; ++c)
+            for (int e = 0; e < nu; ++e) {
+                dd_t v = dd_add(dd_d(2.0 * S->R[c * nu + e]), dd_add(dd_d(2.0 * S->dR[c * nu + e]), PB[(nx + c) * nu + e]));
+                for (int s = 0; s < nx; ++s) v = dd_fmad(v, PB[s * nu + e], Bk[s * nu + c]);
+                if (c == e) { int r = ms + 2 * (k * nu + c); v = dd_add(v, dd_add(dd_d(th[r]), dd_d(th[r + 1]))); }
+                H[c * nu + e] = v;
+            }
+        /* PA = P[:, :nx] A_k (na x nx) */
+        for (int i = 0; i < na; ++i)
+            for (int j = 0; j < nx; ++j) {
+                dd_t v = dd_d(0.0);
+                for (int s = 0; s < nx; ++s) v = dd_fmad(v, P[i * na + s], Ak[s * nx + j]);
+                PA[i * nx + j] = v;
+            }
+        for (int c = 0; c < nu; ++c)
+            for (int j = 0; j < na; ++j) {
+                dd_t v;
+                if (j < nx) {
+                    v = PA[(nx + c) * nx + j];
+                    for (int s = 0; s < nx; ++s) v = dd_fmad(v, PA[s * nx + j], Bk[s * nu + c]);
+                } else {
+                    v = dd_d(-2.0 * S->dR[c * nu + (j - nx)]);
+                }
+                Hy[c * na + j] = v;
+            }
+        for (int j = 0; j < nu; ++j) {
+            dd_t d = H[j * nu + j];
+            for (int p = 0; p < j; ++p) d = dd_add(d, dd_neg(dd_mul(Lf[j * nu + p], Lf[j * nu + p])));
+            if (!(d.hi > 0.0)) return -1;
+            d = dd_sqrt(d);
+            Lf[j * nu + j] = d;
+            for (int i = j + 1; i < nu; ++i) {
+                dd_t v = H[i * nu + j];
+                for (int p = 0; p < j; ++p) v = dd_add(v, dd_neg(dd_mul(Lf[i * nu + p], Lf[j * nu + p])));
+                Lf[i * nu + j] = dd_div(v, d);
+            }
+        }
+        for (int c = 0; c < nu; ++c) {
+            dd_t e[NU_MAX];
+            for (int i = 0; i < nu; ++i) e[i] = dd_d(i == c ? 1.0 : 0.0);
+            for (int i = 0; i < nu; ++i) {
+                dd_t v = e[i];
+                for (int p = 0; p < i; ++p) v = dd_add(v, dd_neg(dd_mul(Lf[i * nu + p], e[p])));
+                e[i] = dd_div(v, Lf[i * nu + i]);
+            }
+            for (int i = nu - 1; i >= 0; --i) {
+                dd_t v = e[i];
+                for (int p = i + 1; p < nu; ++p) v = dd_add(v, dd_neg(dd_mul(Lf[p * nu + i], e[p])));
+                e[i] = dd_div(v, Lf[i * nu + i]);
+            }
+            for (int i = 0; i < nu; ++i) Hi[i * nu + c] = e[i];
+        }
+        double* Fk = F + (size_t)k * sF;
+        for (int c = 0; c < nu; ++c)
+            for (int j = 0; j < na; ++j) {
+                dd_t v = dd_d(0.0);
+                for (int e = 0; e < nu; ++e) v = dd_add(v, dd_neg(dd_mul(Hi[c * nu + e], Hy[e * na + j])));
+                Kk[c * na + j] = v;
+                Fk[c * na + j] = v.hi;
+            }
+        for (int c = 0; c < nu * nu; ++c) Fk[nu * na + c] = Hi[c].hi;
+        if (k == 0) break;
+        stage_w(S, a, th, Dsig, k - 1, W);
+        /* P_k = blkdiag(W_k + A'Pxx A, 2dR) + Hvy'K */
+        for (int i = 0; i < na; ++i)
+            for (int j = 0; j <= i; ++j) {
+                dd_t v;
+                if (i < nx) {
+                    v = dd_d(W[i * nx + j]);
+                    for (int s = 0; s < nx; ++s) v = dd_fmad(v, PA[s * nx + j], Ak[s * nx + i]);
+                } else {
+                    v = dd_d((j >= nx) ? 2.0 * S->dR[(i - nx) * nu + (j - nx)] : 0.0);
+                }
+                for (int c = 0; c < nu; ++c) v = dd_fma(v, Hy[c * na + i], Kk[c * na + j]);
+                Pn[i * na + j] = v;
+                Pn[j * na + i] = v;
+            }
+        memcpy(P, Pn, sizeof(dd_t) * na * na);
+    }
+    return 0;
+}
+
+/* out = rhs - K v, the product in double-double (refinement residual; K as in kmul) */
+static void kres_dd(const shared_t* S, const agent_t* a, const double* th, const double* Dsig, const double* v,
+                    const double* rhs, double* out, dd_t* X) {
+    const int nx = S->nx, nu = S->nu, N = S->N, ms = N * S->mc;
+    double W[NA_MAX * NA_MAX];
+    dd_t psi[NA_MAX], tmp[NA_MAX], yk[NA_MAX];
+    for (int s = 0; s < nx; ++s) X[s] = dd_d(0.0);
+    for (int k = 0; k < N; ++k) {
+        const double* Ak = a->A + (size_t)k * nx * nx;
+        const double* Bk = a->B + (size_t)k * nx * nu;
+        for (int s = 0; s < nx; ++s) {
+            dd_t acc = dd_d(0.0);
+            for (int t = 0; t < nx; ++t) acc = dd_fmad(acc, X[k * nx + t], Ak[s * nx + t]);
+            for (int i = 0; i < nu; ++i) acc = dd_add(acc, dd_mul(dd_d(Bk[s * nu + i]), dd_d(v[k * nu + i])));
+            X[(k + 1) * nx + s] = acc;
+        }
+    }
+    for (int k = N; k >= 1; --k) { /* W_k X_k into X (in place, stage by stage from the end) */
+        stage_w(S, a, th, Dsig, k - 1, W);
+        for (int s = 0; s < nx; ++s) {
+            dd_t acc = dd_d(0.0);
+            for (int u = 0; u < nx; ++u) acc = dd_fmad(acc, X[k * nx + u], W[s * nx + u]);
+            yk[s] = acc;
+        }
+        for (int s = 0; s < nx; ++s) X[k * nx + s] = yk[s];
+    }
+    for (int s = 0; s < nx; ++s) psi[s] = X[N * nx + s];
+    for (int k = N - 1; k >= 0; --k) {
+        const double* Ak = a->A + (size_t)k * nx * nx;
+        const double* Bk = a->B + (size_t)k * nx * nu;
+        for (int i = 0; i < nu; ++i) {
+            dd_t acc = dd_d(0.0);
+            for (int s = 0; s < nx; ++s) acc = dd_fmad(acc, psi[s], Bk[s * nu + i]);
+            for (int j = 0; j < nu; ++j) {
+                const double vk = v[k * nu + j];
+                const dd_t dk = dd_ts(vk, k ? -v[(k - 1) * nu + j] : 0.0);
+                const dd_t dn = (k + 1 < N) ? dd_ts(v[(k + 1) * nu + j], -vk) : dd_d(0.0);
+                acc = dd_add(acc, dd_mul(dd_d(2.0 * S->R[i * nu + j]), dd_d(vk)));
+                acc = dd_fmad(acc, dd_add(dk, dd_neg(dn)), 2.0 * S->dR[i * nu + j]);
+            }
+            const int r = ms + 2 * (k * nu + i);
+            acc = dd_fmad(acc, dd_add(dd_d(th[r]), dd_d(th[r + 1])), v[k * nu + i]);
+            dd_t res = dd_add(dd_d(rhs[k * nu + i]), dd_neg(acc));
+            out[k * nu + i] = res.hi;
+        }
+        if (k > 0) {
+            for (int t = 0; t < nx; ++t) {
+                dd_t acc = X[k * nx + t];
+                for (int s = 0; s < nx; ++s) acc = dd_fmad(acc, psi[s], Ak[s * nx + t]);
+                tmp[t] = acc;
+            }
+            for (int t = 0; t < nx; ++t) psi[t] = tmp[t];
+        }
+    }
+}
+
 /* largest step keeping v + a dv >= 0 (unbounded: +inf; callers clip) */
 static double max_step(const double* v, const double* dv, const unsigned char* act, int m) {
     double a = INFINITY;
@@ -125,8 +874,9 @@ static double max_step(const double* v, const double* dv, const unsigned char* a
 }
 
 typedef struct {
+    dd_t* Xdd;
     double *bU, *bsig, *Gam, *K, *X, *dX, *U, *dU, *sig, *dsig, *Dsig, *rsig, *t, *lam, *th, *rho, *rt, *rp, *w,
-        *dt_a, *dl_a, *dtv, *dlv, *GdU, *ybar, *gU, *rd, *rhs, *psi, *tmp, *W, *Yk;
+        *dt_a, *dl_a, *dtv, *dlv, *GdU, *ybar, *gU, *rd, *rhs, *psi, *tmp, *W, *Yk, *F;
     unsigned char* act;
 } work_t;
 
@@ -136,8 +886,8 @@ static int solve_one(const shared_t* S, const agent_t* a, double tol, int max_it
     const int nx = S->nx, nu = S->nu, N = S->N, ns = S->ns, mc = S->mc;
     const int n = N * nu, ms = N * mc, m = ms + 2 * nu * N;
     double* Gam = wk->Gam; /* (N+1) x nx x n */
-    memset(Gam, 0, sizeof(double) * (size_t)(N + 1) * nx * n);
-    for (int k = 0; k < N; ++k) {
+    if (!NEWTON_C) memset(Gam, 0, sizeof(double) * (size_t)(N + 1) * nx * n);
+    for (int k = 0; k < N && !NEWTON_C; ++k) {
         const double* Ak = a->A + (size_t)k * nx * nx;
         const double* Bk = a->B + (size_t)k * nx * nu;
         double* Gn = Gam + (size_t)(k + 1) * nx * n;
@@ -189,12 +939,39 @@ static int solve_one(const shared_t* S, const agent_t* a, double tol, int max_it
         }                                                                               \
     } while (0)
 
+#ifdef SIGMA_START
+    /* slack-consistent start: sigma_j = the projection of 0 onto the interval the group's rows
+       allow at X (most relaxed feasible slack); the binding row carries lambda = |2 Qs sigma|,
+       the slack stationarity 2 Qs sigma + sum sign lambda = 0 */
+    for (int k = 0; k < N; ++k)
+        for (int j = 0; j < ns; ++j) {
+            double lo = -INFINITY, hi = INFINITY;
+            for (int r = 0; r < mc; ++r) {
+                if (S->row_slack[r] != j || !wk->act[k * mc + r]) continue;
+                double g; ROWVAL(X, U, (const double*)NULL, k * mc + r, g);
+                const double e = wk->w[k * mc + r] - g; /* sign sigma <= e */
+                if (S->row_sign[r] > 0) hi = fmin(hi, e); else lo = fmax(lo, -e);
+            }
+            double s = 0.0;
+            if (hi < 0.0) s = hi; else if (lo > 0.0) s = lo;
+            sig[k * ns + j] = SIGMA_START * s;
+        }
+#endif
     for (int r = 0; r < m; ++r) {
         if (!wk->act[r]) { t[r] = 1.0; lam[r] = 0.0; continue; }
         double g; ROWVAL(X, U, sig, r, g);
         double s0 = wk->w[r] - g;
         t[r] = s0 > 1.0 ? s0 : 1.0;
         lam[r] = 1.0;
+#ifdef SIGMA_START
+        if (r < ms) {
+            const int j = S->row_slack[r % mc];
+            if (j >= 0) {
+                const double sg = sig[(r / mc) * ns + j];
+                if (S->row_sign[r % mc] * sg < 0.0 && s0 < 1e-12 + fabs(sg) * 1e-9) lam[r] = fmax(1.0, LAMF * 2.0 * S->Qs[j] * fabs(sg));
+            }
+        }
+#endif
     }
     double scale_p = 1.0;
     for (int r = 0; r < m; ++r) if (wk->act[r] && fabs(wk->w[r]) > scale_p) scale_p = fabs(wk->w[r]);
@@ -291,7 +1068,11 @@ static int solve_one(const shared_t* S, const agent_t* a, double tol, int max_it
         if (best_m < 1e3 * tol && it - best_it >= STALL_ITERS) { stop = 3; break; }
 
         /* ---- Newton matrix ---- */
+        int hp = 0; /* Riccati: this iteration factors in double-double (newton == 3) */
         for (int r = 0; r < m; ++r) wk->th[r] = wk->act[r] ? lam[r] / t[r] : 0.0;
+#ifdef THMAX
+        for (int r = 0; r < m; ++r) wk->th[r] = fmin(wk->th[r], THMAX);
+#endif
         for (int k = 0; k < N; ++k)
             for (int j = 0; j < ns; ++j) {
                 double v = 2.0 * S->Qs[j];
@@ -299,9 +1080,22 @@ static int solve_one(const shared_t* S, const agent_t* a, double tol, int max_it
                 wk->Dsig[k * ns + j] = v;
             }
         double* K = wk->K;
-        memset(K, 0, sizeof(double) * n * n);
         double* W = wk->W;
-        for (int k = 0; k < N; ++k) {
+        if (S->newton) {
+                        hp = 0;
+            if (S->newton == 3) {
+                double thm = 0.0;
+                for (int r = 0; r < m; ++r) if (wk->act[r] && wk->th[r] > thm) thm = wk->th[r];
+                hp = thm > RIC_DD_TH;
+            }
+#ifdef RIC_QUAD
+            if (ric_factor_q(S, a, wk->th, wk->Dsig, wk->F)) { stop = 2; break; }
+#else
+            if (hp ? ric_factor_dd(S, a, wk->th, wk->Dsig, wk->F) : ric_factor(S, a, wk->th, wk->Dsig, wk->F)) { stop = 2; break; }
+#endif
+        }
+        if (!NEWTON_C) memset(K, 0, sizeof(double) * n * n);
+        for (int k = 0; k < N && !NEWTON_C; ++k) {
             /* W = 2Q + M_{k+1} (stable group Schur forms) */
             for (int s = 0; s < nx * nx; ++s) W[s] = 2.0 * S->Q[s];
             for (int r = 0; r < mc; ++r) {
@@ -340,7 +1134,7 @@ static int solve_one(const shared_t* S, const agent_t* a, double tol, int max_it
                     K[IDX2(c1, c2, n)] += v;
                 }
         }
-        for (int k = 0; k < N; ++k)
+        for (int k = 0; k < N && !NEWTON_C; ++k)
             for (int i = 0; i < nu; ++i)
                 for (int j = 0; j < nu; ++j) {
                     int ci = k * nu + i, cj = k * nu + j;
@@ -348,12 +1142,17 @@ static int solve_one(const shared_t* S, const agent_t* a, double tol, int max_it
                     if (cj <= ci) K[IDX2(ci, cj, n)] += v;
                     if (k > 0 && 1) K[IDX2(ci, (k - 1) * nu + j, n)] += -2.0 * S->dR[i * nu + j];
                 }
-        for (int k = 0; k < N; ++k)
+        for (int k = 0; k < N && !NEWTON_C; ++k)
             for (int i = 0; i < nu; ++i) {
                 int r = ms + (k * nu + i) * 2;
                 K[IDX2(k * nu + i, k * nu + i, n)] += wk->th[r] + wk->th[r + 1];
             }
-        if (chol(K, n)) { stop = 2; break; }
+#ifdef RIC_DEBUG
+        const int chol_bad = chol(K, n);
+        if (!S->newton && chol_bad) { stop = 2; break; }
+#else
+        if (!S->newton && chol(K, n)) { stop = 2; break; }
+#endif
 
         /* ---- predictor / corrector ---- */
         double sig_c = 0.0, mu_aff = 0.0;
@@ -393,9 +1192,65 @@ static int solve_one(const shared_t* S, const agent_t* a, double tol, int max_it
                 int r = ms + c * 2;
                 wk->rhs[c] = -wk->rd[c] - (wk->rhs[c] + wk->rt[r] - wk->rt[r + 1]);
             }
-            memcpy(wk->dU, wk->rhs, sizeof(double) * n);
-            chol_solve(K, n, wk->dU);
-            fwd_sim(S, a, NULL, wk->dU, wk->dX);
+            if (S->newton) {
+                ric_solve(S, a, wk->F, wk->rhs, wk->dU, wk->dX);
+                /* iterative refinement: dU += M^-1 (rhs - K dU) */
+                const int nref = hp ? RIC_REFINE_MAX : S->refine;
+                for (int ir = 0; ir < nref; ++ir) {
+                    double *kv = wk->Yk, *cr = wk->Yk + n, *cx = wk->Yk + 2 * n;
+#ifdef KMUL_QUAD
+                    kres_q(S, a, wk->th, wk->Dsig, wk->dU, wk->rhs, kv);
+#else
+                    if (hp) {
+                        kres_dd(S, a, wk->th, wk->Dsig, wk->dU, wk->rhs, kv, wk->Xdd);
+                    } else {
+                        kmul(S, a, wk->th, wk->Dsig, wk->dU, kv, cx, ybar, wk->psi, wk->tmp);
+                        for (int c = 0; c < n; ++c) kv[c] = wk->rhs[c] - kv[c];
+                    }
+#endif
+                    ric_solve(S, a, wk->F, kv, cr, cx);
+                    double cn = 0.0, un = 0.0;
+                    for (int c = 0; c < n; ++c) {
+                        wk->dU[c] += cr[c];
+                        cn = fmax(cn, fabs(cr[c]));
+                        un = fmax(un, fabs(wk->dU[c]));
+                    }
+                    if (cn <= 1e-16 * un) break;
+                }
+                if (nref) fwd_sim(S, a, NULL, wk->dU, wk->dX);
+#ifdef RIC_DEBUG
+                {
+                    double* cu = wk->Yk;
+                    memcpy(cu, wk->rhs, sizeof(double) * n);
+                    double de = 0, dn = 0, thm = 0;
+                    if (!chol_bad) {
+                        chol_solve(K, n, cu);
+                        for (int c = 0; c < n; ++c) { de = fmax(de, fabs(cu[c] - wk->dU[c])); dn = fmax(dn, fabs(cu[c])); }
+                    }
+                    for (int r = 0; r < m; ++r) if (wk->act[r]) thm = fmax(thm, wk->th[r]);
+#ifdef RIC_QREF
+                    if (it >= 46) {
+                        double* qu = malloc(sizeof(double) * n);
+                        condensed_q(S, a, wk->th, wk->Dsig, wk->rhs, qu);
+#ifdef USE_QUAD_DIR
+                        memcpy(wk->dU, qu, sizeof(double) * n);
+                        fwd_sim(S, a, NULL, wk->dU, wk->dX);
+#endif
+                        double eq = 0, ec = 0, nq = 0;
+                        for (int c = 0; c < n; ++c) { nq = fmax(nq, fabs(qu[c])); eq = fmax(eq, fabs(qu[c] - wk->dU[c])); if (!chol_bad) ec = fmax(ec, fabs(qu[c] - cu[c])); }
+                        fprintf(stderr, "it %d pass %d vs quad: riccati %.2e condensed %.2e\n", it, pass, eq / nq, ec / nq);
+                        free(qu);
+                    }
+#endif
+                    fprintf(stderr, "it %d pass %d |dU_ric - dU_chol|/|dU| %.2e (chol %s) thmax %.1e\n", it, pass, de / dn, chol_bad ? "FAILED" : "ok", thm);
+                    if (pass == 0) for (int r = 0; r < m; ++r) if (wk->act[r] && wk->th[r] > 1e10) fprintf(stderr, "   row %d (k %d rr %d) th %.1e t %.1e lam %.1e\n", r, r < ms ? r / mc : (r - ms) / (2 * nu), r < ms ? r % mc : (r - ms) % (2 * nu), wk->th[r], t[r], lam[r]);
+                }
+#endif
+            } else {
+                memcpy(wk->dU, wk->rhs, sizeof(double) * n);
+                chol_solve(K, n, wk->dU);
+                fwd_sim(S, a, NULL, wk->dU, wk->dX);
+            }
             for (int r = 0; r < m; ++r) {
                 double g; ROWVAL(wk->dX, wk->dU, (const double*)NULL, r, g);
                 wk->GdU[r] = g;
@@ -520,14 +1375,16 @@ static int solve_one(const shared_t* S, const agent_t* a, double tol, int max_it
     return status;
 }
 
-int cmpc_oracle_solve(int nx, int nu, int N, int ns, int mc, int batch,
-                      const double* Q, const double* R, const double* dR, const double* Qs,
-                      const double* u_ub, const double* u_lb, const int* row_slack, const int* row_sign,
-                      const double* A, const double* Bm, const double* x0, const double* u_prev,
-                      const double* qlin, const double* Crow, const double* hrow,
-                      double tol, int max_iter, int nthreads,
-                      double* z, double* kkt, int* iters, int* status) {
-    shared_t S = {nx, nu, N, ns, mc, Q, R, dR, Qs, u_ub, u_lb, row_slack, row_sign};
+/* newton: 0 condensed Cholesky (default), 1 Riccati, 2 Riccati in Joseph form */
+int cmpc_oracle_solve_ex(int nx, int nu, int N, int ns, int mc, int batch,
+                         const double* Q, const double* R, const double* dR, const double* Qs,
+                         const double* u_ub, const double* u_lb, const int* row_slack, const int* row_sign,
+                         const double* A, const double* Bm, const double* x0, const double* u_prev,
+                         const double* qlin, const double* Crow, const double* hrow,
+                         double tol, int max_iter, int nthreads, int newton, int refine,
+                         double* z, double* kkt, int* iters, int* status) {
+    shared_t S = {nx, nu, N, ns, mc, Q, R, dR, Qs, u_ub, u_lb, row_slack, row_sign, newton, refine};
+    if (newton && (nx + nu > NA_MAX || nu > NU_MAX)) return -1;
     const int n = N * nu, m = N * mc + 2 * nu * N;
     const size_t nz = (size_t)(nx + ns) * (N + 1) + 2 * (size_t)nu * N;
 #ifdef _OPENMP
@@ -538,9 +1395,15 @@ int cmpc_oracle_solve(int nx, int nu, int N, int ns, int mc, int batch,
     int err = 0;
 #pragma omp parallel
     {
-        work_t wk;
-        size_t need = (size_t)n + (size_t)N * ns + (size_t)(N + 1) * nx * n + (size_t)n * n + 4 * (size_t)(N + 1) * nx + 4 * (size_t)n +
-                      4 * (size_t)N * ns + 12 * (size_t)m + 2 * (size_t)nx + (size_t)nx * nx + (size_t)n * 3 + (size_t)nx * n;
+        work_t wk = {0};
+        const size_t nF = (size_t)N * (nu * (nx + nu) + nu * nu);
+#ifdef RIC_DEBUG
+        const size_t nG = (size_t)(N + 1) * nx * n, nK = (size_t)n * n;
+#else
+        const size_t nG = newton ? 0 : (size_t)(N + 1) * nx * n, nK = newton ? 0 : (size_t)n * n;
+#endif
+        size_t need = nF + (size_t)n + (size_t)N * ns + nG + nK + 4 * (size_t)(N + 1) * nx + 4 * (size_t)n +
+                      4 * (size_t)N * ns + 12 * (size_t)m + 2 * (size_t)nx + (size_t)nx * nx + (size_t)n * 3 + (size_t)nx * n + 2 * (size_t)n + (size_t)(N + 1) * nx;
         double* buf = (double*)calloc(need, sizeof(double));
         unsigned char* act = (unsigned char*)calloc(m, 1);
         if (!buf || !act) {
@@ -550,15 +1413,16 @@ int cmpc_oracle_solve(int nx, int nu, int N, int ns, int mc, int batch,
             double* p = buf;
 #define TAKE(f, cnt) do { wk.f = p; p += (cnt); } while (0)
             TAKE(bU, n); TAKE(bsig, N * ns);
-            TAKE(Gam, (size_t)(N + 1) * nx * n); TAKE(K, (size_t)n * n);
+            TAKE(Gam, nG); TAKE(K, nK); TAKE(F, nF);
             TAKE(X, (N + 1) * nx); TAKE(dX, (N + 1) * nx); TAKE(ybar, (N + 1) * nx); TAKE(W, nx * nx);
             TAKE(U, n); TAKE(dU, n); TAKE(gU, n); TAKE(rd, n); TAKE(rhs, n);
             TAKE(sig, N * ns); TAKE(dsig, N * ns); TAKE(Dsig, N * ns); TAKE(rsig, N * ns);
             TAKE(t, m); TAKE(lam, m); TAKE(th, m); TAKE(rho, m); TAKE(rt, m); TAKE(rp, m); TAKE(w, m);
             TAKE(dt_a, m); TAKE(dl_a, m); TAKE(dtv, m); TAKE(dlv, m); TAKE(GdU, m);
-            TAKE(psi, nx); TAKE(tmp, nx); TAKE(Yk, (size_t)nx * n);
+            TAKE(psi, nx); TAKE(tmp, nx); TAKE(Yk, (size_t)nx * n + 2 * (size_t)n + (size_t)(N + 1) * nx);
 #undef TAKE
             wk.act = act;
+            wk.Xdd = (dd_t*)malloc(sizeof(dd_t) * (size_t)(N + 1) * nx);
 #pragma omp for schedule(dynamic, 4)
             for (int b = 0; b < batch; ++b) {
                 agent_t ag = {A + (size_t)b * N * nx * nx, Bm + (size_t)b * N * nx * nu, x0 + (size_t)b * nx,
@@ -567,8 +1431,20 @@ int cmpc_oracle_solve(int nx, int nu, int N, int ns, int mc, int batch,
                 status[b] = solve_one(&S, &ag, tol, max_iter, &wk, z + b * nz, kkt + b, iters + b);
             }
         }
+        if (buf && act) free(wk.Xdd);
         free(buf);
         free(act);
     }
     return err ? -1 : 0;
+}
+
+int cmpc_oracle_solve(int nx, int nu, int N, int ns, int mc, int batch,
+                      const double* Q, const double* R, const double* dR, const double* Qs,
+                      const double* u_ub, const double* u_lb, const int* row_slack, const int* row_sign,
+                      const double* A, const double* Bm, const double* x0, const double* u_prev,
+                      const double* qlin, const double* Crow, const double* hrow,
+                      double tol, int max_iter, int nthreads,
+                      double* z, double* kkt, int* iters, int* status) {
+    return cmpc_oracle_solve_ex(nx, nu, N, ns, mc, batch, Q, R, dR, Qs, u_ub, u_lb, row_slack, row_sign, A, Bm, x0,
+                                u_prev, qlin, Crow, hrow, tol, max_iter, nthreads, 0, 0, z, kkt, iters, status);
 }

@@ -1,5 +1,6 @@
 """ORACLE (test infrastructure only) — ctypes binding of oracle/libcmpc_oracle.so,
 the plain-C condensed IPM restatement (cmpc_oracle.c).
+newton: 0 condensed Cholesky, 1 stage-wise Riccati (as csrc/mpc_riccati.hip), 2 Riccati in Joseph form.
 
 Problems are plain dicts of numpy arrays (batch-major):
   nx nu N ns mc                 ints
@@ -30,6 +31,7 @@ def lib():
             build()
         _LIB = ct.CDLL(path)
         _LIB.cmpc_oracle_solve.restype = ct.c_int
+        _LIB.cmpc_oracle_solve_ex.restype = ct.c_int
     return _LIB
 
 
@@ -47,7 +49,7 @@ def nz_of(p):
     return (p["nx"] + p["ns"]) * (p["N"] + 1) + 2 * p["nu"] * p["N"]
 
 
-def solve_batch(p, tol=1e-9, max_iter=60, nthreads=0):
+def solve_batch(p, tol=1e-9, max_iter=60, nthreads=0, newton=0, refine=0):
     nb = p["A"].shape[0]
     keep = []
     args = []
@@ -61,9 +63,9 @@ def solve_batch(p, tol=1e-9, max_iter=60, nthreads=0):
     kkt = np.zeros(nb)
     iters = np.zeros(nb, np.int32)
     status = np.zeros(nb, np.int32)
-    rc = lib().cmpc_oracle_solve(
+    rc = lib().cmpc_oracle_solve_ex(
         ct.c_int(p["nx"]), ct.c_int(p["nu"]), ct.c_int(p["N"]), ct.c_int(p["ns"]), ct.c_int(p["mc"]),
-        ct.c_int(nb), *args, ct.c_double(tol), ct.c_int(max_iter), ct.c_int(nthreads),
+        ct.c_int(nb), *args, ct.c_double(tol), ct.c_int(max_iter), ct.c_int(nthreads), ct.c_int(newton), ct.c_int(refine),
         z.ctypes.data_as(ct.POINTER(ct.c_double)), kkt.ctypes.data_as(ct.POINTER(ct.c_double)),
         iters.ctypes.data_as(ct.POINTER(ct.c_int)), status.ctypes.data_as(ct.POINTER(ct.c_int)))
     if rc != 0:

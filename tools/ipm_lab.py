@@ -82,6 +82,7 @@ def variant(flags):
     subprocess.run(f"gcc -O2 -fPIC -shared -fopenmp {flags} -o {so} {src} -lm", shell=True, check=True)
     lib = ct.CDLL(so)
     lib.cmpc_oracle_solve.restype = ct.c_int
+    lib.cmpc_oracle_solve_ex.restype = ct.c_int
     return lib
 
 
