@@ -238,7 +238,8 @@ static int lpv_run(cmpc_ctx* ctx, const cmpc_lpv_params* prm, const cmpc_track* 
     HIP_TRY(hipMemsetAsync(err, 0, 4 * B, s));
     cmpc::LpvPtrs lp{in->x_last, in->u_last, in->x_agents, in->pose, A, Bm, p, C, h, out->planes, err};
     HIP_TRY(cmpc::lpv_build_launch(lc, lp, d->batch, s));
-    cmpc::MpcPtrs mp{A, Bm, in->x0, in->u_old, p, C, h, out->z, out->kkt, out->iters, out->status, nullptr, ws};
+    cmpc::MpcPtrs mp{A, Bm, in->x0, in->u_old, p, C, h, out->z, out->kkt, out->iters, out->status,
+                    opts ? (unsigned long long*)opts->stamps : nullptr, ws};  // stamps: device memory
     HIP_TRY(cmpc::mpc_launch(mc, mp, d->batch, s, opts ? opts->flags : 0));
     HIP_TRY(cmpc::lpv_mark_launch(err, out->status, out->z, (int)(12 * (N + 1) + 4 * N), d->batch, s));
     return CMPC_OK;

@@ -32,10 +32,6 @@ namespace {
 
 // Intra-wave LDS ordering: the hardware keeps one wave's LDS operations in order; this
 // only stops the compiler from moving LDS accesses across the hand-off point.
-__device__ __forceinline__ void wsync() {
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-    asm volatile("" ::: "memory");
-}
 
 // PlannerLPV row pattern: row 0 no slack; 1 -> s0 (+); 2,3 -> s1 (+); 4.. -> s2 (-)
 __host__ __device__ constexpr int slk(int r) { return r == 0 ? -1 : (r == 1 ? 0 : (r < 4 ? 1 : 2)); }

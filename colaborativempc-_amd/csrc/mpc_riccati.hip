@@ -41,7 +41,9 @@ namespace {
 constexpr int kMaxNa = CMPC_MAX_NX + CMPC_MAX_NU;
 constexpr int kStageMax = CMPC_MAX_NX * CMPC_MAX_NX + CMPC_MAX_NX * CMPC_MAX_NU + CMPC_MAX_NU * kMaxNa +
                           CMPC_MAX_NU * CMPC_MAX_NU;
-constexpr int kPer = (kStageMax + kWave - 1) / kWave;  // stage-image values per lane
+constexpr int kPerMax = (kStageMax + kWave - 1) / kWave;  // stage-image values per lane (largest dims)
+constexpr int kPerSmall = 2;                               // ... when the stage image fits 128 values
+constexpr int kDepth = 3;  // stage images in flight: a sweep step waits for a load issued 2 steps earlier
 constexpr double kDdTh = 1e10;   // max th above which an iteration runs in double-double
 constexpr int kRefineMax = 6;    // refinement steps of a double-double iteration's direction
 
@@ -52,11 +54,22 @@ struct RLds {
     int sig, dsig, Dsig, rsig;            // per stage slack
     int P, pv, sb, T, G, Hy, Kk, gv, xpp; // Riccati working set
     int Pd, PAd, PBd, Hd, Hyd, Kd, psid;  // double-double working set
+    int stamps;                           // diagnostic clock sums (kStampSlots u64)
+    int cst;                              // copy of MpcConst (weights read from LDS)
     int total;
 };
 
 struct Dims {
     int nx, nu, na, nc, sA, sB, sF, sAB, S;
+};
+
+// Compile-time problem configuration of a kernel instantiation: stage-image values per lane
+// (KP) and, when nonzero, the state / input / rows-per-stage counts.  With the dimensions
+// fixed the stage loops unroll and their independent loads issue together — the sweeps are
+// serial chains of short steps on one wavefront, so latency is all that counts.
+template <int KP_, int NX_, int NU_, int MC_>
+struct Cfg {
+    static constexpr int KP = KP_, NX = NX_, NU = NU_, MC = MC_;
 };
 
 __host__ __device__ inline Dims dims_of(const MpcConst& c) {
@@ -72,6 +85,23 @@ __host__ __device__ inline Dims dims_of(const MpcConst& c) {
     d.S = d.sAB + d.sF;
     return d;
 }
+
+template <class G>
+__device__ __forceinline__ Dims dims_t(const MpcConst& c) {
+    Dims d;
+    d.nx = G::NX ? G::NX : c.nx;
+    d.nu = G::NU ? G::NU : c.nu;
+    d.na = d.nx + d.nu;
+    d.nc = d.na;
+    d.sA = d.nx * d.nx;
+    d.sB = d.nx * d.nu;
+    d.sF = d.nu * d.na + d.nu * d.nu;
+    d.sAB = d.sA + d.sB;
+    d.S = d.sAB + d.sF;
+    return d;
+}
+template <class G>
+__device__ __forceinline__ int mc_t(const MpcConst& c) { return G::MC ? G::MC : c.mc; }
 
 __host__ __device__ inline RLds r_layout(const MpcConst& c) {
     const Dims d = dims_of(c);
@@ -122,6 +152,8 @@ __host__ __device__ inline RLds r_layout(const MpcConst& c) {
     L.Hyd = take(2 * c.nu * d.na);
     L.Kd = take(2 * c.nu * d.na);
     L.psid = take(4 * nx);
+    L.stamps = take(kStampSlots);
+    L.cst = take((int)((sizeof(MpcConst) + 7) / 8));
     L.total = o;
     return L;
 }
@@ -160,10 +192,11 @@ struct StageSrc {
     int sA, sB, sF;
 };
 
-__device__ __forceinline__ void stage_fetch(const StageSrc& s, int k, int cnt, double (&r)[kPer]) {
+template <int KP>
+__device__ __forceinline__ void stage_fetch(const StageSrc& s, int k, int cnt, double (&r)[KP]) {
     const int l = threadIdx.x;
 #pragma unroll
-    for (int q = 0; q < kPer; ++q) {
+    for (int q = 0; q < KP; ++q) {
         const int e = l + q * kWave;
         double v = 0.0;
         if (e < s.sA) v = s.A[(size_t)k * s.sA + e];
@@ -173,18 +206,68 @@ __device__ __forceinline__ void stage_fetch(const StageSrc& s, int k, int cnt, d
     }
 }
 
-__device__ __forceinline__ void stage_put(double* buf, int cnt, const double (&r)[kPer]) {
+template <int KP>
+__device__ __forceinline__ void stage_put(double* buf, int cnt, const double (&r)[KP]) {
     const int l = threadIdx.x;
 #pragma unroll
-    for (int q = 0; q < kPer; ++q) {
+    for (int q = 0; q < KP; ++q) {
         const int e = l + q * kWave;
         if (e < cnt) buf[e] = r[q];
     }
 }
 
+// Stage images of a sweep (forward: k = 0..N-1, backward: k = N-1..0) streamed through the
+// 2-slot LDS buffer sb (stage k in slot k & 1), each fetched into registers kDepth steps
+// before it is stored: the sweep is a serial chain of short steps, so one step cannot hide
+// a global load.  Register sets are indexed statically (sweep() unrolls by kDepth).
+template <int KP>
+struct Pipe {
+    double r[kDepth][KP];
+    const StageSrc src;
+    const int cnt, N, S;
+    const bool back;
+    double* const sb;
+    __device__ Pipe(const StageSrc& s_, int cnt_, int N_, int S_, bool back_, double* sb_)
+        : src(s_), cnt(cnt_), N(N_), S(S_), back(back_), sb(sb_) {}
+    __device__ int stg(int j) const { return back ? N - 1 - j : j; }
+    // fetch the first kDepth stages, store the first; follow with bar()
+    __device__ void prime() {
+        static_for<0, kDepth>([&](auto i) {
+            if (i < N) stage_fetch<KP>(src, stg(i), cnt, r[i]);
+        });
+        stage_put<KP>(sb + (stg(0) & 1) * S, cnt, r[0]);
+        if (kDepth < N) stage_fetch<KP>(src, stg(kDepth), cnt, r[0]);
+    }
+    // after step j: store stage j+1 (register set I = (j+1) % kDepth) into the other slot and
+    // refill the set with stage j+1+kDepth
+    template <int I>
+    __device__ void advance(int j) {
+        if (j + 1 < N) {
+            stage_put<KP>(sb + (stg(j + 1) & 1) * S, cnt, r[I]);
+            if (j + 1 + kDepth < N) stage_fetch<KP>(src, stg(j + 1 + kDepth), cnt, r[I]);
+        }
+    }
+};
+
+// body(k, img) for every stage of the sweep (img: the stage image of k), then bar()
+template <int KP, class Body>
+__device__ __forceinline__ void sweep(Pipe<KP>& p, Body&& body) {
+    for (int j0 = 0; j0 < p.N; j0 += kDepth)
+        static_for<0, kDepth>([&](auto ii) {
+            const int j = j0 + ii;
+            if (j < p.N) {
+                const int k = p.stg(j);
+                body(k, (const double*)(p.sb + (k & 1) * p.S));
+                p.template advance<(ii + 1) % kDepth>(j);
+                wsync();
+            }
+        });
+}
+
 // 2R u_k + 2dR (du_k - du_{k+1}) for condensed variable index cidx (k*nu + i)
+template <class G>
 __device__ __forceinline__ double rdr_grad(const MpcConst& c, const double* U, const double* up, int cidx) {
-    const int nu = c.nu, k = cidx / nu, i = cidx - k * nu;
+    const int nu = G::NU ? G::NU : c.nu, k = cidx / nu, i = cidx - k * nu;
     double v = 0.0;
     for (int j = 0; j < nu; ++j) {
         const double uk = U[k * nu + j];
@@ -196,14 +279,16 @@ __device__ __forceinline__ double rdr_grad(const MpcConst& c, const double* U, c
 }
 
 // Value of row r at (X, U, sig): state rows C_{k,r} . X_{k+1} (+ sign * sig), input rows +-U
+template <class G>
 __device__ __forceinline__ double row_value(const MpcConst& c, const double* __restrict__ C, int r, const double* X,
                                             const double* U, const double* sig) {
+    const int nx = G::NX ? G::NX : c.nx, mc = mc_t<G>(c);
     if (r < c.ms) {
-        const int k = r / c.mc, rr = r - k * c.mc;
-        const double* cr = C + (size_t)r * c.nx;
-        const double* xk = X + (k + 1) * c.nx;
+        const int k = r / mc, rr = r - k * mc;
+        const double* cr = C + (size_t)r * nx;
+        const double* xk = X + (k + 1) * nx;
         double v = 0.0;
-        for (int s = 0; s < c.nx; ++s) v = fma(cr[s], xk[s], v);
+        for (int s = 0; s < nx; ++s) v = fma(cr[s], xk[s], v);
         const int j = c.row_slack[rr];
         if (sig && j >= 0) v += c.row_sign[rr] * sig[k * c.ns + j];
         return v;
@@ -216,11 +301,12 @@ __device__ __forceinline__ double row_value(const MpcConst& c, const double* __r
 // Entry (s,u) of the per-stage constraint curvature M (stable group Schur form; see
 // mpc_ipm.hip m_entry): no-slack rows th c c'; slack group j
 // [q sum_r th_r c_r c_r' + sum_{r<r'} th_r th_r' (a_r - a_r')(a_r - a_r')'] / (q + sum th)
+template <class G>
 __device__ __forceinline__ double m_entry(const MpcConst& c, const double* __restrict__ Ck, const double* th_k,
                                           const double* Dsig_k, int s, int u) {
-    const int nx = c.nx;
+    const int nx = G::NX ? G::NX : c.nx, mc = mc_t<G>(c);
     double v = 0.0;
-    for (int r = 0; r < c.mc; ++r) {
+    for (int r = 0; r < mc; ++r) {
         const double* c1 = Ck + r * nx;
         const double t1 = th_k[r];
         const int j = c.row_slack[r];
@@ -232,7 +318,7 @@ __device__ __forceinline__ double m_entry(const MpcConst& c, const double* __res
         const double q = 2.0 * c.Qs[j];
         double g = q * t1 * c1[s] * c1[u];
         const double s1 = c.row_sign[r];
-        for (int r2 = r + 1; r2 < c.mc; ++r2) {
+        for (int r2 = r + 1; r2 < mc; ++r2) {
             if (c.row_slack[r2] != j) continue;
             const double* c2 = Ck + r2 * nx;
             const double s2 = c.row_sign[r2];
@@ -244,17 +330,15 @@ __device__ __forceinline__ double m_entry(const MpcConst& c, const double* __res
 }
 
 // X_0 = x0 (or 0), X_{k+1} = A_k X_k + B_k U_k  (stage images through sb)
-__device__ void fwd_sim(const MpcConst& c, const Dims& d, const StageSrc& src, double* sb,
+template <class G>
+__device__ __forceinline__ void fwd_sim(const MpcConst& c, const Dims& d, const StageSrc& src, double* sb,
                         const double* __restrict__ x0, const double* U, double* X) {
     const int l = threadIdx.x, nx = d.nx, nu = d.nu, N = c.N;
-    double r[kPer];
-    stage_fetch(src, 0, d.sAB, r);
+    Pipe<G::KP> pp(src, d.sAB, N, d.S, false, sb);
+    pp.prime();
     if (l < nx) X[l] = x0 ? x0[l] : 0.0;
-    stage_put(sb, d.sAB, r);
-    if (N > 1) stage_fetch(src, 1, d.sAB, r);
-    bar();
-    for (int k = 0; k < N; ++k) {
-        const double* Ak = sb + (k & 1) * d.S;
+    wsync();
+    sweep(pp, [&](int k, const double* Ak) {
         const double* Bk = Ak + d.sA;
         if (l < nx) {
             double v = 0.0;
@@ -262,29 +346,22 @@ __device__ void fwd_sim(const MpcConst& c, const Dims& d, const StageSrc& src, d
             for (int i = 0; i < nu; ++i) v = fma(Bk[l * nu + i], U[k * nu + i], v);
             X[(k + 1) * nx + l] = v;
         }
-        if (k + 1 < N) {
-            stage_put(sb + ((k + 1) & 1) * d.S, d.sAB, r);
-            if (k + 2 < N) stage_fetch(src, k + 2, d.sAB, r);
-        }
-        bar();
-    }
+    });
 }
 
 // out_k = B_k' psi_{k+1}, psi_N = yb_N, psi_k = yb_k + A_k' psi_{k+1}   (out: n values)
-__device__ void adjoint(const MpcConst& c, const Dims& d, const StageSrc& src, double* sb, const double* yb,
+template <class G>
+__device__ __forceinline__ void adjoint(const MpcConst& c, const Dims& d, const StageSrc& src, double* sb, const double* yb,
                         double* out, double* psi2) {
     const int l = threadIdx.x, nx = d.nx, nu = d.nu, N = c.N;
-    double* pa = psi2;
-    double* pb = psi2 + nx;
-    double r[kPer];
-    stage_fetch(src, N - 1, d.sAB, r);
-    if (l < nx) pa[l] = yb[N * nx + l];
-    stage_put(sb + ((N - 1) & 1) * d.S, d.sAB, r);
-    if (N > 1) stage_fetch(src, N - 2, d.sAB, r);
-    bar();
-    for (int k = N - 1; k >= 0; --k) {
-        const double* Ak = sb + (k & 1) * d.S;
+    Pipe<G::KP> pp(src, d.sAB, N, d.S, true, sb);
+    pp.prime();
+    if (l < nx) psi2[l] = yb[N * nx + l];
+    wsync();
+    sweep(pp, [&](int k, const double* Ak) {
         const double* Bk = Ak + d.sA;
+        const double* pa = psi2 + ((N - 1 - k) & 1) * nx;
+        double* pb = psi2 + ((N - k) & 1) * nx;
         if (l < nu) {
             double v = 0.0;
             for (int s = 0; s < nx; ++s) v = fma(Bk[s * nu + l], pa[s], v);
@@ -295,57 +372,48 @@ __device__ void adjoint(const MpcConst& c, const Dims& d, const StageSrc& src, d
             for (int s = 0; s < nx; ++s) v = fma(Ak[s * nx + t], pa[s], v);
             pb[t] = v;
         }
-        if (k > 0) {
-            stage_put(sb + ((k - 1) & 1) * d.S, d.sAB, r);
-            if (k > 1) stage_fetch(src, k - 2, d.sAB, r);
-        }
-        bar();
-        double* tq = pa;
-        pa = pb;
-        pb = tq;
-    }
+    });
 }
 
 // W_k = 2Q + M_k of the state X_{k+1} for every block k (global scratch, one pass of all lanes)
-__device__ void stage_weights(const MpcConst& c, const RLds& L, const double* sm, const double* __restrict__ C,
-                              double* __restrict__ Wg) {
-    const int nx = c.nx, nx2 = nx * nx, mc = c.mc, ns = c.ns;
+template <class G>
+__device__ __forceinline__ void stage_weights(const MpcConst& c, const RLds& L, const double* sm,
+                                              const double* __restrict__ C, double* __restrict__ Wg) {
+    const int nx = G::NX ? G::NX : c.nx, nx2 = nx * nx, mc = mc_t<G>(c), ns = c.ns;
     const double* th = sm + L.th;
     const double* Dsig = sm + L.Dsig;
     for (int e = threadIdx.x; e < c.N * nx2; e += kWave) {
         const int k = e / nx2, q = e - k * nx2, i = q / nx, j = q - i * nx;
-        Wg[e] = 2.0 * c.Q[q] + m_entry(c, C + (size_t)k * mc * nx, th + k * mc, Dsig + k * ns, i, j);
+        Wg[e] = 2.0 * c.Q[q] + m_entry<G>(c, C + (size_t)k * mc * nx, th + k * mc, Dsig + k * ns, i, j);
     }
 }
 
 // Riccati factorisation of the Newton system at the current (th, Dsig), with the stage weights
 // Wg of stage_weights: writes the gains K_k = -Hvv^-1 Hvy and Hinv_k = Hvv^-1 of every stage
 // into F.  Returns false on a non-positive pivot (wave-uniform).
-__device__ bool riccati_factor(const MpcConst& c, const Dims& d, const RLds& L, double* sm,
+template <class G>
+__device__ __forceinline__ bool riccati_factor(const MpcConst& c, const Dims& d, const RLds& L, double* sm,
                                const double* __restrict__ A, const double* __restrict__ B,
                                const double* __restrict__ Wg, double* __restrict__ F) {
     const int l = threadIdx.x, nx = d.nx, nu = d.nu, na = d.na, nc = d.nc, N = c.N;
     double* P = sm + L.P;
     double* T = sm + L.T;
-    double* G = sm + L.G;
+    double* Gm = sm + L.G;
     double* Hy = sm + L.Hy;
     double* Kk = sm + L.Kk;
     double* sb = sm + L.sb;
     const double* th = sm + L.th;
     const StageSrc src{A, B, nullptr, d.sA, d.sB, d.sF};
-    double r[kPer];
-    stage_fetch(src, N - 1, d.sAB, r);
+    Pipe<G::KP> pp(src, d.sAB, N, d.S, true, sb);
+    pp.prime();
     // P_N = blkdiag(W_N, 0),  W_N = 2Q + M_N (stage rows of X_N)
     for (int e = l; e < na * na; e += kWave) {
         const int i = e / na, j = e - i * na;
         P[e] = (i < nx && j < nx) ? Wg[(size_t)(N - 1) * nx * nx + i * nx + j] : 0.0;
     }
-    stage_put(sb + ((N - 1) & 1) * d.S, d.sAB, r);
-    if (N > 1) stage_fetch(src, N - 2, d.sAB, r);
-    bar();
+    wsync();
     bool ok = true;
-    for (int k = N - 1; k >= 0; --k) {
-        const double* Ak = sb + (k & 1) * d.S;
+    sweep(pp, [&](int k, const double* Ak) {
         const double* Bk = Ak + d.sA;
         // T = P[:, :nx] [A_k | B_k]   (na x nc);  W_k = 2Q + M_k for the state X_k (k >= 1)
         for (int e = l; e < na * nc; e += kWave) {
@@ -357,7 +425,7 @@ __device__ bool riccati_factor(const MpcConst& c, const Dims& d, const RLds& L, 
                 for (int s = 0; s < nx; ++s) v = fma(P[i * na + s], Bk[s * nu + (j - nx)], v);
             T[e] = v;
         }
-        bar();
+        wsync();
         // G = [A_k | B_k]' T[:nx, :]   (nc x nc, lower triangle)
         for (int e = l; e < nc * nc; e += kWave) {
             const int i = e / nc, j = e - i * nc;
@@ -366,9 +434,9 @@ __device__ bool riccati_factor(const MpcConst& c, const Dims& d, const RLds& L, 
             const int ldi = (i < nx) ? nx : nu;
             double v = 0.0;
             for (int s = 0; s < nx; ++s) v = fma(ci[s * ldi], T[s * nc + j], v);
-            G[e] = v;
+            Gm[e] = v;
         }
-        bar();
+        wsync();
         // Hvv = 2R + 2dR + diag(th_u) + B'Pxx B + Pux B + B'Pxu + Puu  (every lane, nu <= 4),
         // its Cholesky factor and inverse in registers
         double Lf[CMPC_MAX_NU][CMPC_MAX_NU], Hi[CMPC_MAX_NU][CMPC_MAX_NU];
@@ -378,7 +446,7 @@ __device__ bool riccati_factor(const MpcConst& c, const Dims& d, const RLds& L, 
             for (int b = 0; b < CMPC_MAX_NU; ++b) {
                 double v = 0.0;
                 if (a < nu && b <= a) {
-                    v = 2.0 * c.R[a * nu + b] + 2.0 * c.dR[a * nu + b] + G[(nx + a) * nc + nx + b] +
+                    v = 2.0 * c.R[a * nu + b] + 2.0 * c.dR[a * nu + b] + Gm[(nx + a) * nc + nx + b] +
                         T[(nx + a) * nc + nx + b] + T[(nx + b) * nc + nx + a] + P[(nx + a) * na + nx + b];
                     if (a == b) {
                         const int rr = c.ms + 2 * (k * nu + a);
@@ -444,7 +512,7 @@ __device__ bool riccati_factor(const MpcConst& c, const Dims& d, const RLds& L, 
 #pragma unroll
             for (int b = 0; b < CMPC_MAX_NU; ++b) {
                 if (b < nu) {
-                    const double hv = (j < nx) ? G[(nx + b) * nc + j] + T[(nx + b) * nc + j] : -2.0 * c.dR[b * nu + (j - nx)];
+                    const double hv = (j < nx) ? Gm[(nx + b) * nc + j] + T[(nx + b) * nc + j] : -2.0 * c.dR[b * nu + (j - nx)];
                     double hab = 0.0;
 #pragma unroll
                     for (int a2 = 0; a2 < CMPC_MAX_NU; ++a2)
@@ -467,31 +535,26 @@ __device__ bool riccati_factor(const MpcConst& c, const Dims& d, const RLds& L, 
                     if (a2 == a && b2 == b) v = Hi[a2][b2];
             Fk[nu * na + l] = v;
         }
-        if (k > 0) {
-            stage_put(sb + ((k - 1) & 1) * d.S, d.sAB, r);
-            if (k > 1) stage_fetch(src, k - 2, d.sAB, r);
-        }
-        bar();
-        if (k == 0) break;
+        wsync();
         // P_k = blkdiag(W_k + A'Pxx A, 2dR) + Hvy' K_k   (symmetric: lower triangle mirrored)
-        for (int e = l; e < na * na; e += kWave) {
+        for (int e = l; e < na * na && k > 0; e += kWave) {
             const int i = e / na, j = e - i * na;
             if (j > i) continue;
-            double v = (i < nx) ? Wg[(size_t)(k - 1) * nx * nx + i * nx + j] + G[i * nc + j]
+            double v = (i < nx) ? Wg[(size_t)(k - 1) * nx * nx + i * nx + j] + Gm[i * nc + j]
                                 : ((j >= nx) ? 2.0 * c.dR[(i - nx) * nu + (j - nx)] : 0.0);
             for (int a = 0; a < nu; ++a) v = fma(Hy[a * na + i], Kk[a * na + j], v);
             P[i * na + j] = v;
             P[j * na + i] = v;
         }
-        bar();
-    }
+    });
     return ok;
 }
 
 // riccati_factor in double-double (standard form: P_k = blkdiag(W_k + A'Pxx A, 2dR) + Hvy'K_k),
 // for the iterations whose th span defeats fp64 (kDdTh).  The gains are rounded to double
 // into F; the refinement against the double-double residual (kres_dd) absorbs that rounding.
-__device__ __noinline__ bool riccati_factor_dd(const MpcConst& c, const Dims& d, const RLds& L, double* sm,
+template <class G>
+__device__ __forceinline__ bool riccati_factor_dd(const MpcConst& c, const Dims& d, const RLds& L, double* sm,
                                   const double* __restrict__ A, const double* __restrict__ B,
                                   const double* __restrict__ Wg, double* __restrict__ F) {
     const int l = threadIdx.x, nx = d.nx, nu = d.nu, na = d.na, N = c.N;
@@ -504,18 +567,15 @@ __device__ __noinline__ bool riccati_factor_dd(const MpcConst& c, const Dims& d,
     double* sb = sm + L.sb;
     const double* th = sm + L.th;
     const StageSrc src{A, B, nullptr, d.sA, d.sB, d.sF};
-    double r[kPer];
-    stage_fetch(src, N - 1, d.sAB, r);
+    Pipe<G::KP> pp(src, d.sAB, N, d.S, true, sb);
+    pp.prime();
     for (int e = l; e < na * na; e += kWave) {
         const int i = e / na, j = e - i * na;
         st_dd(P, e, dd_of((i < nx && j < nx) ? Wg[(size_t)(N - 1) * nx * nx + i * nx + j] : 0.0));
     }
-    stage_put(sb + ((N - 1) & 1) * d.S, d.sAB, r);
-    if (N > 1) stage_fetch(src, N - 2, d.sAB, r);
-    bar();
+    wsync();
     bool ok = true;
-    for (int k = N - 1; k >= 0; --k) {
-        const double* Ak = sb + (k & 1) * d.S;
+    sweep(pp, [&](int k, const double* Ak) {
         const double* Bk = Ak + d.sA;
         // PA = P[:, :nx] A_k (na x nx);  PB = P [B_k; I] (na x nu)
         for (int e = l; e < na * (nx + nu); e += kWave) {
@@ -531,7 +591,7 @@ __device__ __noinline__ bool riccati_factor_dd(const MpcConst& c, const Dims& d,
                 st_dd(PB, e2, v);
             }
         }
-        bar();
+        wsync();
         // Hvy = [B'PA + PA_u | -2dR] (nu x na);  Hvv = 2R + 2dR + diag(th_u) + B'PB + PB_u (nu x nu)
         for (int e = l; e < nu * na + nu * nu; e += kWave) {
             if (e < nu * na) {
@@ -555,7 +615,7 @@ __device__ __noinline__ bool riccati_factor_dd(const MpcConst& c, const Dims& d,
                 st_dd(H, e2, v);
             }
         }
-        bar();
+        wsync();
         // Cholesky of Hvv and its inverse, in registers (every lane; nu <= 4)
         dd Lf[CMPC_MAX_NU][CMPC_MAX_NU], Hi[CMPC_MAX_NU][CMPC_MAX_NU];
 #pragma unroll
@@ -638,14 +698,9 @@ __device__ __noinline__ bool riccati_factor_dd(const MpcConst& c, const Dims& d,
                     if (a2 == a && b2 == b) v = Hi[a2][b2].hi;
             Fk[nu * na + l] = v;
         }
-        if (k > 0) {
-            stage_put(sb + ((k - 1) & 1) * d.S, d.sAB, r);
-            if (k > 1) stage_fetch(src, k - 2, d.sAB, r);
-        }
-        bar();
-        if (k == 0) break;
-        // P_k = blkdiag(W_k + A'Pxx A, 2dR) + Hvy'K_k  (A_k still in the other half of sb)
-        for (int e = l; e < na * na; e += kWave) {
+        wsync();
+        // P_k = blkdiag(W_k + A'Pxx A, 2dR) + Hvy'K_k
+        for (int e = l; e < na * na && k > 0; e += kWave) {
             const int i = e / na, j = e - i * na;
             if (j > i) continue;
             dd v;
@@ -659,187 +714,193 @@ __device__ __noinline__ bool riccati_factor_dd(const MpcConst& c, const Dims& d,
             st_dd(P, i * na + j, v);
             st_dd(P, j * na + i, v);
         }
-        bar();
-    }
+    });
     return ok;
 }
 
 // Solve the Newton system for the right-hand side rh (n values): dU (n) and, when dX is not
 // null, dX ((N+1) nx, dX_0 = 0), with the gains of riccati_factor.
-__device__ void riccati_solve(const MpcConst& c, const Dims& d, const RLds& L, double* sm,
+template <class G>
+__device__ __forceinline__ void riccati_solve(const MpcConst& c, const Dims& d, const RLds& L, double* sm,
                               const double* __restrict__ A, const double* __restrict__ B,
                               const double* __restrict__ F, const double* rh, double* dU, double* dX) {
     const int l = threadIdx.x, nx = d.nx, nu = d.nu, na = d.na, N = c.N;
     double* sb = sm + L.sb;
     double* pv = sm + L.pv;
-    double* gv = sm + L.gv;
     double* xb = sm + L.xpp;  // dX_k, ping-pong
     const StageSrc src{A, B, F, d.sA, d.sB, d.sF};
-    double r[kPer];
-    // backward: p_N = 0;  gv = -rh_k + B'p_x + p_u;  kk_k = -Hinv gv (into dU);  p_k = [A'p_x; 0] + K' gv
-    stage_fetch(src, N - 1, d.S, r);
-    if (l < na) pv[l] = 0.0;
-    stage_put(sb + ((N - 1) & 1) * d.S, d.S, r);
-    if (N > 1) stage_fetch(src, N - 2, d.S, r);
-    bar();
-    for (int k = N - 1; k >= 0; --k) {
-        const double* Ak = sb + (k & 1) * d.S;
-        const double* Bk = Ak + d.sA;
-        const double* Kg = Bk + d.sB;
-        const double* Hg = Kg + nu * na;
-        const double* pc = pv + ((N - 1 - k) & 1) * na;
-        double* pn = pv + ((N - k) & 1) * na;
-        if (l < nu) {
-            double v = pc[nx + l] - rh[k * nu + l];
-            for (int s = 0; s < nx; ++s) v = fma(Bk[s * nu + l], pc[s], v);
-            gv[l] = v;
-        } else if (l >= 32 && l < 32 + nx) {
-            const int j = l - 32;
-            double v = 0.0;
-            for (int s = 0; s < nx; ++s) v = fma(Ak[s * nx + j], pc[s], v);
-            gv[nu + j] = v;
-        }
-        bar();
-        if (l < nu) {
-            double v = 0.0;
-            for (int b = 0; b < nu; ++b) v = fma(-Hg[l * nu + b], gv[b], v);
-            dU[k * nu + l] = v;
-        } else if (l >= 32 && l < 32 + na) {
-            const int j = l - 32;
-            double v = (j < nx) ? gv[nu + j] : 0.0;
-            for (int a = 0; a < nu; ++a) v = fma(Kg[a * na + j], gv[a], v);
-            pn[j] = v;
-        }
-        if (k > 0) {
-            stage_put(sb + ((k - 1) & 1) * d.S, d.S, r);
-            if (k > 1) stage_fetch(src, k - 2, d.S, r);
-        }
-        bar();
+    // backward: p_N = 0;  g = -rh_k + B'p_x + p_u;  kk_k = -Hinv g (into dU);  p_k = [A'p_x; 0] + K'g.
+    // Every lane forms the nu values of g itself (nu <= 4), so a stage needs one barrier.
+    {
+        Pipe<G::KP> pp(src, d.S, N, d.S, true, sb);
+        pp.prime();
+        if (l < na) pv[l] = 0.0;
+        wsync();
+        sweep(pp, [&](int k, const double* Ak) {
+            const double* Bk = Ak + d.sA;
+            const double* Kg = Bk + d.sB;
+            const double* Hg = Kg + nu * na;
+            const double* pc = pv + ((N - 1 - k) & 1) * na;
+            double* pn = pv + ((N - k) & 1) * na;
+            if (l < na) {
+                double g[CMPC_MAX_NU];
+#pragma unroll
+                for (int a = 0; a < CMPC_MAX_NU; ++a) {
+                    double v = 0.0;
+                    if (a < nu) {
+                        v = pc[nx + a] - rh[k * nu + a];
+                        for (int s2 = 0; s2 < nx; ++s2) v = fma(Bk[s2 * nu + a], pc[s2], v);
+                    }
+                    g[a] = v;
+                }
+                double v = 0.0;
+                if (l < nx)
+                    for (int s2 = 0; s2 < nx; ++s2) v = fma(Ak[s2 * nx + l], pc[s2], v);
+#pragma unroll
+                for (int a = 0; a < CMPC_MAX_NU; ++a)
+                    if (a < nu) v = fma(Kg[a * na + l], g[a], v);
+                pn[l] = v;
+                if (l < nu) {
+                    double u = 0.0;
+#pragma unroll
+                    for (int b = 0; b < CMPC_MAX_NU; ++b)
+                        if (b < nu) u = fma(-Hg[l * nu + b], g[b], u);
+                    dU[k * nu + l] = u;
+                }
+            }
+        });
     }
-    // forward: y_0 = 0;  v_k = kk_k + K_k y_k;  dX_{k+1} = A_k dX_k + B_k v_k
-    stage_fetch(src, 0, d.S, r);
-    if (l < nx) {
-        xb[l] = 0.0;
-        if (dX) dX[l] = 0.0;
-    }
-    stage_put(sb, d.S, r);
-    if (N > 1) stage_fetch(src, 1, d.S, r);
-    bar();
-    for (int k = 0; k < N; ++k) {
-        const double* Ak = sb + (k & 1) * d.S;
-        const double* Bk = Ak + d.sA;
-        const double* Kg = Bk + d.sB;
-        const double* xc = xb + (k & 1) * nx;
-        if (l < nu) {
-            double v = dU[k * nu + l];
-            for (int j = 0; j < nx; ++j) v = fma(Kg[l * na + j], xc[j], v);
-            if (k > 0)
-                for (int b = 0; b < nu; ++b) v = fma(Kg[l * na + nx + b], dU[(k - 1) * nu + b], v);
-            dU[k * nu + l] = v;
-        }
-        bar();
+    // forward: y_0 = 0;  v_k = kk_k + K_k y_k;  dX_{k+1} = A_k dX_k + B_k v_k (every lane < nx forms v_k)
+    {
+        Pipe<G::KP> pp(src, d.S, N, d.S, false, sb);
+        pp.prime();
         if (l < nx) {
-            double v = 0.0;
-            for (int t = 0; t < nx; ++t) v = fma(Ak[l * nx + t], xc[t], v);
-            for (int a = 0; a < nu; ++a) v = fma(Bk[l * nu + a], dU[k * nu + a], v);
-            xb[((k + 1) & 1) * nx + l] = v;
-            if (dX) dX[(k + 1) * nx + l] = v;
+            xb[l] = 0.0;
+            if (dX) dX[l] = 0.0;
         }
-        if (k + 1 < N) {
-            stage_put(sb + ((k + 1) & 1) * d.S, d.S, r);
-            if (k + 2 < N) stage_fetch(src, k + 2, d.S, r);
-        }
-        bar();
+        wsync();
+        sweep(pp, [&](int k, const double* Ak) {
+            const double* Bk = Ak + d.sA;
+            const double* Kg = Bk + d.sB;
+            const double* xc = xb + (k & 1) * nx;
+            if (l < nx || l < nu) {
+                double vk[CMPC_MAX_NU];
+#pragma unroll
+                for (int a = 0; a < CMPC_MAX_NU; ++a) {
+                    double v = 0.0;
+                    if (a < nu) {
+                        v = dU[k * nu + a];
+                        for (int j = 0; j < nx; ++j) v = fma(Kg[a * na + j], xc[j], v);
+                        if (k > 0)
+                            for (int b = 0; b < nu; ++b) v = fma(Kg[a * na + nx + b], dU[(k - 1) * nu + b], v);
+                    }
+                    vk[a] = v;
+                }
+                if (l < nx) {
+                    double v = 0.0;
+                    for (int t = 0; t < nx; ++t) v = fma(Ak[l * nx + t], xc[t], v);
+#pragma unroll
+                    for (int a = 0; a < CMPC_MAX_NU; ++a)
+                        if (a < nu) v = fma(Bk[l * nu + a], vk[a], v);
+                    xb[((k + 1) & 1) * nx + l] = v;
+                    if (dX) dX[(k + 1) * nx + l] = v;
+                }
+                // one wavefront: every lane's reads of dU_k above precede this write-back
+#pragma unroll
+                for (int a = 0; a < CMPC_MAX_NU; ++a)
+                    if (a < nu && l == a) dU[k * nu + a] = vk[a];
+            }
+        });
     }
 }
 
 // out = rhs - K v with the product evaluated in double-double (the refinement residual of a
 // double-double iteration):  K v = sum_k Gamma_k' W_k Gamma_k v + (2R + 2D'dR D + diag(th_u)) v,
 // through the stage recursions (dd states in [yb, yb2), dd adjoint in psid).
-__device__ __noinline__ void kres_dd(const MpcConst& c, const Dims& d, const RLds& L, double* sm, const double* __restrict__ A,
-                        const double* __restrict__ B, const double* __restrict__ Wg, const double* v,
-                        const double* rhs, double* out) {
+template <class G>
+__device__ __forceinline__ void kres_dd(const MpcConst& c, const Dims& d, const RLds& L, double* sm,
+                                        const double* __restrict__ A, const double* __restrict__ B,
+                                        const double* __restrict__ Wg, const double* v, const double* rhs,
+                                        double* out) {
     const int l = threadIdx.x, nx = d.nx, nu = d.nu, N = c.N, nx2 = nx * nx;
     double* Xd = sm + L.yb;
     double* sb = sm + L.sb;
     const double* th = sm + L.th;
-    double* pa = sm + L.psid;
-    double* pb = pa + 2 * nx;
+    double* psid = sm + L.psid;  // two dd vectors of nx, ping-pong
     const StageSrc src{A, B, nullptr, d.sA, d.sB, d.sF};
-    double r[kPer];
     // forward: X_0 = 0, X_{k+1} = A_k X_k + B_k v_k
-    stage_fetch(src, 0, d.sAB, r);
-    if (l < nx) st_dd(Xd, l, dd_of(0.0));
-    stage_put(sb, d.sAB, r);
-    if (N > 1) stage_fetch(src, 1, d.sAB, r);
-    bar();
-    for (int k = 0; k < N; ++k) {
-        const double* Ak = sb + (k & 1) * d.S;
-        const double* Bk = Ak + d.sA;
-        if (l < nx) {
-            dd acc = dd_of(0.0);
-            for (int t = 0; t < nx; ++t) acc = dd_fmad(acc, ld_dd(Xd, k * nx + t), Ak[l * nx + t]);
-            for (int i = 0; i < nu; ++i) acc = dd_fmadd(acc, Bk[l * nu + i], v[k * nu + i]);
-            st_dd(Xd, (k + 1) * nx + l, acc);
-        }
-        if (k + 1 < N) {
-            stage_put(sb + ((k + 1) & 1) * d.S, d.sAB, r);
-            if (k + 2 < N) stage_fetch(src, k + 2, d.sAB, r);
-        }
-        bar();
+    {
+        Pipe<G::KP> pp(src, d.sAB, N, d.S, false, sb);
+        pp.prime();
+        if (l < nx) st_dd(Xd, l, dd_of(0.0));
+        wsync();
+        sweep(pp, [&](int k, const double* Ak) {
+            const double* Bk = Ak + d.sA;
+            if (l < nx) {
+                dd acc = dd_of(0.0);
+                for (int t = 0; t < nx; ++t) acc = dd_fmad(acc, ld_dd(Xd, k * nx + t), Ak[l * nx + t]);
+                for (int i = 0; i < nu; ++i) acc = dd_fmadd(acc, Bk[l * nu + i], v[k * nu + i]);
+                st_dd(Xd, (k + 1) * nx + l, acc);
+            }
+        });
     }
     // adjoint: psi_N = W X_N, psi_k = W X_k + A_k' psi_{k+1};  out_k = rhs_k - B_k' psi_{k+1} - (...)
-    stage_fetch(src, N - 1, d.sAB, r);
-    if (l < nx) {
-        dd acc = dd_of(0.0);
-        for (int u = 0; u < nx; ++u) acc = dd_fmad(acc, ld_dd(Xd, N * nx + u), Wg[(size_t)(N - 1) * nx2 + l * nx + u]);
-        st_dd(pa, l, acc);
-    }
-    stage_put(sb + ((N - 1) & 1) * d.S, d.sAB, r);
-    if (N > 1) stage_fetch(src, N - 2, d.sAB, r);
-    bar();
-    for (int k = N - 1; k >= 0; --k) {
-        const double* Ak = sb + (k & 1) * d.S;
-        const double* Bk = Ak + d.sA;
-        if (l < nu) {
+    {
+        Pipe<G::KP> pp(src, d.sAB, N, d.S, true, sb);
+        pp.prime();
+        if (l < nx) {
             dd acc = dd_of(0.0);
-            for (int s2 = 0; s2 < nx; ++s2) acc = dd_fmad(acc, ld_dd(pa, s2), Bk[s2 * nu + l]);
-            for (int j = 0; j < nu; ++j) {
-                const double vk = v[k * nu + j];
-                const dd dk = dd_ts(vk, k ? -v[(k - 1) * nu + j] : 0.0);
-                const dd dn = (k + 1 < N) ? dd_ts(v[(k + 1) * nu + j], -vk) : dd_of(0.0);
-                acc = dd_fmadd(acc, 2.0 * c.R[l * nu + j], vk);
-                acc = dd_fmad(acc, dd_sub(dk, dn), 2.0 * c.dR[l * nu + j]);
+            for (int u = 0; u < nx; ++u) acc = dd_fmad(acc, ld_dd(Xd, N * nx + u), Wg[(size_t)(N - 1) * nx2 + l * nx + u]);
+            st_dd(psid, l, acc);
+        }
+        wsync();
+        sweep(pp, [&](int k, const double* Ak) {
+            const double* Bk = Ak + d.sA;
+            const double* pa = psid + ((N - 1 - k) & 1) * 2 * nx;
+            double* pb = psid + ((N - k) & 1) * 2 * nx;
+            if (l < nu) {
+                dd acc = dd_of(0.0);
+                for (int s2 = 0; s2 < nx; ++s2) acc = dd_fmad(acc, ld_dd(pa, s2), Bk[s2 * nu + l]);
+                for (int j = 0; j < nu; ++j) {
+                    const double vk = v[k * nu + j];
+                    const dd dk = dd_ts(vk, k ? -v[(k - 1) * nu + j] : 0.0);
+                    const dd dn = (k + 1 < N) ? dd_ts(v[(k + 1) * nu + j], -vk) : dd_of(0.0);
+                    acc = dd_fmadd(acc, 2.0 * c.R[l * nu + j], vk);
+                    acc = dd_fmad(acc, dd_sub(dk, dn), 2.0 * c.dR[l * nu + j]);
+                }
+                const int rr = c.ms + 2 * (k * nu + l);
+                acc = dd_fmad(acc, dd_ts(th[rr], th[rr + 1]), v[k * nu + l]);
+                out[k * nu + l] = dd_sub(dd_of(rhs[k * nu + l]), acc).hi;
+            } else if (k > 0 && l >= 32 && l < 32 + nx) {
+                const int t = l - 32;
+                dd acc = dd_of(0.0);
+                for (int u = 0; u < nx; ++u)
+                    acc = dd_fmad(acc, ld_dd(Xd, k * nx + u), Wg[(size_t)(k - 1) * nx2 + t * nx + u]);
+                for (int s2 = 0; s2 < nx; ++s2) acc = dd_fmad(acc, ld_dd(pa, s2), Ak[s2 * nx + t]);
+                st_dd(pb, t, acc);
             }
-            const int rr = c.ms + 2 * (k * nu + l);
-            acc = dd_fmad(acc, dd_ts(th[rr], th[rr + 1]), v[k * nu + l]);
-            out[k * nu + l] = dd_sub(dd_of(rhs[k * nu + l]), acc).hi;
-        } else if (k > 0 && l >= 32 && l < 32 + nx) {
-            const int t = l - 32;
-            dd acc = dd_of(0.0);
-            for (int u = 0; u < nx; ++u) acc = dd_fmad(acc, ld_dd(Xd, k * nx + u), Wg[(size_t)(k - 1) * nx2 + t * nx + u]);
-            for (int s2 = 0; s2 < nx; ++s2) acc = dd_fmad(acc, ld_dd(pa, s2), Ak[s2 * nx + t]);
-            st_dd(pb, t, acc);
-        }
-        if (k > 0) {
-            stage_put(sb + ((k - 1) & 1) * d.S, d.sAB, r);
-            if (k > 1) stage_fetch(src, k - 2, d.sAB, r);
-        }
-        bar();
-        double* tq = pa;
-        pa = pb;
-        pb = tq;
+        });
     }
 }
 
-__global__ __launch_bounds__(kWave) void mpc_riccati_kernel(const MpcConst c, const MpcPtrs P) {
+template <class G>
+__global__ __launch_bounds__(kWave) void mpc_riccati_kernel(const MpcConst c_arg, const MpcPtrs P) {
     extern __shared__ __attribute__((aligned(16))) double sm[];
     const int b = blockIdx.x;
     const int l = threadIdx.x;
-    const RLds L = r_layout(c);
-    const Dims d = dims_of(c);
+    const RLds L = r_layout(c_arg);
+    // the weights are indexed by lane-dependent expressions: read them from an LDS copy (a
+    // kernel-argument struct indexed that way is materialised in scratch)
+    {
+        const unsigned long long* src = reinterpret_cast<const unsigned long long*>(&c_arg);
+        unsigned long long* dst = reinterpret_cast<unsigned long long*>(sm + L.cst);
+        for (int i = l; i < (int)(sizeof(MpcConst) / 8); i += kWave) dst[i] = src[i];
+        wsync();
+    }
+    const MpcConst& c = *reinterpret_cast<const MpcConst*>(sm + L.cst);
+    const Dims d = dims_t<G>(c);
     const RGlb gl = r_glb(c);
-    const int nx = c.nx, nu = c.nu, N = c.N, ns = c.ns, mc = c.mc, n = c.n, ms = c.ms, m = c.m;
+    const int nx = d.nx, nu = d.nu, N = c.N, ns = c.ns, mc = mc_t<G>(c), n = c.n, ms = c.ms, m = c.m;
 
     const double* __restrict__ A = P.A + (size_t)b * N * nx * nx;
     const double* __restrict__ B = P.B + (size_t)b * N * nx * nu;
@@ -881,8 +942,22 @@ __global__ __launch_bounds__(kWave) void mpc_riccati_kernel(const MpcConst c, co
     double* sb = sm + L.sb;
     const StageSrc sAB{A, B, nullptr, d.sA, d.sB, d.sF};
 
-    for (int i = l; i < L.total; i += kWave) sm[i] = 0.0;
-    bar();
+    for (int i = l; i < L.cst; i += kWave) sm[i] = 0.0;
+    wsync();
+    // diagnostic per-section clock sums (MpcPtrs::stamps; tools/ric_stamps.py):
+    // 0 residuals, 1 stage weights, 2 factor, 3 factor (dd), 4 rhs, 5 solve, 6 refinement,
+    // 7 rows / slacks / step, 8 update, 12 dd iterations, 13 refinement steps, 14 setup + output
+    const bool stamp = P.stamps != nullptr;
+    unsigned long long* tsum = reinterpret_cast<unsigned long long*>(sm + L.stamps);
+    unsigned long long t_a = stamp ? clock64_() : 0, t_b = 0;
+#define RSTAMP(slot)                          \
+    if (stamp) {                              \
+        t_b = clock64_();                     \
+        if (l == 0) tsum[slot] += t_b - t_a;  \
+        t_a = t_b;                            \
+    }
+#define RCOUNT(slot) \
+    if (stamp && l == 0) tsum[slot] += 1;
 
     // ---- row right-hand sides; inactive rows carry w = +inf ----
     for (int r = l; r < m; r += kWave) {
@@ -895,13 +970,13 @@ __global__ __launch_bounds__(kWave) void mpc_riccati_kernel(const MpcConst c, co
         }
         w[r] = isfinite(v) ? v : INFINITY;
     }
-    bar();
-    fwd_sim(c, d, sAB, sb, x0, U, X);
+    wsync();
+    fwd_sim<G>(c, d, sAB, sb, x0, U, X);
 
     double mact_l = 0.0, sp_l = 1.0;
     for (int r = l; r < m; r += kWave) {
         if (isfinite(w[r])) {
-            const double g = row_value(c, C, r, X, U, sig);
+            const double g = row_value<G>(c, C, r, X, U, sig);
             t[r] = fmax(w[r] - g, 1.0);
             lam[r] = 1.0;
             mact_l += 1.0;
@@ -913,11 +988,12 @@ __global__ __launch_bounds__(kWave) void mpc_riccati_kernel(const MpcConst c, co
     }
     const double mact = fmax(wave_sum(mact_l), 1.0);
     const double scale_p = wave_max(sp_l);
-    bar();
+    wsync();
 
     double best_m = INFINITY, best_kkt = INFINITY;
     int best_it = 0, stop = kStopMaxIter, it;
     double kkt = INFINITY;
+    RSTAMP(14);
     for (it = 1; it <= c.max_iter; ++it) {
         // ================= residuals (as mpc_ipm.hip) =================
         for (int i = l; i < (N + 1) * nx; i += kWave) {
@@ -926,11 +1002,11 @@ __global__ __launch_bounds__(kWave) void mpc_riccati_kernel(const MpcConst c, co
             for (int u = 0; u < nx; ++u) v = fma(2.0 * c.Q[s * nx + u], X[k * nx + u], v);
             yb[i] = v;
         }
-        bar();
-        adjoint(c, d, sAB, sb, yb, gU, psi);
+        wsync();
+        adjoint<G>(c, d, sAB, sb, yb, gU, psi);
         double gs_l = 1.0;
         for (int i = l; i < n; i += kWave) {
-            gU[i] += rdr_grad(c, U, up, i);
+            gU[i] += rdr_grad<G>(c, U, up, i);
             gs_l = nmax(gs_l, fabs(gU[i]));
         }
         const double gscale = wave_max(gs_l);
@@ -940,12 +1016,12 @@ __global__ __launch_bounds__(kWave) void mpc_riccati_kernel(const MpcConst c, co
             for (int r = 0; r < mc; ++r) v = fma(lam[k * mc + r], C[((size_t)k * mc + r) * nx + s], v);
             yb[(k + 1) * nx + s] += v;
         }
-        bar();
-        adjoint(c, d, sAB, sb, yb, rd, psi);
+        wsync();
+        adjoint<G>(c, d, sAB, sb, yb, rd, psi);
         double nrd_l = 0.0, nrs_l = 0.0, nrp_l = 0.0, mu_l = 0.0;
         for (int i = l; i < n; i += kWave) {
             const int r = ms + 2 * i;
-            rd[i] += rdr_grad(c, U, up, i) + lam[r] - lam[r + 1];
+            rd[i] += rdr_grad<G>(c, U, up, i) + lam[r] - lam[r + 1];
             nrd_l = nmax(nrd_l, fabs(rd[i]));
         }
         for (int i = l; i < N * ns; i += kWave) {
@@ -958,7 +1034,7 @@ __global__ __launch_bounds__(kWave) void mpc_riccati_kernel(const MpcConst c, co
         }
         for (int r = l; r < m; r += kWave) {
             if (isfinite(w[r])) {
-                const double v = row_value(c, C, r, X, U, sig) + t[r] - w[r];
+                const double v = row_value<G>(c, C, r, X, U, sig) + t[r] - w[r];
                 rp[r] = v;
                 nrp_l = nmax(nrp_l, fabs(v));
                 mu_l += t[r] * lam[r];
@@ -989,11 +1065,12 @@ __global__ __launch_bounds__(kWave) void mpc_riccati_kernel(const MpcConst c, co
             stop = kStopStalled;
             break;
         }
-        bar();
+        wsync();
 
+        RSTAMP(0);
         // ================= Newton system: Riccati factorisation =================
         for (int r = l; r < m; r += kWave) th[r] = isfinite(w[r]) ? lam[r] / t[r] : 0.0;
-        bar();
+        wsync();
         for (int i = l; i < N * ns; i += kWave) {
             const int k = i / ns, j = i - k * ns;
             double v = 2.0 * c.Qs[j];
@@ -1001,16 +1078,22 @@ __global__ __launch_bounds__(kWave) void mpc_riccati_kernel(const MpcConst c, co
                 if (c.row_slack[r] == j) v += th[k * mc + r];
             Dsig[i] = v;
         }
-        bar();
-        stage_weights(c, L, sm, C, Wg);
+        wsync();
+        stage_weights<G>(c, L, sm, C, Wg);
+        gsync();  // W_k: stored by one lane, read by others
         double thm_l = 0.0;
         for (int r = l; r < m; r += kWave) thm_l = fmax(thm_l, th[r]);
         const bool hp = wave_max(thm_l) > kDdTh;  // wave-uniform
-        bar();
-        if (!(hp ? riccati_factor_dd(c, d, L, sm, A, B, Wg, F) : riccati_factor(c, d, L, sm, A, B, Wg, F))) {
+        wsync();
+        RSTAMP(1);
+        const bool fact_ok = hp ? riccati_factor_dd<G>(c, d, L, sm, A, B, Wg, F) : riccati_factor<G>(c, d, L, sm, A, B, Wg, F);
+        gsync();  // gains F: stored by the factor's lanes, read by every lane of the solves
+        if (!fact_ok) {
             stop = kStopBreakdown;
             break;
         }
+        RSTAMP(hp ? 3 : 2);
+        if (hp) RCOUNT(12);
 
         // ================= predictor / corrector =================
         double sig_c = 0.0, alpha = 0.0;
@@ -1024,7 +1107,7 @@ __global__ __launch_bounds__(kWave) void mpc_riccati_kernel(const MpcConst c, co
                 if (pass) rc += sig_c * mu - dta[r] * dla[r];
                 rho[r] = (rc + lam[r] * rp[r]) / t[r];
             }
-            bar();
+            wsync();
             for (int r = l; r < m; r += kWave) {
                 double v = rho[r];
                 if (r < ms) {
@@ -1042,7 +1125,7 @@ __global__ __launch_bounds__(kWave) void mpc_riccati_kernel(const MpcConst c, co
                 }
                 rt[r] = v;
             }
-            bar();
+            wsync();
             for (int i = l; i < (N + 1) * nx; i += kWave) {
                 const int k = i / nx, s = i - k * nx;
                 double v = 0.0;
@@ -1050,17 +1133,19 @@ __global__ __launch_bounds__(kWave) void mpc_riccati_kernel(const MpcConst c, co
                     for (int r = 0; r < mc; ++r) v = fma(rt[(k - 1) * mc + r], C[((size_t)(k - 1) * mc + r) * nx + s], v);
                 yb[i] = v;
             }
-            bar();
-            adjoint(c, d, sAB, sb, yb, rh, psi);
+            wsync();
+            adjoint<G>(c, d, sAB, sb, yb, rh, psi);
             // rhs = -rd - G' rt
             for (int i = l; i < n; i += kWave) rh[i] = -rd[i] - (rh[i] + rt[ms + 2 * i] - rt[ms + 2 * i + 1]);
-            bar();
-            riccati_solve(c, d, L, sm, A, B, F, rh, dU, dX);
+            wsync();
+            RSTAMP(4);
+            riccati_solve<G>(c, d, L, sm, A, B, F, rh, dU, dX);
+            RSTAMP(5);
             if (hp) {
                 // refinement: dU += M^-1 (rhs - K dU), residual in double-double (gU, cr: free here)
                 for (int ir = 0; ir < kRefineMax; ++ir) {
-                    kres_dd(c, d, L, sm, A, B, Wg, dU, rh, gU);
-                    riccati_solve(c, d, L, sm, A, B, F, gU, cr, nullptr);
+                    kres_dd<G>(c, d, L, sm, A, B, Wg, dU, rh, gU);
+                    riccati_solve<G>(c, d, L, sm, A, B, F, gU, cr, nullptr);
                     double cn_l = 0.0, un_l = 0.0;
                     for (int i = l; i < n; i += kWave) {
                         const double u = dU[i] + cr[i];
@@ -1069,13 +1154,15 @@ __global__ __launch_bounds__(kWave) void mpc_riccati_kernel(const MpcConst c, co
                         un_l = fmax(un_l, fabs(u));
                     }
                     const double cn = wave_max(cn_l), un = wave_max(un_l);
-                    bar();
+                    wsync();
+                    RCOUNT(13);
                     if (!(cn > 1e-16 * un)) break;
                 }
-                fwd_sim(c, d, sAB, sb, nullptr, dU, dX);
+                fwd_sim<G>(c, d, sAB, sb, nullptr, dU, dX);
+                RSTAMP(6);
             }
-            for (int r = l; r < m; r += kWave) GdU[r] = row_value(c, C, r, dX, dU, nullptr);
-            bar();
+            for (int r = l; r < m; r += kWave) GdU[r] = row_value<G>(c, C, r, dX, dU, nullptr);
+            wsync();
             for (int i = l; i < N * ns; i += kWave) {
                 const int k = i / ns, j = i - k * ns;
                 double v = rsig[i];
@@ -1086,7 +1173,7 @@ __global__ __launch_bounds__(kWave) void mpc_riccati_kernel(const MpcConst c, co
                     }
                 dsig[i] = -v / Dsig[i];
             }
-            bar();
+            wsync();
             double amax_l = 1.0e300;
             double* dtp = pass ? rho : dta;  // corrector reuses rho/rt storage for (dt, dl)
             double* dlp = pass ? rt : dla;
@@ -1110,7 +1197,7 @@ __global__ __launch_bounds__(kWave) void mpc_riccati_kernel(const MpcConst c, co
                 if (dlv < 0.0) amax_l = fmin(amax_l, -lam[r] / dlv);
             }
             const double amax = fmin(wave_min(amax_l), 1.0e300);
-            bar();
+            wsync();
             if (!pass) {
                 const double a = fmin(amax, 1.0);
                 double mua_l = 0.0;
@@ -1134,6 +1221,7 @@ __global__ __launch_bounds__(kWave) void mpc_riccati_kernel(const MpcConst c, co
                     alpha *= 0.8;
                 }
             }
+            RSTAMP(7);
         }
         // ---- update (corrector direction: dU, dX, dsig, (rho, rt) = (dt, dl)) ----
         for (int i = l; i < n; i += kWave) U[i] = fma(alpha, dU[i], U[i]);
@@ -1144,10 +1232,11 @@ __global__ __launch_bounds__(kWave) void mpc_riccati_kernel(const MpcConst c, co
                 t[r] = fma(alpha, rho[r], t[r]);
                 lam[r] = fma(alpha, rt[r], lam[r]);
             }
-        bar();
+        wsync();
+        RSTAMP(8);
     }
     if (it > c.max_iter) it = c.max_iter;
-    bar();
+    wsync();
     int status = CMPC_SOLVED;
     if (stop != kStopConverged) {
         if (best_it > 0) {  // restore the best iterate
@@ -1157,10 +1246,10 @@ __global__ __launch_bounds__(kWave) void mpc_riccati_kernel(const MpcConst c, co
         }
         status = stop_status(stop, best_m, c.tol);
     }
-    bar();
+    wsync();
 
     // ---- output in the reference layout ----
-    fwd_sim(c, d, sAB, sb, x0, U, X);
+    fwd_sim<G>(c, d, sAB, sb, x0, U, X);
     const int nxe = nx + ns;
     const size_t nz = (size_t)nxe * (N + 1) + 2 * (size_t)n;
     double* z = P.z + (size_t)b * nz;
@@ -1178,6 +1267,13 @@ __global__ __launch_bounds__(kWave) void mpc_riccati_kernel(const MpcConst c, co
         if (P.iters) P.iters[b] = it;
         if (P.status) P.status[b] = status;
     }
+    RSTAMP(14);
+    if (stamp) {
+        wsync();
+        if (l < kStampSlots) P.stamps[(size_t)b * kStampSlots + l] = (l == kStampSlots - 1) ? (unsigned long long)it : tsum[l];
+    }
+#undef RSTAMP
+#undef RCOUNT
 }
 
 }  // namespace
@@ -1190,10 +1286,26 @@ hipError_t mpc_riccati_launch(const MpcConst& c, const MpcPtrs& p, int batch, hi
     if (batch == 0) return hipSuccess;
     if (!p.ws) return hipErrorInvalidValue;
     const size_t lds = mpc_riccati_lds_bytes(c);
-    hipError_t e = hipFuncSetAttribute((const void*)mpc_riccati_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                       (int)lds);
+    const Dims d = dims_of(c);
+    const bool small = d.S <= kPerSmall * kWave;
+    // instantiations: the PlannerLPV agent (nx 9, nu 2, 4 + nb rows per stage), the synthetic
+    // double integrator (nx 4, nu 2), and runtime dimensions
+    auto go = [&](auto g) -> hipError_t {
+        using G = decltype(g);
+        hipError_t e = hipFuncSetAttribute((const void*)mpc_riccati_kernel<G>,
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        if (e != hipSuccess) return e;
+        hipLaunchKernelGGL(mpc_riccati_kernel<G>, dim3(batch), dim3(kWave), lds, s, c, p);
+        return hipSuccess;
+    };
+    hipError_t e;
+    if (c.nx == 9 && c.nu == 2 && c.mc == 5) e = go(Cfg<kPerSmall, 9, 2, 5>{});
+    else if (c.nx == 9 && c.nu == 2 && c.mc == 6) e = go(Cfg<kPerSmall, 9, 2, 6>{});
+    else if (c.nx == 9 && c.nu == 2 && c.mc == 7) e = go(Cfg<kPerSmall, 9, 2, 7>{});
+    else if (c.nx == 4 && c.nu == 2) e = go(Cfg<kPerSmall, 4, 2, 0>{});
+    else if (small) e = go(Cfg<kPerSmall, 0, 0, 0>{});
+    else e = go(Cfg<kPerMax, 0, 0, 0>{});
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(mpc_riccati_kernel, dim3(batch), dim3(kWave), lds, s, c, p);
     return hipGetLastError();
 }
 

@@ -10,6 +10,18 @@ typedef double v4d __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ void bar() { __syncthreads(); }
 
+// One-wavefront workgroups: a wave's LDS operations execute in order, so an LDS hand-off
+// between lanes needs only this compiler fence (no s_barrier, no counter drain — outstanding
+// global prefetches stay in flight).
+__device__ __forceinline__ void wsync() {
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    asm volatile("" ::: "memory");
+}
+
+// ... and a hand-off through global memory (stores by one lane, loads by another) drains the
+// vector-memory counter first.
+__device__ __forceinline__ void gsync() { __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup"); }
+
 // Broadcast lane `lane` (must be wave-uniform) of a double to every lane (two v_readlane_b32).
 __device__ __forceinline__ double readlane_d(double v, int lane) {
     long long i = __double_as_longlong(v);
