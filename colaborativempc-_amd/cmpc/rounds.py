@@ -40,6 +40,13 @@ def exchange_positions(traj_all, traj_local, world=1, group=None):
 
     if traj_all.shape[0] != world * traj_local.shape[0]:
         raise ValueError("traj_all must hold world x local agents")
+    if traj_all.is_cuda and dist.get_backend(group) == "gloo":
+        # gloo moves host memory only: stage through the host (multi-process runs sharing one
+        # GPU, or hosts without RCCL); the gathered rows are the same bytes in the same order
+        host = traj_all.new_empty(traj_all.shape, device="cpu")
+        dist.all_gather_into_tensor(host, traj_local.detach().cpu().contiguous(), group=group)
+        traj_all.copy_(host)
+        return
     dist.all_gather_into_tensor(traj_all, traj_local.contiguous(), group=group)
 
 

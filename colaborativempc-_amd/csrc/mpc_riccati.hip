@@ -188,7 +188,7 @@ __host__ __device__ inline RGlb r_glb(const MpcConst& c) {
 struct StageSrc {
     const double* A;
     const double* B;
-    const double* F;
+    const double* F;  // gains K_k | Hinv_k (solve sweeps)
     int sA, sB, sF;
 };
 
@@ -382,9 +382,55 @@ __device__ __forceinline__ void stage_weights(const MpcConst& c, const RLds& L, 
     const int nx = G::NX ? G::NX : c.nx, nx2 = nx * nx, mc = mc_t<G>(c), ns = c.ns;
     const double* th = sm + L.th;
     const double* Dsig = sm + L.Dsig;
-    for (int e = threadIdx.x; e < c.N * nx2; e += kWave) {
-        const int k = e / nx2, q = e - k * nx2, i = q / nx, j = q - i * nx;
-        Wg[e] = 2.0 * c.Q[q] + m_entry<G>(c, C + (size_t)k * mc * nx, th + k * mc, Dsig + k * ns, i, j);
+    if constexpr (G::NX != 0 && G::MC != 0) {
+        // one lane per row (k, i) of W_k: the stage's constraint rows are read once per row
+        // and every load of an item issues together (same grouping as m_entry)
+        constexpr int NX = G::NX, MC = G::MC;
+        for (int e = threadIdx.x; e < c.N * NX; e += kWave) {
+            const int k = e / NX, i = e - k * NX;
+            const double* Ck = C + (size_t)k * MC * NX;
+            const double* thk = th + k * MC;
+            double w[NX];
+#pragma unroll
+            for (int u = 0; u < NX; ++u) w[u] = 0.0;
+            // rows streamed one (or one pair) at a time: few registers live across the loop;
+            // the sums round exactly like m_entry's (2Q added last)
+#pragma unroll
+            for (int r = 0; r < MC; ++r) {
+                const double* c1 = Ck + r * NX;
+                const double t1 = thk[r], ci1 = c1[i];
+                const int j = c.row_slack[r];
+                if (j < 0) {
+#pragma unroll
+                    for (int u = 0; u < NX; ++u) w[u] = fma(t1 * ci1, c1[u], w[u]);
+                    continue;
+                }
+                const double inv = 1.0 / Dsig[k * ns + j];
+                const double q = 2.0 * c.Qs[j];
+                const double s1 = c.row_sign[r];
+                double g[NX];
+#pragma unroll
+                for (int u = 0; u < NX; ++u) g[u] = q * t1 * ci1 * c1[u];
+#pragma unroll
+                for (int r2 = r + 1; r2 < MC; ++r2) {
+                    if (c.row_slack[r2] != j) continue;
+                    const double* c2 = Ck + r2 * NX;
+                    const double s2 = c.row_sign[r2];
+                    const double a2 = t1 * thk[r2] * (s1 * ci1 - s2 * c2[i]);
+#pragma unroll
+                    for (int u = 0; u < NX; ++u) g[u] += a2 * (s1 * c1[u] - s2 * c2[u]);
+                }
+#pragma unroll
+                for (int u = 0; u < NX; ++u) w[u] = fma(g[u], inv, w[u]);
+            }
+#pragma unroll
+            for (int u = 0; u < NX; ++u) Wg[(size_t)k * NX * NX + i * NX + u] = 2.0 * c.Q[i * NX + u] + w[u];
+        }
+    } else {
+        for (int e = threadIdx.x; e < c.N * nx2; e += kWave) {
+            const int k = e / nx2, q = e - k * nx2, i = q / nx, j = q - i * nx;
+            Wg[e] = 2.0 * c.Q[q] + m_entry<G>(c, C + (size_t)k * mc * nx, th + k * mc, Dsig + k * ns, i, j);
+        }
     }
 }
 
@@ -415,7 +461,14 @@ __device__ __forceinline__ bool riccati_factor(const MpcConst& c, const Dims& d,
     bool ok = true;
     sweep(pp, [&](int k, const double* Ak) {
         const double* Bk = Ak + d.sA;
-        // T = P[:, :nx] [A_k | B_k]   (na x nc);  W_k = 2Q + M_k for the state X_k (k >= 1)
+        // this lane's entries of W_{k-1} for the P_k update at the end of the stage: load now
+        double wk[(CMPC_MAX_NX + CMPC_MAX_NU) * (CMPC_MAX_NX + CMPC_MAX_NU) / kWave + 1];
+#pragma unroll
+        for (int q = 0; q < (int)(sizeof(wk) / sizeof(double)); ++q) {
+            const int e = l + q * kWave, i = e / na, j = e - i * na;
+            wk[q] = (k > 0 && e < na * na && i < nx && j <= i) ? Wg[(size_t)(k - 1) * nx * nx + i * nx + j] : 0.0;
+        }
+        // T = P[:, :nx] [A_k | B_k]   (na x nc)
         for (int e = l; e < na * nc; e += kWave) {
             const int i = e / nc, j = e - i * nc;
             double v = 0.0;
@@ -537,10 +590,11 @@ __device__ __forceinline__ bool riccati_factor(const MpcConst& c, const Dims& d,
         }
         wsync();
         // P_k = blkdiag(W_k + A'Pxx A, 2dR) + Hvy' K_k   (symmetric: lower triangle mirrored)
-        for (int e = l; e < na * na && k > 0; e += kWave) {
-            const int i = e / na, j = e - i * na;
-            if (j > i) continue;
-            double v = (i < nx) ? Wg[(size_t)(k - 1) * nx * nx + i * nx + j] + Gm[i * nc + j]
+#pragma unroll
+        for (int q = 0; q < (int)(sizeof(wk) / sizeof(double)); ++q) {
+            const int e = l + q * kWave, i = e / na, j = e - i * na;
+            if (!(k > 0 && e < na * na) || j > i) continue;
+            double v = (i < nx) ? wk[q] + Gm[i * nc + j]
                                 : ((j >= nx) ? 2.0 * c.dR[(i - nx) * nu + (j - nx)] : 0.0);
             for (int a = 0; a < nu; ++a) v = fma(Hy[a * na + i], Kk[a * na + j], v);
             P[i * na + j] = v;

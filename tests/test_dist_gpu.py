@@ -1,0 +1,60 @@
+"""cfg4 on the HIP path: 4096 agents in two ranks of 2048 (BASELINE.json configs[3]'s
+sharding, one process per rank), the real device-resident rounds (cmpc.rounds.DIRounds: HIP
+build / solve / advance) and the per-round all-gather of predicted positions.  On a one-GPU box
+both ranks share device 0 and the exchange runs over gloo with a host staging copy (RCCL
+refuses two ranks on one device); the collective's semantics are the same.
+
+Jacobi semantics of planner/scripts/LPV_HP_N_main.py:96-117: every rank must end every round
+holding exactly the node-global trajectories of a single-process run (bit-equal), and the
+solved agent-QPs must match the C restatement (oracle/cmpc_oracle.c)."""
+import os
+import socket
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+N_AGENTS, HORIZON, ROUNDS, SAMPLE = 4096, 30, 3, 256
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def test_two_rank_hip_rounds_match_single_process(tmp_path, gpu_ctx):
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    from dist_rounds import run
+    from oracle import cmpc_oracle as CO
+
+    port = _free_port()
+    procs = []
+    for r in range(2):
+        env = dict(os.environ, RANK=str(r), WORLD_SIZE="2", LOCAL_RANK="0", MASTER_ADDR="127.0.0.1",
+                   MASTER_PORT=str(port), CMPC_DIST_BACKEND="gloo")
+        procs.append(subprocess.Popen([sys.executable, os.path.join(ROOT, "tools", "dist_rounds.py"),
+                                       str(tmp_path / f"rank{r}.npz"), str(N_AGENTS), str(HORIZON), str(ROUNDS),
+                                       str(SAMPLE)], env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT))
+    ref, prob, z0 = run(N_AGENTS, HORIZON, ROUNDS, SAMPLE)   # single process, while the ranks run
+    for p in procs:
+        out, _ = p.communicate(timeout=240)
+        assert p.returncode == 0, out.decode()[-3000:]
+    for r in range(2):
+        d = np.load(tmp_path / f"rank{r}.npz")
+        assert d["trajs"].shape == ref.shape
+        assert np.array_equal(d["trajs"], ref), f"rank {r}: rounds differ from the single-process run"
+        # a sample of this rank's round-0 agent-QPs against the C restatement
+        P = {k[2:]: d[k] for k in d.files if k.startswith("p_")}
+        for k in ("nx", "nu", "N", "ns", "mc"):
+            P[k] = int(P[k])
+        zc, _, _, stc = CO.solve_batch(P, nthreads=8)
+        assert np.isin(stc, (1, 2)).all()
+        assert np.abs(d["z0"] - zc).max() < 1e-6
+    # the single-process sample is rank 0's first agents: same problems, same solution bits
+    d0 = np.load(tmp_path / "rank0.npz")
+    assert np.array_equal(d0["z0"], z0)
