@@ -155,7 +155,13 @@ SIGNATURES = {
     "cmpc_ocd_converged_dev": (ct.c_int, [ct.c_void_p, ct.c_int, ct.c_int, ct.c_double, ct.c_double, _DP, _DP, _IP,
                                           ct.c_void_p]),
     "cmpc_selftest_mfma": (ct.c_int, [ct.c_void_p, _DP, _DP, _DP]),
+    "cmpc_comm_id": (ct.c_int, [ct.c_char_p]),
+    "cmpc_comm_init": (ct.c_int, [ct.c_void_p, ct.c_int, ct.c_int, ct.c_char_p]),
+    "cmpc_allgather_trajectories": (ct.c_int, [ct.c_void_p, _DP, _DP, ct.c_ulonglong, ct.c_void_p]),
+    "cmpc_comm_destroy": (ct.c_int, [ct.c_void_p]),
 }
+
+CMPC_COMM_ID_BYTES = 128
 
 
 def load():

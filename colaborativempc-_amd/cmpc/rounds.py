@@ -27,12 +27,15 @@ from . import _lib as L
 from .solver import _dims, _tptr, _weights, nz_of
 
 
-def exchange_positions(traj_all, traj_local, world=1, group=None):
+def exchange_positions(traj_all, traj_local, world=1, group=None, comm=None):
     """The per-round exchange of predicted positions (the np.swapaxes "exchange" of
     LPV_HP_N_main.py:117, and the ROS topic publish/subscribe of LPV_ROS_main.py:66-77):
     every rank's contiguous block `traj_local` (B, N+1, 2) is gathered, in rank order,
     into the node-global `traj_all` (world*B, N+1, 2).  One all-gather per round;
     over RCCL/xGMI with the "nccl" backend, gloo on CPU tensors."""
+    if comm is not None:   # libcmpc's own RCCL communicator (cmpc.comm.Comm), no torch.distributed
+        comm.allgather(traj_local, traj_all)
+        return
     if world == 1:
         traj_all.copy_(traj_local)
         return
@@ -52,11 +55,11 @@ def exchange_positions(traj_all, traj_local, world=1, group=None):
 
 class DIRounds:
     def __init__(self, scen, rank=0, world=1, device=None, ctx=None, tol=None, max_iter=None, group=None,
-                 fp32=False):
+                 fp32=False, comm=None):
         import torch
 
         self.torch = torch
-        self.scen, self.rank, self.world, self.group = scen, rank, world, group
+        self.scen, self.rank, self.world, self.group, self.comm = scen, rank, world, group, comm
         if scen.n_agents % world:
             raise ValueError("n_agents must be divisible by the number of ranks")
         self.dev = torch.device("cuda", torch.cuda.current_device() if device is None else device)
@@ -130,7 +133,7 @@ class DIRounds:
                                                         _tptr(self.traj_local), self._stream()))
 
     def exchange(self):
-        exchange_positions(self.traj_all, self.traj_local, self.world, self.group)
+        exchange_positions(self.traj_all, self.traj_local, self.world, self.group, self.comm)
 
     def step(self, timer=None):
         """One consensus round.  `timer` (start, stop) events bracket the solve launch."""

@@ -6,6 +6,8 @@
 #include <cstring>
 #include <string>
 
+#include <rccl/rccl.h>
+
 #include "internal.h"
 
 struct cmpc_ctx {
@@ -13,6 +15,7 @@ struct cmpc_ctx {
     hipStream_t stream = nullptr;  // private stream for the host-pointer entry points
     char* ws = nullptr;            // device arena
     size_t ws_bytes = 0;
+    ncclComm_t comm = nullptr;     // RCCL communicator of cmpc_comm_init (multi-GPU exchange)
     std::string err;
 };
 
@@ -144,9 +147,58 @@ int cmpc_destroy(cmpc_ctx* ctx) {
     if (!ctx) return CMPC_OK;
     (void)hipSetDevice(ctx->device);
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+    if (ctx->comm) (void)ncclCommDestroy(ctx->comm);
     if (ctx->ws) (void)hipFree(ctx->ws);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     delete ctx;
+    return CMPC_OK;
+}
+
+// ---- multi-GPU exchange over RCCL (cmpc.h) ----
+static_assert(sizeof(ncclUniqueId) == CMPC_COMM_ID_BYTES, "ncclUniqueId size");
+
+int cmpc_comm_id(unsigned char id[CMPC_COMM_ID_BYTES]) {
+    if (!id) return CMPC_ERR_ARG;
+    ncclUniqueId u;
+    if (ncclGetUniqueId(&u) != ncclSuccess) return CMPC_ERR_DEVICE;
+    std::memcpy(id, &u, sizeof u);
+    return CMPC_OK;
+}
+
+int cmpc_comm_init(cmpc_ctx* ctx, int nranks, int rank, const unsigned char id[CMPC_COMM_ID_BYTES]) {
+    if (!ctx || !id || nranks < 1 || rank < 0 || rank >= nranks) return fail(ctx, CMPC_ERR_ARG, "bad communicator arguments");
+    if (ctx->comm) return fail(ctx, CMPC_ERR_ARG, "context already joined a communicator");
+    int rc = set_device(ctx);
+    if (rc != CMPC_OK) return rc;
+    ncclUniqueId u;
+    std::memcpy(&u, id, sizeof u);
+    const ncclResult_t r = ncclCommInitRank(&ctx->comm, nranks, u, rank);
+    if (r != ncclSuccess) {
+        ctx->comm = nullptr;
+        return fail(ctx, CMPC_ERR_DEVICE, std::string("ncclCommInitRank: ") + ncclGetErrorString(r));
+    }
+    return CMPC_OK;
+}
+
+int cmpc_allgather_trajectories(cmpc_ctx* ctx, const double* traj_local, double* traj_all, unsigned long long count,
+                                void* stream) {
+    if (!ctx) return CMPC_ERR_ARG;
+    if (!ctx->comm) return fail(ctx, CMPC_ERR_ARG, "cmpc_comm_init has not been called on this context");
+    if (count && (!traj_local || !traj_all)) return fail(ctx, CMPC_ERR_ARG, "null trajectory buffer");
+    int rc = set_device(ctx);
+    if (rc != CMPC_OK) return rc;
+    const ncclResult_t r = ncclAllGather(traj_local, traj_all, (size_t)count, ncclDouble, ctx->comm, (hipStream_t)stream);
+    if (r != ncclSuccess) return fail(ctx, CMPC_ERR_DEVICE, std::string("ncclAllGather: ") + ncclGetErrorString(r));
+    return CMPC_OK;
+}
+
+int cmpc_comm_destroy(cmpc_ctx* ctx) {
+    if (!ctx) return CMPC_ERR_ARG;
+    if (ctx->comm) {
+        (void)set_device(ctx);
+        (void)ncclCommDestroy(ctx->comm);
+        ctx->comm = nullptr;
+    }
     return CMPC_OK;
 }
 

@@ -461,13 +461,6 @@ __device__ __forceinline__ bool riccati_factor(const MpcConst& c, const Dims& d,
     bool ok = true;
     sweep(pp, [&](int k, const double* Ak) {
         const double* Bk = Ak + d.sA;
-        // this lane's entries of W_{k-1} for the P_k update at the end of the stage: load now
-        double wk[(CMPC_MAX_NX + CMPC_MAX_NU) * (CMPC_MAX_NX + CMPC_MAX_NU) / kWave + 1];
-#pragma unroll
-        for (int q = 0; q < (int)(sizeof(wk) / sizeof(double)); ++q) {
-            const int e = l + q * kWave, i = e / na, j = e - i * na;
-            wk[q] = (k > 0 && e < na * na && i < nx && j <= i) ? Wg[(size_t)(k - 1) * nx * nx + i * nx + j] : 0.0;
-        }
         // T = P[:, :nx] [A_k | B_k]   (na x nc)
         for (int e = l; e < na * nc; e += kWave) {
             const int i = e / nc, j = e - i * nc;
@@ -590,11 +583,10 @@ __device__ __forceinline__ bool riccati_factor(const MpcConst& c, const Dims& d,
         }
         wsync();
         // P_k = blkdiag(W_k + A'Pxx A, 2dR) + Hvy' K_k   (symmetric: lower triangle mirrored)
-#pragma unroll
-        for (int q = 0; q < (int)(sizeof(wk) / sizeof(double)); ++q) {
-            const int e = l + q * kWave, i = e / na, j = e - i * na;
-            if (!(k > 0 && e < na * na) || j > i) continue;
-            double v = (i < nx) ? wk[q] + Gm[i * nc + j]
+        for (int e = l; e < na * na && k > 0; e += kWave) {
+            const int i = e / na, j = e - i * na;
+            if (j > i) continue;
+            double v = (i < nx) ? Wg[(size_t)(k - 1) * nx * nx + i * nx + j] + Gm[i * nc + j]
                                 : ((j >= nx) ? 2.0 * c.dR[(i - nx) * nu + (j - nx)] : 0.0);
             for (int a = 0; a < nu; ++a) v = fma(Hy[a * na + i], Kk[a * na + j], v);
             P[i * na + j] = v;

@@ -15,9 +15,9 @@
  *   quadprog(H,f,A,b,Aeq,beq,lb,ub) reached through       cmpc_solve_qp_batch (dense
  *     YALMIP callquadprog.m:63-69                         standard form, quadprog semantics)
  *     (Matlab-tests/yalmip/.../solvers/callquadprog.m)
- *   ROS topic exchange of predicted trajectories          caller-side RCCL all-gather (see
- *     (ROS/src/planner_experiments/src/LPV_ROS_main.py     INTEGRATION.md); the solver reads
- *     :66-77,124-150) / LPV_HP_N_main.py:117              neighbour rows from device memory
+ *   ROS topic exchange of predicted trajectories          cmpc_allgather_trajectories (RCCL
+ *     (ROS/src/planner_experiments/src/LPV_ROS_main.py     all-gather, cmpc_comm_*); the solver
+ *     :66-77,124-150) / LPV_HP_N_main.py:117              reads neighbour rows from device memory
  *
  * Conventions
  *  - All floating point is IEEE fp64, row-major, batch-major (agent b's block is
@@ -294,6 +294,29 @@ int cmpc_ocd_update_dev(cmpc_ctx* ctx, const cmpc_ocd_dims* dims, double alpha, 
                         const double* traj_all, double* lam, void* hip_stream);
 int cmpc_ocd_converged_dev(cmpc_ctx* ctx, int batch, int per, double atol, double rtol, const double* x_old,
                            const double* x_pred, int* close, void* hip_stream);
+
+/* ----------------------------------------------------------------------
+ * Multi-GPU exchange (RCCL over xGMI).  One process per GPU, one
+ * context per process.  Replaces the per-round exchange of predicted trajectories —
+ * the ROS topics of ROS/src/planner_experiments/src/LPV_ROS_main.py:66-77 (publish)
+ * and :124-150 (subscribe), the in-process np.swapaxes of LPV_HP_N_main.py:117 —
+ * for hosts that shard agents without torch (a MATLAB / C host).
+ *
+ *   cmpc_comm_id:   rank 0 creates the communicator id; the host hands its
+ *                   CMPC_COMM_ID_BYTES bytes to every rank (MPI, a file, a socket).
+ *   cmpc_comm_init: every rank joins (collective; blocks until all ranks joined).
+ *   cmpc_allgather_trajectories: traj_all (nranks*count doubles, DEVICE) receives every
+ *                   rank's traj_local (count doubles, DEVICE) in rank order; stream-ordered
+ *                   (hip_stream as void*, 0 = default).  For the position exchange of a
+ *                   round, count = local agents * (N+1) * 2.
+ *   cmpc_comm_destroy: leaves the communicator (cmpc_destroy does it too).
+ * ---------------------------------------------------------------------- */
+#define CMPC_COMM_ID_BYTES 128
+int cmpc_comm_id(unsigned char id[CMPC_COMM_ID_BYTES]);
+int cmpc_comm_init(cmpc_ctx* ctx, int nranks, int rank, const unsigned char id[CMPC_COMM_ID_BYTES]);
+int cmpc_allgather_trajectories(cmpc_ctx* ctx, const double* traj_local, double* traj_all, unsigned long long count,
+                                void* hip_stream);
+int cmpc_comm_destroy(cmpc_ctx* ctx);
 
 /* Device self-test of the f64 MFMA fragment mapping used by the solver
  * (D = A*B for one 16x16x4 tile, A,B host 16x4 / 4x16 row-major, D host 16x16). */

@@ -18,6 +18,11 @@ def lib():
         m = ct.CDLL(MOCK)
         m.mock_array.restype = ct.c_void_p
         m.mock_array.argtypes = [ct.c_int, ct.POINTER(ct.c_long), ct.POINTER(ct.c_double)]
+        m.mock_sparse.restype = ct.c_void_p
+        m.mock_sparse.argtypes = [ct.c_long, ct.c_long, ct.c_long, ct.POINTER(ct.c_double), ct.POINTER(ct.c_long),
+                                  ct.POINTER(ct.c_long)]
+        m.mock_struct.restype = ct.c_void_p
+        m.mock_struct.argtypes = [ct.c_int, ct.POINTER(ct.c_char_p), ct.POINTER(ct.c_void_p)]
         m.mock_struct2.restype = ct.c_void_p
         m.mock_struct2.argtypes = [ct.c_char_p, ct.c_void_p, ct.c_char_p, ct.c_void_p]
         m.mock_call.restype = ct.c_int
@@ -48,6 +53,39 @@ def mx(a):
     dims = (ct.c_long * a.ndim)(*a.shape)
     buf = np.asfortranarray(a).ravel(order="F")
     return m.mock_array(a.ndim, dims, buf.ctypes.data_as(ct.POINTER(ct.c_double)))
+
+
+def mx_sparse(a):
+    """scipy sparse / dense 2-D -> mock sparse mxArray (CSC, as MATLAB stores it)."""
+    import scipy.sparse as sp
+
+    m = lib()
+    c = sp.csc_matrix(a)
+    c.sort_indices()
+    pr = np.ascontiguousarray(c.data, dtype=np.float64)
+    ir = np.ascontiguousarray(c.indices, dtype=np.int64)
+    jc = np.ascontiguousarray(c.indptr, dtype=np.int64)
+    return m.mock_sparse(c.shape[0], c.shape[1], c.nnz, pr.ctypes.data_as(ct.POINTER(ct.c_double)),
+                         ir.ctypes.data_as(ct.POINTER(ct.c_long)), jc.ctypes.data_as(ct.POINTER(ct.c_long)))
+
+
+def mx_struct(fields):
+    """dict name -> numpy array (or an mxArray pointer from mx/mx_sparse) -> 1 x 1 struct."""
+    m = lib()
+    names = (ct.c_char_p * len(fields))(*[k.encode() for k in fields])
+    vals = (ct.c_void_p * len(fields))(*[v if isinstance(v, int) else mx(v) for v in fields.values()])
+    return m.mock_struct(len(fields), names, vals)
+
+
+def call_raw(ps, nlhs):
+    """mexFunction on prepared mxArray pointers -> (outputs | None, (err_id, err_msg) | None)."""
+    m = lib()
+    prhs = (ct.c_void_p * len(ps))(*ps)
+    plhs = (ct.c_void_p * nlhs)()
+    rc = m.mock_call(nlhs, plhs, len(ps), prhs)
+    if rc:
+        return None, (m.mock_err_id().decode(), m.mock_err_msg().decode())
+    return list(plhs), None
 
 
 def values(p):

@@ -1,11 +1,12 @@
 /* TEST INFRASTRUCTURE: a minimal stand-in for MATLAB's mex.h / matrix.h, enough to compile
  * and exercise colaborativempc-_amd/mex/cmpc_quadprog_mex.c without MATLAB (there is none
- * in this image).  Doubles only, column-major, struct arrays of one element. */
+ * in this image).  Doubles only (full or sparse CSC), column-major, struct arrays of one element. */
 #ifndef CMPC_MEX_MOCK_H
 #define CMPC_MEX_MOCK_H
 #include <stddef.h>
 
 typedef size_t mwSize;
+typedef size_t mwIndex;
 typedef enum { mxDOUBLE_CLASS = 6, mxSTRUCT_CLASS = 2, mxCHAR_CLASS = 4 } mxClassID;
 typedef enum { mxREAL = 0, mxCOMPLEX = 1 } mxComplexity;
 typedef struct mxArray_tag mxArray;
@@ -19,6 +20,9 @@ double* mxGetPr(const mxArray* a);
 int mxIsDouble(const mxArray* a);
 int mxIsComplex(const mxArray* a);
 int mxIsSparse(const mxArray* a);
+mwIndex* mxGetIr(const mxArray* a);
+mwIndex* mxGetJc(const mxArray* a);
+int mxGetNumberOfFields(const mxArray* a);
 int mxIsEmpty(const mxArray* a);
 int mxIsStruct(const mxArray* a);
 double mxGetScalar(const mxArray* a);

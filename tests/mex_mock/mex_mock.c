@@ -9,7 +9,7 @@
 
 #include "mex.h"
 
-#define MAXF 8
+#define MAXF 32
 struct mxArray_tag {
     mxClassID cls;
     mwSize nd;
@@ -19,6 +19,8 @@ struct mxArray_tag {
     char names[MAXF][32];
     mxArray* fields[MAXF];
     char* str;
+    int sparse;          /* CSC: pr holds the nonzeros, ir their rows, jc the column starts */
+    mwIndex *ir, *jc;
 };
 
 static jmp_buf g_jmp;
@@ -41,7 +43,10 @@ size_t mxGetN(const mxArray* a) {
 double* mxGetPr(const mxArray* a) { return a->pr; }
 int mxIsDouble(const mxArray* a) { return a->cls == mxDOUBLE_CLASS; }
 int mxIsComplex(const mxArray* a) { (void)a; return 0; }
-int mxIsSparse(const mxArray* a) { (void)a; return 0; }
+int mxIsSparse(const mxArray* a) { return a->sparse; }
+mwIndex* mxGetIr(const mxArray* a) { return a->ir; }
+mwIndex* mxGetJc(const mxArray* a) { return a->jc; }
+int mxGetNumberOfFields(const mxArray* a) { return a->nfields; }
 int mxIsEmpty(const mxArray* a) { return mxGetNumberOfElements(a) == 0; }
 int mxIsStruct(const mxArray* a) { return a->cls == mxSTRUCT_CLASS; }
 double mxGetScalar(const mxArray* a) { return a->pr && mxGetNumberOfElements(a) ? a->pr[0] : 0.0; }
@@ -118,6 +123,30 @@ mxArray* mock_array(int nd, const long* dims, const double* data) {
     size_t k = mxGetNumberOfElements(a);
     if (data && k) memcpy(a->pr, data, k * sizeof(double));
     return a;
+}
+/* m x n sparse double in CSC form (nnz values, their row indices, n+1 column starts) */
+mxArray* mock_sparse(long m, long n, long nnz, const double* pr, const long* ir, const long* jc) {
+    mxArray* a = (mxArray*)calloc(1, sizeof(mxArray));
+    a->cls = mxDOUBLE_CLASS;
+    a->nd = 2;
+    a->dims[0] = (mwSize)m;
+    a->dims[1] = (mwSize)n;
+    a->sparse = 1;
+    a->pr = (double*)calloc(nnz ? nnz : 1, sizeof(double));
+    a->ir = (mwIndex*)calloc(nnz ? nnz : 1, sizeof(mwIndex));
+    a->jc = (mwIndex*)calloc(n + 1, sizeof(mwIndex));
+    for (long k = 0; k < nnz; ++k) {
+        a->pr[k] = pr[k];
+        a->ir[k] = (mwIndex)ir[k];
+    }
+    for (long j = 0; j <= n; ++j) a->jc[j] = (mwIndex)jc[j];
+    return a;
+}
+/* 1 x 1 struct with nf fields */
+mxArray* mock_struct(int nf, const char** names, mxArray** vals) {
+    mxArray* s = mxCreateStructMatrix(1, 1, nf, names);
+    for (int k = 0; k < nf; ++k) mxSetField(s, 0, names[k], vals[k]);
+    return s;
 }
 mxArray* mock_struct2(const char* n1, mxArray* v1, const char* n2, mxArray* v2) {
     const char* names[2] = {n1, n2};

@@ -58,3 +58,36 @@ def test_two_rank_hip_rounds_match_single_process(tmp_path, gpu_ctx):
     # the single-process sample is rank 0's first agents: same problems, same solution bits
     d0 = np.load(tmp_path / "rank0.npz")
     assert np.array_equal(d0["z0"], z0)
+
+
+def test_c_abi_rccl_allgather_single_rank(gpu_ctx):
+    """cmpc_comm_init / cmpc_allgather_trajectories (the C-ABI exchange a MATLAB / C host uses
+    instead of torch.distributed), one rank: the gather is the identity, and rounds driven
+    through it equal the default rounds bit for bit."""
+    import torch
+
+    import cmpc
+    from cmpc import scenarios as S
+    from cmpc.comm import Comm
+    from cmpc.rounds import DIRounds
+
+    comm = Comm(gpu_ctx, 1, 0, Comm.new_id())
+    try:
+        loc = torch.randn(64, 31, 2, dtype=torch.float64, device="cuda")
+        out = torch.zeros_like(loc)
+        comm.allgather(loc, out)
+        torch.cuda.synchronize()
+        assert torch.equal(out, loc)
+        with pytest.raises(ValueError):
+            comm.allgather(loc, torch.zeros(65, 31, 2, dtype=torch.float64, device="cuda"))
+        sc = S.make_di(256, 30, 2, 2)
+        a, b = DIRounds(sc, ctx=gpu_ctx), DIRounds(sc, ctx=gpu_ctx, comm=comm)
+        for _ in range(2):
+            a.step()
+            b.step()
+        torch.cuda.synchronize()
+        assert torch.equal(a.traj_all, b.traj_all) and torch.equal(a.z, b.z)
+    finally:
+        comm.close()
+    with pytest.raises(cmpc.CmpcError):   # left the communicator: the exchange refuses to run
+        gpu_ctx.check(gpu_ctx.lib.cmpc_allgather_trajectories(gpu_ctx.h, None, None, 0, None))
