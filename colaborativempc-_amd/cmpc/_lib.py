@@ -86,6 +86,10 @@ class cmpc_lpv_out(ct.Structure):
     _fields_ = [("z", _DP), ("planes", _DP), ("kkt", _DP), ("iters", _IP), ("status", _IP)]
 
 
+class cmpc_lpv_build_out(ct.Structure):
+    _fields_ = [("A", _DP), ("B", _DP), ("qlin", _DP), ("C", _DP), ("h", _DP), ("planes", _DP), ("err", _IP)]
+
+
 class cmpc_di_params(ct.Structure):
     _fields_ = [("dim", ct.c_int)] + [(k, ct.c_double) for k in ("v_ref", "q_v", "q_lane", "hw", "min_vel",
                                                                  "max_vel", "min_dist", "wq")]
@@ -155,6 +159,9 @@ SIGNATURES = {
     "cmpc_ocd_converged_dev": (ct.c_int, [ct.c_void_p, ct.c_int, ct.c_int, ct.c_double, ct.c_double, _DP, _DP, _IP,
                                           ct.c_void_p]),
     "cmpc_selftest_mfma": (ct.c_int, [ct.c_void_p, _DP, _DP, _DP]),
+    "cmpc_lpv_build_dev": (ct.c_int, [ct.c_void_p, ct.POINTER(cmpc_lpv_params), ct.POINTER(cmpc_track),
+                                      ct.POINTER(cmpc_lpv_dims), ct.POINTER(cmpc_lpv_data),
+                                      ct.POINTER(cmpc_lpv_build_out), ct.c_void_p]),
     "cmpc_comm_id": (ct.c_int, [ct.c_char_p]),
     "cmpc_comm_init": (ct.c_int, [ct.c_void_p, ct.c_int, ct.c_int, ct.c_char_p]),
     "cmpc_allgather_trajectories": (ct.c_int, [ct.c_void_p, _DP, _DP, ct.c_ulonglong, ct.c_void_p]),

@@ -104,6 +104,40 @@ class PlannerLPVBatch:
         return dict(z=z, planes=planes, kkt=kkt, iters=iters, status=status)
 
 
+    def build(self, x_last, u_last, x_agents, pose):
+        """The builder alone on the GPU (cmpc_lpv_build_dev): the structured agent-QP the solve
+        runs on.  Returns host arrays dict(A, B, qlin, C, h, planes, err)."""
+        import torch
+
+        x_last, u_last, pose = L.f64(x_last), L.f64(u_last), L.f64(pose)
+        B = x_last.shape[0]
+        N = self.N
+        nb = 0 if x_agents is None else np.shape(x_agents)[2]
+        dev = torch.device("cuda", self.ctx.device)
+        T = lambda a: torch.as_tensor(a, device=dev)   # noqa: E731
+        ins = dict(x_last=T(x_last), u_last=T(u_last), pose=T(pose),
+                   x_agents=None if x_agents is None else T(L.f64(x_agents)))
+        mc = 4 + nb
+        outs = dict(A=torch.empty((B, N, 9, 9), dtype=torch.float64, device=dev),
+                    B=torch.empty((B, N, 9, 2), dtype=torch.float64, device=dev),
+                    qlin=torch.empty((B, N + 1, 9), dtype=torch.float64, device=dev),
+                    C=torch.empty((B, N, mc, 9), dtype=torch.float64, device=dev),
+                    h=torch.empty((B, N, mc), dtype=torch.float64, device=dev),
+                    planes=torch.zeros((B, N, 3, max(nb, 1)), dtype=torch.float64, device=dev),
+                    err=torch.empty(B, dtype=torch.int32, device=dev))
+        dp = lambda t: None if t is None else ct.cast(t.data_ptr(), L._DP)   # noqa: E731
+        dims = L.cmpc_lpv_dims(B, N, nb, x_last.shape[1])
+        data = L.cmpc_lpv_data(None, dp(ins["x_last"]), dp(ins["u_last"]), None, dp(ins["x_agents"]), dp(ins["pose"]))
+        o = L.cmpc_lpv_build_out(*[dp(outs[k]) for k in ("A", "B", "qlin", "C", "h")],
+                                 dp(outs["planes"]) if nb else None, ct.cast(outs["err"].data_ptr(), L._IP))
+        s = torch.cuda.current_stream(dev)
+        self.ctx.check(self.ctx.lib.cmpc_lpv_build_dev(self.ctx.h, ct.byref(self.prm), ct.byref(self.track),
+                                                       ct.byref(dims), ct.byref(data), ct.byref(o),
+                                                       ct.c_void_p(s.cuda_stream)))
+        torch.cuda.synchronize(dev)
+        return {k: v.cpu().numpy() for k, v in outs.items()}
+
+
 def unpack(z, N):
     """Solution unpacking of LPV_Planner.py:164-178 (xPred, uPred, duPred, sPred, raw_States).
 

@@ -312,6 +312,23 @@ int cmpc_solve_lpv_batch_dev(cmpc_ctx* ctx, const cmpc_lpv_params* prm, const cm
     return lpv_run(ctx, prm, tr, d, in, out, opts, (hipStream_t)stream, cv);
 }
 
+int cmpc_lpv_build_dev(cmpc_ctx* ctx, const cmpc_lpv_params* prm, const cmpc_track* tr, const cmpc_lpv_dims* d,
+                       const cmpc_lpv_data* in, const cmpc_lpv_build_out* out, void* stream) {
+    if (!ctx || !in || !out || !d) return fail(ctx, CMPC_ERR_ARG, "null argument");
+    if (!out->A || !out->B || !out->qlin || !out->C || !out->h || !out->err)
+        return fail(ctx, CMPC_ERR_ARG, "null builder output");
+    int rc = set_device(ctx);
+    if (rc != CMPC_OK) return rc;
+    cmpc::LpvConst lc;
+    if ((rc = build_lpv_const(ctx, prm, tr, d, &lc)) != CMPC_OK) return rc;
+    hipStream_t s = (hipStream_t)stream;
+    HIP_TRY(hipMemsetAsync(out->err, 0, 4 * (size_t)d->batch, s));
+    cmpc::LpvPtrs lp{in->x_last, in->u_last, in->x_agents, in->pose, out->A, out->B, out->qlin, out->C, out->h,
+                     out->planes, out->err};
+    HIP_TRY(cmpc::lpv_build_launch(lc, lp, d->batch, s));
+    return CMPC_OK;
+}
+
 int cmpc_solve_lpv_batch(cmpc_ctx* ctx, const cmpc_lpv_params* prm, const cmpc_track* tr, const cmpc_lpv_dims* d,
                          const cmpc_lpv_data* in, const cmpc_lpv_out* out, const cmpc_opts* opts) {
     if (!ctx) return CMPC_ERR_ARG;

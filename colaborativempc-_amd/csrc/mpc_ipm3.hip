@@ -1034,9 +1034,11 @@ static hipError_t launch3_t(const MpcConst& c, const MpcPtrs& p, int batch, hipS
 #if CMPC_V3_SET == 1
 bool mpc3_try_set2(const MpcConst& c, const MpcPtrs& p, int batch, hipStream_t s, hipError_t* err, int nb);
 bool mpc3_try_set3(const MpcConst& c, const MpcPtrs& p, int batch, hipStream_t s, hipError_t* err, int nb);
+bool mpc3_try_set4(const MpcConst& c, const MpcPtrs& p, int batch, hipStream_t s, hipError_t* err, int nb);
 
 // Returns true (and launches) when a v3 instantiation covers the problem: PlannerLPV row
-// pattern with nb <= 2 neighbour rows, N <= 32, N*nu <= 64; (nx, nu) in {(4,2), (9,2), (6,3)}.
+// pattern with nb <= 2 neighbour rows (nb = 3 at nx = 9: the reference's 4-agent case),
+// N <= 32, N*nu <= 64; (nx, nu) in {(4,2), (9,2), (6,3)}.
 bool mpc3_try_launch(const MpcConst& c, const MpcPtrs& p, int batch, hipStream_t s, hipError_t* err) {
     if (c.ns != 3 || c.N > 32 || c.mc < 4 || c.n > 64) return false;
     for (int r = 0; r < c.mc; ++r)
@@ -1045,7 +1047,8 @@ bool mpc3_try_launch(const MpcConst& c, const MpcPtrs& p, int batch, hipStream_t
     CASE(4, 2, 2)
     CASE(4, 2, 1)
     CASE(4, 2, 0)
-    return mpc3_try_set2(c, p, batch, s, err, nb) || mpc3_try_set3(c, p, batch, s, err, nb);
+    return mpc3_try_set2(c, p, batch, s, err, nb) || mpc3_try_set3(c, p, batch, s, err, nb) ||
+           mpc3_try_set4(c, p, batch, s, err, nb);
 }
 #elif CMPC_V3_SET == 2
 bool mpc3_try_set2(const MpcConst& c, const MpcPtrs& p, int batch, hipStream_t s, hipError_t* err, int nb) {
@@ -1054,9 +1057,14 @@ bool mpc3_try_set2(const MpcConst& c, const MpcPtrs& p, int batch, hipStream_t s
     CASE(9, 2, 0)
     return false;
 }
-#else
+#elif CMPC_V3_SET == 3
 bool mpc3_try_set3(const MpcConst& c, const MpcPtrs& p, int batch, hipStream_t s, hipError_t* err, int nb) {
     CASE(6, 3, 2)
+    return false;
+}
+#else
+bool mpc3_try_set4(const MpcConst& c, const MpcPtrs& p, int batch, hipStream_t s, hipError_t* err, int nb) {
+    CASE(9, 2, 3)
     return false;
 }
 #endif

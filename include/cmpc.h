@@ -199,6 +199,24 @@ int cmpc_solve_lpv_batch_dev(cmpc_ctx* ctx, const cmpc_lpv_params* prm, const cm
                              const cmpc_lpv_dims* dims, const cmpc_lpv_data* dev_in,
                              const cmpc_lpv_out* dev_out, const cmpc_opts* opts, void* hip_stream);
 
+/* The LPV builder alone, DEVICE pointers: the structured agent-QP that
+ * cmpc_solve_lpv_batch_dev hands its solver, for hosts that inspect or extend it before
+ * cmpc_solve_mpc_batch_dev.  _EstimateABC (LPV_Planner.py:477-591: A_k = I + dt A_c, B_k = dt B_c
+ * at the scheduling point of Last_xPredicted row k and uPred row k, curvature / half-width by
+ * track-segment lookup misc.py:78-126), compute_hyperplane (compute_plane.py:41-68) and
+ * compute_weights (misc.py:10-18) feed the rows (:251-380) and the linear cost (:382-427):
+ *   A batch x N x 9 x 9, B batch x N x 9 x 2, qlin batch x (N+1) x 9, C batch x N x (4+nb) x 9,
+ *   h batch x N x (4+nb), planes batch x N x 3 x nb (may be NULL), err batch (1: s of the
+ *   previous prediction lies on no track segment — the reference raises there, misc.py:97). */
+typedef struct {
+    double *A, *B, *qlin, *C, *h, *planes;
+    int* err;
+} cmpc_lpv_build_out;
+
+int cmpc_lpv_build_dev(cmpc_ctx* ctx, const cmpc_lpv_params* prm, const cmpc_track* track,
+                       const cmpc_lpv_dims* dims, const cmpc_lpv_data* dev_in, const cmpc_lpv_build_out* dev_out,
+                       void* hip_stream);
+
 /* ------------------------------------------------------------------------
  * Synthetic agent family of BASELINE.json configs 1-5 (no reference counterpart:
  * the reference's model is the 9-state LPV bicycle; BASELINE fixes a double

@@ -36,6 +36,7 @@ typedef struct {
 
 typedef struct {
     const double *A, *B, *x0, *up, *p, *C, *h;
+    const double* U0; /* optional starting inputs (warm start), NULL: U = 0 */
 } agent_t;
 
 #define IDX2(i, j, ld) ((size_t)(i) * (ld) + (j))
@@ -919,7 +920,7 @@ static int solve_one(const shared_t* S, const agent_t* a, double tol, int max_it
     for (int r = 0; r < m; ++r) mact += wk->act[r];
 
     double *U = wk->U, *sig = wk->sig, *X = wk->X, *t = wk->t, *lam = wk->lam;
-    memset(U, 0, sizeof(double) * n);
+    if (a->U0) memcpy(U, a->U0, sizeof(double) * n); else memset(U, 0, sizeof(double) * n);
     memset(sig, 0, sizeof(double) * N * ns);
     fwd_sim(S, a, a->x0, U, X);
 
@@ -961,7 +962,11 @@ static int solve_one(const shared_t* S, const agent_t* a, double tol, int max_it
         if (!wk->act[r]) { t[r] = 1.0; lam[r] = 0.0; continue; }
         double g; ROWVAL(X, U, sig, r, g);
         double s0 = wk->w[r] - g;
+#ifdef T0_FLOOR
+        t[r] = s0 > T0_FLOOR ? s0 : T0_FLOOR;
+#else
         t[r] = s0 > 1.0 ? s0 : 1.0;
+#endif
         lam[r] = 1.0;
 #ifdef SIGMA_START
         if (r < ms) {
@@ -1381,7 +1386,7 @@ int cmpc_oracle_solve_ex(int nx, int nu, int N, int ns, int mc, int batch,
                          const double* u_ub, const double* u_lb, const int* row_slack, const int* row_sign,
                          const double* A, const double* Bm, const double* x0, const double* u_prev,
                          const double* qlin, const double* Crow, const double* hrow,
-                         double tol, int max_iter, int nthreads, int newton, int refine,
+                         double tol, int max_iter, int nthreads, int newton, int refine, const double* U0,
                          double* z, double* kkt, int* iters, int* status) {
     shared_t S = {nx, nu, N, ns, mc, Q, R, dR, Qs, u_ub, u_lb, row_slack, row_sign, newton, refine};
     if (newton && (nx + nu > NA_MAX || nu > NU_MAX)) return -1;
@@ -1427,7 +1432,7 @@ int cmpc_oracle_solve_ex(int nx, int nu, int N, int ns, int mc, int batch,
             for (int b = 0; b < batch; ++b) {
                 agent_t ag = {A + (size_t)b * N * nx * nx, Bm + (size_t)b * N * nx * nu, x0 + (size_t)b * nx,
                               u_prev + (size_t)b * nu, qlin + (size_t)b * (N + 1) * nx,
-                              Crow + (size_t)b * N * mc * nx, hrow + (size_t)b * N * mc};
+                              Crow + (size_t)b * N * mc * nx, hrow + (size_t)b * N * mc, U0 ? U0 + (size_t)b * n : NULL};
                 status[b] = solve_one(&S, &ag, tol, max_iter, &wk, z + b * nz, kkt + b, iters + b);
             }
         }
@@ -1446,5 +1451,5 @@ int cmpc_oracle_solve(int nx, int nu, int N, int ns, int mc, int batch,
                       double tol, int max_iter, int nthreads,
                       double* z, double* kkt, int* iters, int* status) {
     return cmpc_oracle_solve_ex(nx, nu, N, ns, mc, batch, Q, R, dR, Qs, u_ub, u_lb, row_slack, row_sign, A, Bm, x0,
-                                u_prev, qlin, Crow, hrow, tol, max_iter, nthreads, 0, 0, z, kkt, iters, status);
+                                u_prev, qlin, Crow, hrow, tol, max_iter, nthreads, 0, 0, NULL, z, kkt, iters, status);
 }

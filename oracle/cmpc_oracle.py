@@ -49,7 +49,7 @@ def nz_of(p):
     return (p["nx"] + p["ns"]) * (p["N"] + 1) + 2 * p["nu"] * p["N"]
 
 
-def solve_batch(p, tol=1e-9, max_iter=60, nthreads=0, newton=0, refine=0):
+def solve_batch(p, tol=1e-9, max_iter=60, nthreads=0, newton=0, refine=0, U0=None):
     nb = p["A"].shape[0]
     keep = []
     args = []
@@ -59,6 +59,9 @@ def solve_batch(p, tol=1e-9, max_iter=60, nthreads=0, newton=0, refine=0):
         a, ptr = _i(p[k]); keep.append(a); args.append(ptr)
     for k in ("A", "B", "x0", "u_prev", "qlin", "C", "h"):
         a, ptr = _d(p[k]); keep.append(a); args.append(ptr)
+    if U0 is not None:
+        U0 = np.ascontiguousarray(U0, dtype=np.float64)
+        keep.append(U0)
     z = np.zeros((nb, nz_of(p)))
     kkt = np.zeros(nb)
     iters = np.zeros(nb, np.int32)
@@ -66,6 +69,7 @@ def solve_batch(p, tol=1e-9, max_iter=60, nthreads=0, newton=0, refine=0):
     rc = lib().cmpc_oracle_solve_ex(
         ct.c_int(p["nx"]), ct.c_int(p["nu"]), ct.c_int(p["N"]), ct.c_int(p["ns"]), ct.c_int(p["mc"]),
         ct.c_int(nb), *args, ct.c_double(tol), ct.c_int(max_iter), ct.c_int(nthreads), ct.c_int(newton), ct.c_int(refine),
+        None if U0 is None else _d(U0)[1],
         z.ctypes.data_as(ct.POINTER(ct.c_double)), kkt.ctypes.data_as(ct.POINTER(ct.c_double)),
         iters.ctypes.data_as(ct.POINTER(ct.c_int)), status.ctypes.data_as(ct.POINTER(ct.c_int)))
     if rc != 0:
