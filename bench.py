@@ -34,12 +34,20 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--agents", type=int, default=1024, help="agents per GPU")
-    ap.add_argument("--horizon", type=int, default=30)
+    ap.add_argument("--config", choices=["cfg3", "cfg5"], default="cfg3",
+                    help="cfg3 (the metric's config, default) or cfg5: 8192 agents/GPU, N=50, 3-D double "
+                         "integrator (nx=6, nu=3) on the fp64 stage-wise Riccati kernel")
+    ap.add_argument("--agents", type=int, default=None, help="agents per GPU (default: the config's)")
+    ap.add_argument("--horizon", type=int, default=None)
     ap.add_argument("--nb", type=int, default=2)
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="target CPU-baseline sample time")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-ref", action="store_true", help="skip the reference-configuration (N=125) line")
     args = ap.parse_args()
+    cfg5 = args.config == "cfg5"
+    args.agents = args.agents or (8192 if cfg5 else 1024)
+    args.horizon = args.horizon or (50 if cfg5 else 30)
+    dim = 3 if cfg5 else 2
 
     import torch
     import torch.distributed as dist
@@ -59,7 +67,7 @@ def main():
     from cmpc.rounds import DIRounds
 
     n_total = args.agents * world
-    scen = S.make_di(n_total, args.horizon, args.nb, 2)
+    scen = S.make_di(n_total, args.horizon, args.nb, dim)
     ctx = cmpc.Context(local)
     R = DIRounds(scen, rank=rank, world=world, device=local, ctx=ctx)
 
@@ -105,7 +113,7 @@ def main():
     sh = scen.shared
     nx, nu, N, mc = sh["nx"], sh["nu"], sh["N"], sh["mc"]
     m_rows = N * mc + 2 * nu * N
-    flops = S.alg_flops(nx, nu, N, m_rows, mean_iters)
+    flops = S.riccati_flops(nx, nu, N, mean_iters) if cfg5 else S.alg_flops(nx, nu, N, m_rows, mean_iters)
     achieved_tf = flops * args.agents / (kern_ms * 1e-3) / 1e12
     alg_bytes = S.di_alg_bytes(nx, nu, N, args.nb)
     traffic, traffic_src = pmc_traffic()
@@ -114,6 +122,9 @@ def main():
     max_err = None
     if rank == 0 and world == 1 and not args.no_cpu:
         cpu, max_err = cpu_baseline(R, args.cpu_seconds)
+    ref_line = None
+    if rank == 0 and world == 1 and not args.no_ref and not cfg5:
+        ref_line = reference_config(ctx)
 
     if rank == 0:
         out = {
@@ -130,8 +141,11 @@ def main():
             "dtype": "f64",
             "data": "synthetic (seeded double-integrator agent population, SURVEY.md §8d)",
             "config": {
-                "workload": f"cfg3: {args.agents} agents/GPU, N={N}, 2-D double integrator nx={nx} nu={nu}, "
-                            f"nb={args.nb}, fp64 condensed IPM; step = build+solve+advance+all-gather",
+                "workload": (f"cfg5: {args.agents} agents/GPU, N={N}, 3-D double integrator nx={nx} nu={nu}, "
+                             f"nb={args.nb}, fp64 stage-wise Riccati IPM (BASELINE asks fp32; fp64 >= it); "
+                             f"step = build+solve+advance+all-gather") if cfg5 else
+                            (f"cfg3: {args.agents} agents/GPU, N={N}, 2-D double integrator nx={nx} nu={nu}, "
+                             f"nb={args.nb}, fp64 condensed IPM; step = build+solve+advance+all-gather"),
                 "agents_total": n_total, "horizon": N, "nx": nx, "nu": nu, "neighbours": args.nb,
                 "parallelism": f"agents sharded over {world} GPU(s), RCCL all-gather per round",
             },
@@ -141,14 +155,14 @@ def main():
             "mean_ipm_iters": mean_iters,
             "max_abs_err_vs_cpu": max_err,
             "roofline": {
-                "kernel": "mpc_ipm3_kernel<4,4,2,2>",
+                "kernel": "mpc_riccati_kernel<Cfg<2,6,3,6>>" if cfg5 else "mpc_ipm3_kernel<4,4,2,2>",
                 "bound": "mfma",
                 "achieved": achieved_tf,
                 "peak": FP64_PEAK_TFLOPS,
                 "unit": "TFLOP/s",
                 "frac": achieved_tf / FP64_PEAK_TFLOPS,
-                "traffic": traffic,
-                "traffic_source": traffic_src,
+                "traffic": None if cfg5 else traffic,
+                "traffic_source": None if cfg5 else traffic_src,
                 "kernel_ms_per_launch": kern_ms,
                 "alg_flops_per_qp": flops,
                 "alg_bytes_per_qp": alg_bytes,
@@ -156,10 +170,56 @@ def main():
                 "hbm_frac": alg_bytes * args.agents / (kern_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
             },
             "cpu_baseline": cpu,
+            "reference_config": ref_line,
         }
         print(json.dumps(out))
     if world > 1:
         dist.destroy_process_group()
+
+
+def reference_config(ctx, reps=10):
+    """The reference's own shipped configuration, timed beside its recorded number: N = 125,
+    3 agents on the Highway map (planner/scripts/config_files/config_LPV.py:13-24), through the
+    PlannerLPV drop-in (host arrays in and out, LPV scheduling + planes + QP build + the
+    stage-wise Riccati IPM on the GPU).  Inputs: the reference-captured steps 0 and 1 of
+    tests/golden/lpv_n125_a3.npz; map table tests/golden/track_highway.npz.  The reference
+    records 111.9 ms per agent solve on an i7-13700H
+    (experiments_paper/LPV3r_agent_laptop/settings.csv), its agents solved one after another."""
+    import types
+
+    import cmpc
+
+    gold = os.path.join(ROOT, "tests", "golden")
+    d = np.load(os.path.join(gold, "lpv_n125_a3.npz"), allow_pickle=False)
+    t = np.load(os.path.join(gold, "track_highway.npz"), allow_pickle=False)
+    track = types.SimpleNamespace(PointAndTangent=t["PointAndTangent"], halfWidth=t["halfWidth"], lane=int(t["lane"]))
+    # config_LPV.py:6-11 gains; "SCALED CAR" model and limits (base_class.py:20-41)
+    Q = np.diag([10.0, 0.0, 0.0, 25.0, 10.0, 0.0, 0.0, 0.0, 0.0])
+    model = dict(lf=0.125, lr=0.125, m=1.98, I=0.09, Cf=70.0, Cr=70.0, mu=0.05)
+    lim = dict(vx_ref=float(d["vx_ref"]), min_dist=0.25, max_vel=5.5, min_vel=0.0, max_rs=0.3, max_ls=0.3,
+               max_ac=5.0, max_dc=10.0, sm=0.9)
+    N = int(d["N"])
+    bp = cmpc.PlannerLPVBatch(Q, 1e7 * np.eye(3), 0.0 * np.eye(2), 50.0 * np.eye(2), N, float(d["dt"]), track, 5.0,
+                              model, lim, ctx=ctx)
+    steps = []
+    for step in sorted(set(d["step"].tolist())):
+        sel = [j for j in range(len(d["step"])) if d["step"][j] == step]
+        args = (d["x0"][sel], np.stack([d[f"x_last_{j}"] for j in sel]), np.stack([d[f"u_last_{j}"] for j in sel]),
+                d["u_old"][sel], d["x_agents"][sel], d["pose"][sel])
+        res = bp.solve(*args)
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            res = bp.solve(*args)
+        ms = (time.perf_counter() - t0) / reps * 1e3
+        steps.append({"step": int(step), "agents": len(sel), "ms_per_step": ms,
+                      "ipm_iters": res["iters"].tolist(), "status": res["status"].tolist(),
+                      "max_abs_err_vs_certified_optimum": float(np.abs(res["z"] - d["z"][sel]).max())})
+    ref_ms = 111.9
+    worst = max(s_["ms_per_step"] for s_ in steps)
+    return {"workload": "reference config_LPV.py: N=125, 3 agents, Highway, nx=9 nu=2 nb=2, fp64 (PlannerLPV drop-in, "
+                        "host arrays)", "steps": steps,
+            "reference_ms_per_agent_solve": ref_ms, "reference_ms_per_step_3_agents_sequential": 3 * ref_ms,
+            "speedup_vs_reference_step": 3 * ref_ms / worst, "reps": reps}
 
 
 def pmc_traffic():

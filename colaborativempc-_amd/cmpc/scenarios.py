@@ -122,6 +122,17 @@ def di_alg_bytes(nx, nu, N, nb, word=8):
                    + N * nu + (N + 1) * nx + 3 * N + 2)
 
 
+def riccati_flops(nx, nu, N, iters):
+    """Algorithmic flops per agent-QP of the stage-wise Riccati method (mpc_riccati.hip): per IPM
+    iteration one factorisation, N x (P[A|B] + [A|B]'T + Hvy'K: 2 na nc nx + nc^2 nx + na^2 nu,
+    na = nc = nx + nu), and two Newton solves of 2 sweeps each (4 N (2 nx na)), plus the two
+    residual adjoints (2 N 2 nx (nx + nu)).  Used for cfg5's roofline instead of the condensed
+    count, which would credit the Riccati kernel with work it does not do."""
+    na = nx + nu
+    per_it = N * (2 * na * na * nx + na * na * nx + na * na * nu) + 4 * N * 2 * nx * na + 2 * N * 2 * nx * na
+    return iters * per_it
+
+
 def alg_flops(nx, nu, N, ncons, iters):
     """Algorithmic flops per agent-QP: condensing + iters x (G'WG + Cholesky + ...)."""
     n = N * nu

@@ -1335,7 +1335,7 @@ hipError_t mpc_riccati_launch(const MpcConst& c, const MpcPtrs& p, int batch, hi
     const Dims d = dims_of(c);
     const bool small = d.S <= kPerSmall * kWave;
     // instantiations: the PlannerLPV agent (nx 9, nu 2, 4 + nb rows per stage), the synthetic
-    // double integrator (nx 4, nu 2), and runtime dimensions
+    // double integrator (nx 4, nu 2; the 3-D one of cfg5: nx 6, nu 3, nb 2), runtime dimensions
     auto go = [&](auto g) -> hipError_t {
         using G = decltype(g);
         hipError_t e = hipFuncSetAttribute((const void*)mpc_riccati_kernel<G>,
@@ -1349,6 +1349,7 @@ hipError_t mpc_riccati_launch(const MpcConst& c, const MpcPtrs& p, int batch, hi
     else if (c.nx == 9 && c.nu == 2 && c.mc == 6) e = go(Cfg<kPerSmall, 9, 2, 6>{});
     else if (c.nx == 9 && c.nu == 2 && c.mc == 7) e = go(Cfg<kPerSmall, 9, 2, 7>{});
     else if (c.nx == 4 && c.nu == 2) e = go(Cfg<kPerSmall, 4, 2, 0>{});
+    else if (c.nx == 6 && c.nu == 3 && c.mc == 6) e = go(Cfg<kPerSmall, 6, 3, 6>{});   // BASELINE cfg5
     else if (small) e = go(Cfg<kPerSmall, 0, 0, 0>{});
     else e = go(Cfg<kPerMax, 0, 0, 0>{});
     if (e != hipSuccess) return e;

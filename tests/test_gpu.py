@@ -401,3 +401,55 @@ def test_unknown_option_flags_are_rejected(gpu_ctx):
             cmpc.solve_mpc(P, gpu_ctx)
     finally:
         Lb.opts = orig
+
+
+def test_lpv_builder_readback_matches_reference_schedule(gpu_ctx):
+    """cmpc_lpv_build_dev read back against the reference's own _EstimateABC / compute_hyperplane
+    outputs (tests/golden/schedule.npz, captured from LPV_Planner.py:477-591 and
+    compute_plane.py:41-68 on seeded states incl. the vx < 0.2 branch): A_k and B_k bit-exact,
+    the track-segment half-widths (index work: the segment lookup of misc.py:105-126) bit-exact,
+    planes to fp64 rounding (a norm and a division, numpy vs the device)."""
+    from conftest import golden
+    from oracle import lpv_ref as L
+
+    import cmpc
+
+    d = golden("schedule")
+    g = L.paper_gains()
+    for case, N in enumerate((10, 30)):
+        bp = cmpc.PlannerLPVBatch(g["Q"], g["Qs"], g["R"], g["dR"], N, 0.025, L.Track.build("Highway"), g["wq"],
+                                  L.SCALED_CAR_MODEL, L.scaled_car_limits(3.0), ctx=gpu_ctx)
+        out = bp.build(d[f"c{case}_states"][None], d[f"c{case}_u"][None], d[f"c{case}_agents"][None],
+                       d[f"c{case}_pose"][None])
+        assert out["err"].tolist() == [0]
+        np.testing.assert_array_equal(out["A"][0], d[f"c{case}_A"])
+        np.testing.assert_array_equal(out["B"][0], d[f"c{case}_B"])
+        np.testing.assert_array_equal(out["h"][0][:, 2], d[f"c{case}_ey"][:N])
+        np.testing.assert_array_equal(out["h"][0][:, 3], d[f"c{case}_ey"][:N])
+        np.testing.assert_allclose(out["planes"][0], d[f"c{case}_planes"], rtol=0, atol=4e-15)
+
+
+@pytest.mark.parametrize("name", ["lpv_n10_a2", "lpv_n30_a3", "lpv_n10_lowspeed", "lpv_n20_a4"])
+def test_lpv_builder_readback_matches_oracle_builder(gpu_ctx, name):
+    """The whole structured QP the GPU builds (A, B, qlin, C, h) against the oracle builder
+    (oracle/lpv_ref.py, pinned bit-exactly to the reference's assembly) on the captured steps:
+    equal up to a few ulps (planes enter C and h through one norm each)."""
+    from oracle import lpv_ref as L
+
+    import cmpc
+
+    g = L.paper_gains()
+    tr = L.Track.build("Highway")
+    for j, c in lpv_qps(name):
+        lim = L.scaled_car_limits(c["vx_ref"])
+        qp = L.assemble(c["x0"], c["x_last"], c["u_last"], c["x_agents"], c["pose"], c["u_old"], c["N"], c["dt"], tr,
+                        L.SCALED_CAR_MODEL, lim, g)
+        s = L.structured(qp, c["x0"], c["u_old"], c["N"], lim, g)
+        bp = cmpc.PlannerLPVBatch(g["Q"], g["Qs"], g["R"], g["dR"], c["N"], c["dt"], tr, g["wq"], L.SCALED_CAR_MODEL,
+                                  lim, ctx=gpu_ctx)
+        xa = c["x_agents"] if c["x_agents"].shape[1] else None
+        o = bp.build(c["x_last"][None], c["u_last"][None], None if xa is None else xa[None], c["pose"][None])
+        for k in ("A", "B", "qlin", "C", "h"):
+            a, b = o[k][0], s[k][0]
+            ulp = np.spacing(np.maximum(np.abs(a), np.abs(b)))
+            assert (np.abs(a - b) <= 16 * ulp).all(), (k, float(np.abs(a - b).max()))
