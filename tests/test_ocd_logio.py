@@ -57,3 +57,47 @@ def test_ros_payload_round_trip():
     back = logio.deserialise_np(logio.serialise_np([x]))[0]
     assert back.dtype == np.float32 and back.shape == x.shape
     assert np.array_equal(back, x.astype(np.float32))
+
+
+REF_LOGS = os.path.join(os.path.dirname(__file__), "golden", "ref_logs")
+
+
+def _bytes(p):
+    with open(p, "rb") as f:
+        return f.read()
+
+
+def test_lpv_log_rewrite_is_byte_identical_to_reference_files(tmp_path):
+    """Rows the reference's writer produced (an LPV run: OCD_it == [] so time / time_OCD are the
+    raw solve times and OCD_it.dat is empty) re-written by cmpc.logio: the same bytes."""
+    src = os.path.join(REF_LOGS, "lpv", "csv", "0")
+    st, u = np.loadtxt(os.path.join(src, "states.dat")), np.loadtxt(os.path.join(src, "u.dat"))
+    la, t = np.loadtxt(os.path.join(src, "plan_dist.dat")), np.loadtxt(os.path.join(src, "time.dat"))
+    out = logio.save_to_csv(str(tmp_path) + "/", 0, st, u, la, t, ocd_it=[])
+    for nm in ("states", "u", "plan_dist", "time", "OCD_it"):
+        assert _bytes(os.path.join(out, f"{nm}.dat")) == _bytes(os.path.join(src, f"{nm}.dat")), nm
+
+
+def test_ocd_log_rewrite_matches_reference_files(tmp_path):
+    """An OCD run (NL_3agents_def_t2, agent 2): states / u / plan_dist / time_OCD / OCD_it
+    byte-identical; time.dat (per-step sums of the round times) equal to the printed digits
+    (re-summed from the 6-digit time_OCD rows the reference printed)."""
+    src = os.path.join(REF_LOGS, "ocd", "csv", "2")
+    rd = lambda nm: np.loadtxt(os.path.join(src, f"{nm}.dat"))   # noqa: E731
+    it = rd("OCD_it").astype(int)
+    tocd = np.atleast_2d(rd("time_OCD"))
+    time_op = np.concatenate([tocd[i, :it[i]] for i in range(len(it))])
+    out = logio.save_to_csv(str(tmp_path) + "/", 2, rd("states"), rd("u"), rd("plan_dist"), time_op, ocd_it=list(it))
+    for nm in ("states", "u", "plan_dist", "time_OCD", "OCD_it"):
+        assert _bytes(os.path.join(out, f"{nm}.dat")) == _bytes(os.path.join(src, f"{nm}.dat")), nm
+    np.testing.assert_allclose(np.loadtxt(os.path.join(out, "time.dat")), rd("time"), rtol=2e-5)
+
+
+def test_settings_rewrite_is_byte_identical_to_reference_file(tmp_path):
+    import csv
+
+    src = os.path.join(REF_LOGS, "lpv", "settings.csv")
+    with open(src, newline="") as f:
+        rows = [tuple(r) for r in csv.reader(f)]
+    logio.save_settings(str(tmp_path), dict(rows))
+    assert _bytes(os.path.join(tmp_path, "settings.csv")) == _bytes(src)
