@@ -1023,7 +1023,7 @@ __global__ __launch_bounds__(kWave) void mpc_riccati_kernel(const MpcConst c_arg
     for (int r = l; r < m; r += kWave) {
         if (isfinite(w[r])) {
             const double g = row_value<G>(c, C, r, X, U, sig);
-            t[r] = fmax(w[r] - g, 1.0);
+            t[r] = fmax(w[r] - g, kT0Floor);
             lam[r] = 1.0;
             mact_l += 1.0;
             sp_l = fmax(sp_l, fabs(w[r]));

@@ -86,6 +86,9 @@ static double nmax(double a, double b) { return (a > b || a != a) ? a : b; }
 #define NBHD_GAMMA 0.01 /* wide-neighbourhood floor: t_r lambda_r >= gamma mu after a step */
 #endif
 #define STALL_ITERS 3   /* near-converged iterations without merit progress before stopping */
+#ifndef T0_FLOOR
+#define T0_FLOOR 0.5    /* starting slacks t_r = max(w_r - g_r, T0_FLOOR) (internal.h kT0Floor) */
+#endif
 
 static int chol(double* K, int n) {
     for (int j = 0; j < n; ++j) {
@@ -962,11 +965,7 @@ static int solve_one(const shared_t* S, const agent_t* a, double tol, int max_it
         if (!wk->act[r]) { t[r] = 1.0; lam[r] = 0.0; continue; }
         double g; ROWVAL(X, U, sig, r, g);
         double s0 = wk->w[r] - g;
-#ifdef T0_FLOOR
-        t[r] = s0 > T0_FLOOR ? s0 : T0_FLOOR;
-#else
-        t[r] = s0 > 1.0 ? s0 : 1.0;
-#endif
+        t[r] = s0 > T0_FLOOR ? s0 : T0_FLOOR; /* kT0Floor of the kernels (internal.h) */
         lam[r] = 1.0;
 #ifdef SIGMA_START
         if (r < ms) {
