@@ -61,6 +61,8 @@ struct RLds {
 
 struct Dims {
     int nx, nu, na, nc, sA, sB, sF, sAB, S;
+    int SW;  // factor / residual stage image [A_k | B_k | W_{k-1}]
+    int Sl;  // LDS slot stride max(S, SW)
 };
 
 // Compile-time problem configuration of a kernel instantiation: stage-image values per lane
@@ -70,6 +72,9 @@ struct Dims {
 template <int KP_, int NX_, int NU_, int MC_>
 struct Cfg {
     static constexpr int KP = KP_, NX = NX_, NU = NU_, MC = MC_;
+    // values per lane of the [A | B | W] images of the factor and residual sweeps
+    static constexpr int KPW = NX_ ? (2 * NX_ * NX_ + NX_ * NU_ + kWave - 1) / kWave
+                                   : (2 * CMPC_MAX_NX * CMPC_MAX_NX + CMPC_MAX_NX * CMPC_MAX_NU + kWave - 1) / kWave;
 };
 
 __host__ __device__ inline Dims dims_of(const MpcConst& c) {
@@ -83,6 +88,8 @@ __host__ __device__ inline Dims dims_of(const MpcConst& c) {
     d.sF = c.nu * d.na + c.nu * c.nu;  // gains K_k (nu x na) | Hinv_k (nu x nu)
     d.sAB = d.sA + d.sB;
     d.S = d.sAB + d.sF;
+    d.SW = d.sAB + d.sA;
+    d.Sl = d.S > d.SW ? d.S : d.SW;
     return d;
 }
 
@@ -98,6 +105,8 @@ __device__ __forceinline__ Dims dims_t(const MpcConst& c) {
     d.sF = d.nu * d.na + d.nu * d.nu;
     d.sAB = d.sA + d.sB;
     d.S = d.sAB + d.sF;
+    d.SW = d.sAB + d.sA;
+    d.Sl = d.S > d.SW ? d.S : d.SW;
     return d;
 }
 template <class G>
@@ -138,7 +147,7 @@ __host__ __device__ inline RLds r_layout(const MpcConst& c) {
     L.rsig = take(N * ns);
     L.P = take(d.na * d.na);
     L.pv = take(2 * d.na);
-    L.sb = take(2 * d.S);
+    L.sb = take(2 * d.Sl);
     L.T = take(d.na * d.nc);
     L.G = take(d.nc * d.nc);
     L.Hy = take(c.nu * d.na);
@@ -183,26 +192,32 @@ __host__ __device__ inline RGlb r_glb(const MpcConst& c) {
     return g;
 }
 
-// Stage image of stage k: [A_k (nx x nx) | B_k (nx x nu) | K_k (nu x na) | Hinv_k (nu x nu)]
-// (the first `cnt` values).  Lane l holds values l, l + 64, ...
+// Stage image of stage k: [A_k (nx x nx) | B_k (nx x nu) | third segment] (the first `cnt`
+// values; lane l holds values l, l + 64, ...).  The third segment is the gains K_k | Hinv_k of
+// the solve sweeps (lag 0) or the weight W_{k-1} of the factor's P_k update (lag 1).
 struct StageSrc {
     const double* A;
     const double* B;
-    const double* F;  // gains K_k | Hinv_k (solve sweeps)
+    const double* F;
     int sA, sB, sF;
+    int lag;
 };
 
+// Exactly KP loads per lane from clamped addresses, no branches: the compiler's wait counting
+// then keeps the prefetched stages in flight (a data-dependent number of loads makes it drain
+// the counter before every use)
 template <int KP>
 __device__ __forceinline__ void stage_fetch(const StageSrc& s, int k, int cnt, double (&r)[KP]) {
     const int l = threadIdx.x;
+    const int kf = k - s.lag > 0 ? k - s.lag : 0;
 #pragma unroll
     for (int q = 0; q < KP; ++q) {
-        const int e = l + q * kWave;
-        double v = 0.0;
-        if (e < s.sA) v = s.A[(size_t)k * s.sA + e];
-        else if (e < s.sA + s.sB) v = s.B[(size_t)k * s.sB + (e - s.sA)];
-        else if (e < cnt) v = s.F[(size_t)k * s.sF + (e - s.sA - s.sB)];
-        r[q] = v;
+        int e = l + q * kWave;
+        e = e < cnt ? e : cnt - 1;
+        const double* p = (e < s.sA) ? s.A + (size_t)k * s.sA + e
+                                     : ((e < s.sA + s.sB) ? s.B + (size_t)k * s.sB + (e - s.sA)
+                                                          : s.F + (size_t)kf * s.sF + (e - s.sA - s.sB));
+        r[q] = *p;
     }
 }
 
@@ -230,37 +245,35 @@ struct Pipe {
     __device__ Pipe(const StageSrc& s_, int cnt_, int N_, int S_, bool back_, double* sb_)
         : src(s_), cnt(cnt_), N(N_), S(S_), back(back_), sb(sb_) {}
     __device__ int stg(int j) const { return back ? N - 1 - j : j; }
-    // fetch the first kDepth stages, store the first; follow with bar()
+    // stage of step j, clamped into the horizon (steps past the end fetch a real stage, unused)
+    __device__ int stc(int j) const { return stg(j < N ? j : N - 1); }
+    // fetch the first kDepth stages, store the first; follow with wsync()
     __device__ void prime() {
-        static_for<0, kDepth>([&](auto i) {
-            if (i < N) stage_fetch<KP>(src, stg(i), cnt, r[i]);
-        });
+        static_for<0, kDepth>([&](auto i) { stage_fetch<KP>(src, stc(i), cnt, r[i]); });
         stage_put<KP>(sb + (stg(0) & 1) * S, cnt, r[0]);
-        if (kDepth < N) stage_fetch<KP>(src, stg(kDepth), cnt, r[0]);
+        stage_fetch<KP>(src, stc(kDepth), cnt, r[0]);
     }
     // after step j: store stage j+1 (register set I = (j+1) % kDepth) into the other slot and
-    // refill the set with stage j+1+kDepth
+    // refill the set with stage j+1+kDepth — unconditionally (see stage_fetch)
     template <int I>
     __device__ void advance(int j) {
-        if (j + 1 < N) {
-            stage_put<KP>(sb + (stg(j + 1) & 1) * S, cnt, r[I]);
-            if (j + 1 + kDepth < N) stage_fetch<KP>(src, stg(j + 1 + kDepth), cnt, r[I]);
-        }
+        stage_put<KP>(sb + ((stg(j) + 1) & 1) * S, cnt, r[I]);
+        stage_fetch<KP>(src, stc(j + 1 + kDepth), cnt, r[I]);
     }
 };
 
 // body(k, img) for every stage of the sweep (img: the stage image of k), then bar()
+// (the step count is padded to a multiple of kDepth; padding steps run no body, only the
+// pipe's unconditional advance, so every path issues the same loads)
 template <int KP, class Body>
 __device__ __forceinline__ void sweep(Pipe<KP>& p, Body&& body) {
     for (int j0 = 0; j0 < p.N; j0 += kDepth)
         static_for<0, kDepth>([&](auto ii) {
             const int j = j0 + ii;
-            if (j < p.N) {
-                const int k = p.stg(j);
-                body(k, (const double*)(p.sb + (k & 1) * p.S));
-                p.template advance<(ii + 1) % kDepth>(j);
-                wsync();
-            }
+            const int k = p.stg(j);
+            if (j < p.N) body(k, (const double*)(p.sb + (k & 1) * p.S));
+            p.template advance<(ii + 1) % kDepth>(j);
+            wsync();
         });
 }
 
@@ -334,7 +347,7 @@ template <class G>
 __device__ __forceinline__ void fwd_sim(const MpcConst& c, const Dims& d, const StageSrc& src, double* sb,
                         const double* __restrict__ x0, const double* U, double* X) {
     const int l = threadIdx.x, nx = d.nx, nu = d.nu, N = c.N;
-    Pipe<G::KP> pp(src, d.sAB, N, d.S, false, sb);
+    Pipe<G::KP> pp(src, d.sAB, N, d.Sl, false, sb);
     pp.prime();
     if (l < nx) X[l] = x0 ? x0[l] : 0.0;
     wsync();
@@ -354,7 +367,7 @@ template <class G>
 __device__ __forceinline__ void adjoint(const MpcConst& c, const Dims& d, const StageSrc& src, double* sb, const double* yb,
                         double* out, double* psi2) {
     const int l = threadIdx.x, nx = d.nx, nu = d.nu, N = c.N;
-    Pipe<G::KP> pp(src, d.sAB, N, d.S, true, sb);
+    Pipe<G::KP> pp(src, d.sAB, N, d.Sl, true, sb);
     pp.prime();
     if (l < nx) psi2[l] = yb[N * nx + l];
     wsync();
@@ -449,8 +462,8 @@ __device__ __forceinline__ bool riccati_factor(const MpcConst& c, const Dims& d,
     double* Kk = sm + L.Kk;
     double* sb = sm + L.sb;
     const double* th = sm + L.th;
-    const StageSrc src{A, B, nullptr, d.sA, d.sB, d.sF};
-    Pipe<G::KP> pp(src, d.sAB, N, d.S, true, sb);
+    const StageSrc src{A, B, Wg, d.sA, d.sB, d.sA, 1};  // [A_k | B_k | W_{k-1}]
+    Pipe<G::KPW> pp(src, d.SW, N, d.Sl, true, sb);
     pp.prime();
     // P_N = blkdiag(W_N, 0),  W_N = 2Q + M_N (stage rows of X_N)
     for (int e = l; e < na * na; e += kWave) {
@@ -586,7 +599,7 @@ __device__ __forceinline__ bool riccati_factor(const MpcConst& c, const Dims& d,
         for (int e = l; e < na * na && k > 0; e += kWave) {
             const int i = e / na, j = e - i * na;
             if (j > i) continue;
-            double v = (i < nx) ? Wg[(size_t)(k - 1) * nx * nx + i * nx + j] + Gm[i * nc + j]
+            double v = (i < nx) ? Ak[d.sAB + i * nx + j] + Gm[i * nc + j]
                                 : ((j >= nx) ? 2.0 * c.dR[(i - nx) * nu + (j - nx)] : 0.0);
             for (int a = 0; a < nu; ++a) v = fma(Hy[a * na + i], Kk[a * na + j], v);
             P[i * na + j] = v;
@@ -612,8 +625,8 @@ __device__ __forceinline__ bool riccati_factor_dd(const MpcConst& c, const Dims&
     double* Kk = sm + L.Kd;
     double* sb = sm + L.sb;
     const double* th = sm + L.th;
-    const StageSrc src{A, B, nullptr, d.sA, d.sB, d.sF};
-    Pipe<G::KP> pp(src, d.sAB, N, d.S, true, sb);
+    const StageSrc src{A, B, Wg, d.sA, d.sB, d.sA, 1};  // [A_k | B_k | W_{k-1}]
+    Pipe<G::KPW> pp(src, d.SW, N, d.Sl, true, sb);
     pp.prime();
     for (int e = l; e < na * na; e += kWave) {
         const int i = e / na, j = e - i * na;
@@ -751,7 +764,7 @@ __device__ __forceinline__ bool riccati_factor_dd(const MpcConst& c, const Dims&
             if (j > i) continue;
             dd v;
             if (i < nx) {
-                v = dd_of(Wg[(size_t)(k - 1) * nx * nx + i * nx + j]);
+                v = dd_of(Ak[d.sAB + i * nx + j]);
                 for (int s2 = 0; s2 < nx; ++s2) v = dd_fmad(v, ld_dd(PA, s2 * nx + j), Ak[s2 * nx + i]);
             } else {
                 v = dd_of((j >= nx) ? 2.0 * c.dR[(i - nx) * nu + (j - nx)] : 0.0);
@@ -774,11 +787,11 @@ __device__ __forceinline__ void riccati_solve(const MpcConst& c, const Dims& d, 
     double* sb = sm + L.sb;
     double* pv = sm + L.pv;
     double* xb = sm + L.xpp;  // dX_k, ping-pong
-    const StageSrc src{A, B, F, d.sA, d.sB, d.sF};
+    const StageSrc src{A, B, F, d.sA, d.sB, d.sF, 0};
     // backward: p_N = 0;  g = -rh_k + B'p_x + p_u;  kk_k = -Hinv g (into dU);  p_k = [A'p_x; 0] + K'g.
     // Every lane forms the nu values of g itself (nu <= 4), so a stage needs one barrier.
     {
-        Pipe<G::KP> pp(src, d.S, N, d.S, true, sb);
+        Pipe<G::KP> pp(src, d.S, N, d.Sl, true, sb);
         pp.prime();
         if (l < na) pv[l] = 0.0;
         wsync();
@@ -818,7 +831,7 @@ __device__ __forceinline__ void riccati_solve(const MpcConst& c, const Dims& d, 
     }
     // forward: y_0 = 0;  v_k = kk_k + K_k y_k;  dX_{k+1} = A_k dX_k + B_k v_k (every lane < nx forms v_k)
     {
-        Pipe<G::KP> pp(src, d.S, N, d.S, false, sb);
+        Pipe<G::KP> pp(src, d.S, N, d.Sl, false, sb);
         pp.prime();
         if (l < nx) {
             xb[l] = 0.0;
@@ -873,10 +886,10 @@ __device__ __forceinline__ void kres_dd(const MpcConst& c, const Dims& d, const 
     double* sb = sm + L.sb;
     const double* th = sm + L.th;
     double* psid = sm + L.psid;  // two dd vectors of nx, ping-pong
-    const StageSrc src{A, B, nullptr, d.sA, d.sB, d.sF};
+    const StageSrc src{A, B, B, d.sA, d.sB, d.sF, 0};  // third segment unused (cnt = sAB); never null
     // forward: X_0 = 0, X_{k+1} = A_k X_k + B_k v_k
     {
-        Pipe<G::KP> pp(src, d.sAB, N, d.S, false, sb);
+        Pipe<G::KP> pp(src, d.sAB, N, d.Sl, false, sb);
         pp.prime();
         if (l < nx) st_dd(Xd, l, dd_of(0.0));
         wsync();
@@ -892,7 +905,8 @@ __device__ __forceinline__ void kres_dd(const MpcConst& c, const Dims& d, const 
     }
     // adjoint: psi_N = W X_N, psi_k = W X_k + A_k' psi_{k+1};  out_k = rhs_k - B_k' psi_{k+1} - (...)
     {
-        Pipe<G::KP> pp(src, d.sAB, N, d.S, true, sb);
+        const StageSrc srw{A, B, Wg, d.sA, d.sB, d.sA, 1};  // [A_k | B_k | W_{k-1}]
+        Pipe<G::KPW> pp(srw, d.SW, N, d.Sl, true, sb);
         pp.prime();
         if (l < nx) {
             dd acc = dd_of(0.0);
@@ -920,8 +934,7 @@ __device__ __forceinline__ void kres_dd(const MpcConst& c, const Dims& d, const 
             } else if (k > 0 && l >= 32 && l < 32 + nx) {
                 const int t = l - 32;
                 dd acc = dd_of(0.0);
-                for (int u = 0; u < nx; ++u)
-                    acc = dd_fmad(acc, ld_dd(Xd, k * nx + u), Wg[(size_t)(k - 1) * nx2 + t * nx + u]);
+                for (int u = 0; u < nx; ++u) acc = dd_fmad(acc, ld_dd(Xd, k * nx + u), Ak[d.sAB + t * nx + u]);
                 for (int s2 = 0; s2 < nx; ++s2) acc = dd_fmad(acc, ld_dd(pa, s2), Ak[s2 * nx + t]);
                 st_dd(pb, t, acc);
             }
@@ -986,7 +999,7 @@ __global__ __launch_bounds__(kWave) void mpc_riccati_kernel(const MpcConst c_arg
     double* Dsig = sm + L.Dsig;
     double* rsig = sm + L.rsig;
     double* sb = sm + L.sb;
-    const StageSrc sAB{A, B, nullptr, d.sA, d.sB, d.sF};
+    const StageSrc sAB{A, B, B, d.sA, d.sB, d.sF, 0};  // third segment unused (cnt = sAB); never null
 
     for (int i = l; i < L.cst; i += kWave) sm[i] = 0.0;
     wsync();
