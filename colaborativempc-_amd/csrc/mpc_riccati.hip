@@ -46,6 +46,9 @@ constexpr int kPerSmall = 2;                               // ... when the stage
 constexpr int kDepth = 3;  // stage images in flight: a sweep step waits for a load issued 2 steps earlier
 constexpr double kDdTh = 1e10;   // max th above which an iteration runs in double-double
 constexpr int kRefineMax = 6;    // refinement steps of a double-double iteration's direction
+constexpr double kRefineTol = 1e-13;  // ... until |correction| <= kRefineTol |dU|: 1e-16 -> 1e-13 cut
+                                      // the steps on the captured LPV QPs by 39% (752 -> 456) with the
+                                      // same iterates to 1e-13 (tools/ipm_lab.py, oracle REF_TOL)
 
 struct RLds {
     int t, lam, th, rp, rho, rt, w, GdU;  // per row
@@ -779,10 +782,17 @@ __device__ __forceinline__ bool riccati_factor_dd(const MpcConst& c, const Dims&
 
 // Solve the Newton system for the right-hand side rh (n values): dU (n) and, when dX is not
 // null, dX ((N+1) nx, dX_0 = 0), with the gains of riccati_factor.
+//
+// Fused form (yb != null, rh unused): the right-hand side rh = -rd - (B'psi + rt_u) of a pass,
+// whose psi is the adjoint recursion psi_k = yb_k + A_k' psi_{k+1} of the stage rows' C'rt,
+// is formed inside the backward sweep: with s = psi + p_x (p the Riccati costate) both
+// recursions become one, s_k = yb_k + A_k' s_{k+1} + (K_k'g)_x, g = p_u + rd_k + rt_u + B_k' s_{k+1}
+// — one sweep fewer per pass.
 template <class G>
 __device__ __forceinline__ void riccati_solve(const MpcConst& c, const Dims& d, const RLds& L, double* sm,
                               const double* __restrict__ A, const double* __restrict__ B,
-                              const double* __restrict__ F, const double* rh, double* dU, double* dX) {
+                              const double* __restrict__ F, const double* rh, double* dU, double* dX,
+                              const double* yb = nullptr, const double* rd = nullptr, const double* rt = nullptr) {
     const int l = threadIdx.x, nx = d.nx, nu = d.nu, na = d.na, N = c.N;
     double* sb = sm + L.sb;
     double* pv = sm + L.pv;
@@ -793,7 +803,7 @@ __device__ __forceinline__ void riccati_solve(const MpcConst& c, const Dims& d, 
     {
         Pipe<G::KP> pp(src, d.S, N, d.Sl, true, sb);
         pp.prime();
-        if (l < na) pv[l] = 0.0;
+        if (l < na) pv[l] = (yb && l < nx) ? yb[N * nx + l] : 0.0;
         wsync();
         sweep(pp, [&](int k, const double* Ak) {
             const double* Bk = Ak + d.sA;
@@ -807,12 +817,13 @@ __device__ __forceinline__ void riccati_solve(const MpcConst& c, const Dims& d, 
                 for (int a = 0; a < CMPC_MAX_NU; ++a) {
                     double v = 0.0;
                     if (a < nu) {
-                        v = pc[nx + a] - rh[k * nu + a];
+                        const int ci = k * nu + a;
+                        v = pc[nx + a] + (yb ? rd[ci] + (rt[c.ms + 2 * ci] - rt[c.ms + 2 * ci + 1]) : -rh[ci]);
                         for (int s2 = 0; s2 < nx; ++s2) v = fma(Bk[s2 * nu + a], pc[s2], v);
                     }
                     g[a] = v;
                 }
-                double v = 0.0;
+                double v = (yb && l < nx) ? yb[k * nx + l] : 0.0;
                 if (l < nx)
                     for (int s2 = 0; s2 < nx; ++s2) v = fma(Ak[s2 * nx + l], pc[s2], v);
 #pragma unroll
@@ -1193,14 +1204,18 @@ __global__ __launch_bounds__(kWave) void mpc_riccati_kernel(const MpcConst c_arg
                 yb[i] = v;
             }
             wsync();
-            adjoint<G>(c, d, sAB, sb, yb, rh, psi);
-            // rhs = -rd - G' rt
-            for (int i = l; i < n; i += kWave) rh[i] = -rd[i] - (rh[i] + rt[ms + 2 * i] - rt[ms + 2 * i + 1]);
-            wsync();
-            RSTAMP(4);
-            riccati_solve<G>(c, d, L, sm, A, B, F, rh, dU, dX);
-            RSTAMP(5);
-            if (hp) {
+            if (!hp) {
+                RSTAMP(4);
+                riccati_solve<G>(c, d, L, sm, A, B, F, nullptr, dU, dX, yb, rd, rt);  // rhs fused in
+                RSTAMP(5);
+            } else {
+                adjoint<G>(c, d, sAB, sb, yb, rh, psi);
+                // rhs = -rd - G' rt (kept: the refinement measures residuals against it)
+                for (int i = l; i < n; i += kWave) rh[i] = -rd[i] - (rh[i] + rt[ms + 2 * i] - rt[ms + 2 * i + 1]);
+                wsync();
+                RSTAMP(4);
+                riccati_solve<G>(c, d, L, sm, A, B, F, rh, dU, dX);
+                RSTAMP(5);
                 // refinement: dU += M^-1 (rhs - K dU), residual in double-double (gU, cr: free here)
                 for (int ir = 0; ir < kRefineMax; ++ir) {
                     kres_dd<G>(c, d, L, sm, A, B, Wg, dU, rh, gU);
@@ -1215,7 +1230,7 @@ __global__ __launch_bounds__(kWave) void mpc_riccati_kernel(const MpcConst c_arg
                     const double cn = wave_max(cn_l), un = wave_max(un_l);
                     wsync();
                     RCOUNT(13);
-                    if (!(cn > 1e-16 * un)) break;
+                    if (!(cn > kRefineTol * un)) break;
                 }
                 fwd_sim<G>(c, d, sAB, sb, nullptr, dU, dX);
                 RSTAMP(6);

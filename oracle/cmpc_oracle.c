@@ -86,6 +86,10 @@ static double nmax(double a, double b) { return (a > b || a != a) ? a : b; }
 #define NBHD_GAMMA 0.01 /* wide-neighbourhood floor: t_r lambda_r >= gamma mu after a step */
 #endif
 #define STALL_ITERS 3   /* near-converged iterations without merit progress before stopping */
+#ifndef REF_TOL
+#define REF_TOL 1e-13 /* refinement stops once |correction| <= REF_TOL |dU| (kernel: kRefineTol) */
+#endif
+
 #ifndef T0_FLOOR
 #define T0_FLOOR 0.5    /* starting slacks t_r = max(w_r - g_r, T0_FLOOR) (internal.h kT0Floor) */
 #endif
@@ -1201,6 +1205,9 @@ static int solve_one(const shared_t* S, const agent_t* a, double tol, int max_it
                 /* iterative refinement: dU += M^-1 (rhs - K dU) */
                 const int nref = hp ? RIC_REFINE_MAX : S->refine;
                 for (int ir = 0; ir < nref; ++ir) {
+#ifdef REF_COUNT
+                    if (hp) fprintf(stderr, "REF\n");
+#endif
                     double *kv = wk->Yk, *cr = wk->Yk + n, *cx = wk->Yk + 2 * n;
 #ifdef KMUL_QUAD
                     kres_q(S, a, wk->th, wk->Dsig, wk->dU, wk->rhs, kv);
@@ -1219,7 +1226,7 @@ static int solve_one(const shared_t* S, const agent_t* a, double tol, int max_it
                         cn = fmax(cn, fabs(cr[c]));
                         un = fmax(un, fabs(wk->dU[c]));
                     }
-                    if (cn <= 1e-16 * un) break;
+                    if (cn <= REF_TOL * un) break;
                 }
                 if (nref) fwd_sim(S, a, NULL, wk->dU, wk->dX);
 #ifdef RIC_DEBUG
