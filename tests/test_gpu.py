@@ -306,6 +306,32 @@ def test_riccati_forced_matches_condensed(gpu_ctx, n, N, nb, dim):
     print(f"riccati iters mean {ir.mean():.2f} vs condensed {idd.mean():.2f}")
 
 
+def test_cfg5_population_on_riccati_kernel(gpu_ctx):
+    """BASELINE cfg5's shape at scale (3-D double integrator nx=6 nu=3, N=50, nb=2; 1024 agents):
+    the path `bench.py --config cfg5` times (fp64 stage-wise Riccati).  >= 99 % of the agents
+    report CMPC_SOLVED, none fails, and a 128-agent sample matches the fp64 C restatement."""
+    import cmpc
+    from cmpc import scenarios as S
+    from oracle import cmpc_oracle as CO
+    from oracle import synth
+
+    n, ns = 1024, 128
+    sc = S.make_di(n, 50, 2, 3)
+    P = synth.structured(sc.shared, sc.params, sc.A, sc.B, sc.x0, sc.u_prev, sc.lane, sc.nbr, sc.traj,
+                         np.arange(n))
+    z, kkt, it, st = cmpc.solve_mpc(P, gpu_ctx)
+    frac = float((st == cmpc.CMPC_SOLVED).mean())
+    print(f"cfg5 x{n}: solved {frac:.4f}, status {np.unique(st, return_counts=True)}, iters mean {it.mean():.1f} "
+          f"max {it.max()}")
+    assert frac >= 0.99 and np.isin(st, (cmpc.CMPC_SOLVED, cmpc.CMPC_SOLVED_INACCURATE)).all()
+    assert np.isfinite(z).all()
+    Ps = {k: (v[:ns] if isinstance(v, np.ndarray) and v.ndim and v.shape[0] == n else v) for k, v in P.items()}
+    zc, _, _, stc = CO.solve_batch(Ps, nthreads=8)
+    both = (st[:ns] == cmpc.CMPC_SOLVED) & (stc == 1)
+    assert both.mean() >= 0.95
+    assert np.abs(z[:ns][both] - zc[both]).max() < Z_TOL
+
+
 # fp32 bar (BASELINE cfg5 "fp32 path with tolerance check vs fp64 reference"): every z entry
 # (states, slacks, inputs) within FP32_ZTOL * max(1, |z|) of the fp64 optimum; measured 2.3e-3
 # on this batch (fp32 resolves mu only to ~1e-6 under the 1e7 slack weights)
