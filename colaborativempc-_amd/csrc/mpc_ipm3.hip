@@ -94,16 +94,21 @@ __device__ __forceinline__ void fwd3(int l, int N, const double* A, const double
     double xr = x0 ? x0[s] : 0.0;
     X[s] = xr;
     if (N <= 0) return;
-    auto fetch = [&](int k, double* av, double& b) __attribute__((always_inline)) {
+    // the fetch only loads: the B u product is formed in the step, so the loads' wait lands at
+    // the step that consumes them (one stage later), not right behind the loads
+    auto fetch = [&](int k, double* av, double* bv) __attribute__((always_inline)) {
 #pragma unroll
         for (int t = 0; t < NX; ++t) av[t] = A[(k * NX + s) * NX + t];
-        double v = 0.0;
 #pragma unroll
-        for (int i = 0; i < NU; ++i) v = fma(B[(k * NX + s) * NU + i], U[k * NU + i], v);
-        b = v;
+        for (int i = 0; i < NU; ++i) {
+            bv[i] = B[(k * NX + s) * NU + i];
+            bv[NU + i] = U[k * NU + i];
+        }
     };
-    auto step = [&](int k, const double* av, double b) __attribute__((always_inline)) {
-        double v0 = b, v1 = 0.0;
+    auto step = [&](int k, const double* av, const double* bv) __attribute__((always_inline)) {
+        double v0 = 0.0, v1 = 0.0;
+#pragma unroll
+        for (int i = 0; i < NU; ++i) v0 = fma(bv[i], bv[NU + i], v0);
         static_for<0, NX>([&](auto t) __attribute__((always_inline)) {
             constexpr int tt = decltype(t)::value;
             if constexpr (tt & 1) v1 = fma(av[tt], bcast16<tt>(xr), v1);
@@ -112,72 +117,92 @@ __device__ __forceinline__ void fwd3(int l, int N, const double* A, const double
         xr = v0 + v1;
         X[(k + 1) * NX + s] = xr;
     };
-    double a0[NX], a1[NX], b0, b1;
+    // three register sets, fetched two stages ahead (unrolled by three: no copies; fetch indices
+    // clamped, not guarded): a stage's LDS latency hides behind two stages of the chain
+    double a0[NX], a1[NX], a2[NX], b0[2 * NU], b1[2 * NU], b2[2 * NU];
     fetch(0, a0, b0);
+    fetch(1 < N ? 1 : N - 1, a1, b1);
     int k = 0;
-    for (; k + 1 < N; k += 2) {
-        fetch(k + 1, a1, b1);
+    // (scheduling barriers keep the machine scheduler from sinking the loads towards their use)
+    for (; k + 2 < N; k += 3) {
+        fetch(k + 2, a2, b2);
+        __builtin_amdgcn_sched_barrier(0);
         step(k, a0, b0);
-        fetch(k + 2 < N ? k + 2 : N - 1, a0, b0);
+        fetch(k + 3 < N ? k + 3 : N - 1, a0, b0);
+        __builtin_amdgcn_sched_barrier(0);
         step(k + 1, a1, b1);
+        fetch(k + 4 < N ? k + 4 : N - 1, a1, b1);
+        __builtin_amdgcn_sched_barrier(0);
+        step(k + 2, a2, b2);
     }
     if (k < N) step(k, a0, b0);
+    if (k + 1 < N) step(k + 1, a1, b1);
 }
 
-// Two adjoints at once (rows 0,1 of the wave on y0 -> o0, rows 2,3 on y1 -> o1):
-// o_k = B_k' psi_{k+1}, psi_N = y_N, psi_k = y_k + A_k' psi_{k+1}.  Lane (l & 15) = s carries
-// psi_s; psi_t reaches the row by DPP row_newbcast; operands of stage k-1 are fetched ahead into
-// ping-pong registers (unrolled by two, clamped fetch index, no branches).  Every lane stores
-// o[k NU + su]: rows 0/1 (2/3) and lanes s >= NU (which compute column 0) duplicate values.
-template <int NX, int NU>
-__device__ __forceinline__ void adj3(int l, int N, const double* A, const double* B, const double* y0,
-                                     const double* y1, double* o0, double* o1) {
-    static_assert(NX <= 16 && NU <= 16, "row broadcast");
+// The adjoint's serial part only: psi_N = y_N, psi_k = y_k + A_k' psi_{k+1} for k = N-1 .. 1,
+// written over y in place (rows 0,1 of the wave on y0, rows 2,3 on y1; y_k is fetched before
+// psi_k overwrites it).  The products o_k = B_k' psi_{k+1} are independent of one another and
+// are formed afterwards by the lanes that own u_k (bpsi3), off the recursion's chain.  The
+// operation order is the fused recursion's (even/odd partial sums), so the bits are unchanged.
+template <int NX>
+__device__ __forceinline__ void psi3(int l, int N, const double* A, double* y0, double* y1) {
+    static_assert(NX <= 16, "row broadcast");
     const int h = l >> 5, s = l & 15;
-    const int sx = s < NX ? s : 0, su = s < NU ? s : 0;
-    const double* y = h ? y1 : y0;
-    double* o = h ? o1 : o0;
+    const int sx = s < NX ? s : 0;
+    double* y = h ? y1 : y0;
     double pr = y[N * NX + sx];
-    if (N <= 0) return;
-    auto fetch = [&](int k, double* av, double* bv, double& yv) __attribute__((always_inline)) {
+    if (N <= 1) return;
+    auto fetch = [&](int k, double* av, double& yv) __attribute__((always_inline)) {
 #pragma unroll
-        for (int t = 0; t < NX; ++t) {
-            av[t] = A[(k * NX + t) * NX + sx];
-            bv[t] = B[(k * NX + t) * NU + su];
-        }
-        const double yy = y[k * NX + sx];
-        yv = k > 0 ? yy : 0.0;
+        for (int t = 0; t < NX; ++t) av[t] = A[(k * NX + t) * NX + sx];
+        yv = y[k * NX + sx];
     };
-    auto step = [&](int k, const double* av, const double* bv, double yk) __attribute__((always_inline)) {
+    auto step = [&](int k, const double* av, double yk) __attribute__((always_inline)) {
         double ps[NX];
         static_for<0, NX>([&](auto t) __attribute__((always_inline)) {
             constexpr int tt = decltype(t)::value;
             ps[tt] = bcast16<tt>(pr);
         });
-        double v0 = 0.0, v1 = 0.0, p0 = yk, p1 = 0.0;
+        double p0 = yk, p1 = 0.0;
 #pragma unroll
         for (int t = 0; t < NX; ++t) {
-            if (t & 1) {
-                v1 = fma(bv[t], ps[t], v1);
-                p1 = fma(av[t], ps[t], p1);
-            } else {
-                v0 = fma(bv[t], ps[t], v0);
-                p0 = fma(av[t], ps[t], p0);
-            }
+            if (t & 1) p1 = fma(av[t], ps[t], p1);
+            else p0 = fma(av[t], ps[t], p0);
         }
-        o[k * NU + su] = v0 + v1;
         pr = p0 + p1;
+        y[k * NX + sx] = pr;
     };
-    double a0[NX], bb0[NX], y0k, a1[NX], bb1[NX], y1k;
-    fetch(N - 1, a0, bb0, y0k);
+    // three register sets fetched two stages ahead; fetch indices clamped to stage 1
+    double a0[NX], y0k, a1[NX], y1k, a2[NX], y2k;
+    fetch(N - 1, a0, y0k);
+    fetch(N >= 3 ? N - 2 : 1, a1, y1k);
     int k = N - 1;
-    for (; k >= 1; k -= 2) {
-        fetch(k - 1, a1, bb1, y1k);
-        step(k, a0, bb0, y0k);
-        fetch(k >= 2 ? k - 2 : 0, a0, bb0, y0k);
-        step(k - 1, a1, bb1, y1k);
+    for (; k >= 3; k -= 3) {
+        fetch(k - 2, a2, y2k);
+        __builtin_amdgcn_sched_barrier(0);
+        step(k, a0, y0k);
+        fetch(k >= 4 ? k - 3 : 1, a0, y0k);
+        __builtin_amdgcn_sched_barrier(0);
+        step(k - 1, a1, y1k);
+        fetch(k >= 5 ? k - 4 : 1, a1, y1k);
+        __builtin_amdgcn_sched_barrier(0);
+        step(k - 2, a2, y2k);
     }
-    if (k == 0) step(0, a0, bb0, y0k);
+    if (k >= 1) step(k, a0, y0k);
+    if (k >= 2) step(k - 1, a1, y1k);
+}
+
+// o = B_k[:, i]' psi_{k+1} (psi as left in place by psi3): even/odd partial sums, as before
+template <int NX, int NU>
+__device__ __forceinline__ double bpsi3(const double* B, const double* psi, int k, int i) {
+    double v0 = 0.0, v1 = 0.0;
+#pragma unroll
+    for (int t = 0; t < NX; ++t) {
+        const double bt = B[(k * NX + t) * NU + i], pt = psi[(k + 1) * NX + t];
+        if (t & 1) v1 = fma(bt, pt, v1);
+        else v0 = fma(bt, pt, v0);
+    }
+    return v0 + v1;
 }
 
 }  // namespace
@@ -210,7 +235,6 @@ __global__ __launch_bounds__(64, 1) void mpc_ipm3_kernel(const MpcConst c, const
     double* U = sm + L.U;
     double* dU = sm + L.dU;
     double* rd = sm + L.rd;
-    double* gU = sm + L.gU;
     double* vb = sm + L.vb;
     double* thin = sm + L.thin;
     double* bU = sm + L.bU;
@@ -360,7 +384,7 @@ __global__ __launch_bounds__(64, 1) void mpc_ipm3_kernel(const MpcConst c, const
         if (l < NX) dX[l] = yb[l];
         wsync();
         STAMP(0);
-        adj3<NX, NU>(l, N, sA, sB, yb, dX, gU, rd);
+        psi3<NX>(l, N, sA, yb, dX);  // psi over yb (-> gradient) and over dX (-> rd)
         wsync();
         STAMP(1);
         double gs_l = 1.0, nrd_l = 0.0, nrs_l = 0.0, nrp_l = 0.0, mu_l = 0.0;
@@ -387,8 +411,8 @@ __global__ __launch_bounds__(64, 1) void mpc_ipm3_kernel(const MpcConst c, const
                         const double dun = (k + 1 < N) ? U[(k + 1) * NU + j] - uk : 0.0;
                         v += R2[i * NU + j] * uk + dR2[i * NU + j] * (duk - dun);
                     }
-                    const double g = gU[ci] + v;
-                    const double rdv = rd[ci] + v + lam[2 * i] - lam[2 * i + 1];
+                    const double g = bpsi3<NX, NU>(sB, yb, k, i) + v;
+                    const double rdv = bpsi3<NX, NU>(sB, dX, k, i) + v + lam[2 * i] - lam[2 * i + 1];
                     rd[ci] = rdv;
                     gs_l = nmax(gs_l, fabs(g));
                     nrd_l = nmax(nrd_l, fabs(rdv));
@@ -802,14 +826,14 @@ __global__ __launch_bounds__(64, 1) void mpc_ipm3_kernel(const MpcConst c, const
             if (l < NX) yb[l] = 0.0;
             wsync();
             STAMP(8);
-            adj3<NX, NU>(l, N, sA, sB, yb, yb, vb, vb);
+            psi3<NX>(l, N, sA, yb, yb);
             wsync();
             STAMP(9);
             if (!lo && own) {
 #pragma unroll
                 for (int i = 0; i < NU; ++i) {
                     const int ci = k * NU + i;
-                    vb[ci] = -rd[ci] - (vb[ci] + rho[2 * i] - rho[2 * i + 1]);
+                    vb[ci] = -rd[ci] - (bpsi3<NX, NU>(sB, yb, k, i) + rho[2 * i] - rho[2 * i + 1]);
                 }
             }
             wsync();
