@@ -83,9 +83,9 @@ __host__ __device__ inline Lds3 lds3_layout(int N) {
 
 // x_0 = x0 (LDS, or 0), x_{k+1} = A_k x_k + B_k u_k.  Lane (l & 15) = s < NX of every row of
 // 16 carries x_s (the rows are duplicates; lanes with s >= NX duplicate x_0); x_t reaches the
-// row by DPP row_newbcast.  The next stage's A row and B u term are fetched while the current
-// stage computes, into ping-pong registers (unrolled by two: no copies, no branches; the
-// fetch index is clamped instead of guarded).  Every lane stores: duplicates write equal values.
+// row by DPP row_newbcast.  A stage's A row and B u term are fetched two stages ahead into
+// rotating register sets (unrolled by three: no copies, no branches; the fetch index is clamped
+// instead of guarded).  Every lane stores: duplicates write equal values.
 template <int NX, int NU>
 __device__ __forceinline__ void fwd3(int l, int N, const double* A, const double* B, const double* x0,
                                      const double* U, double* X) {
@@ -94,21 +94,23 @@ __device__ __forceinline__ void fwd3(int l, int N, const double* A, const double
     double xr = x0 ? x0[s] : 0.0;
     X[s] = xr;
     if (N <= 0) return;
-    // the fetch only loads: the B u product is formed in the step, so the loads' wait lands at
-    // the step that consumes them (one stage later), not right behind the loads
+    // B_k u_k of every stage first, in parallel (off the chain), into X_{k+1}'s slot; the
+    // recursion then adds A_k x_k to it in place (the slot is fetched before it is overwritten)
+    for (int i = l; i < N * NX; i += 64) {
+        const int k = i / NX, r = i - k * NX;
+        double v = 0.0;
+#pragma unroll
+        for (int j = 0; j < NU; ++j) v = fma(B[(k * NX + r) * NU + j], U[k * NU + j], v);
+        X[NX + i] = v;
+    }
+    wsync();
     auto fetch = [&](int k, double* av, double* bv) __attribute__((always_inline)) {
 #pragma unroll
         for (int t = 0; t < NX; ++t) av[t] = A[(k * NX + s) * NX + t];
-#pragma unroll
-        for (int i = 0; i < NU; ++i) {
-            bv[i] = B[(k * NX + s) * NU + i];
-            bv[NU + i] = U[k * NU + i];
-        }
+        bv[0] = X[(k + 1) * NX + s];
     };
     auto step = [&](int k, const double* av, const double* bv) __attribute__((always_inline)) {
-        double v0 = 0.0, v1 = 0.0;
-#pragma unroll
-        for (int i = 0; i < NU; ++i) v0 = fma(bv[i], bv[NU + i], v0);
+        double v0 = bv[0], v1 = 0.0;
         static_for<0, NX>([&](auto t) __attribute__((always_inline)) {
             constexpr int tt = decltype(t)::value;
             if constexpr (tt & 1) v1 = fma(av[tt], bcast16<tt>(xr), v1);
@@ -119,7 +121,7 @@ __device__ __forceinline__ void fwd3(int l, int N, const double* A, const double
     };
     // three register sets, fetched two stages ahead (unrolled by three: no copies; fetch indices
     // clamped, not guarded): a stage's LDS latency hides behind two stages of the chain
-    double a0[NX], a1[NX], a2[NX], b0[2 * NU], b1[2 * NU], b2[2 * NU];
+    double a0[NX], a1[NX], a2[NX], b0[1], b1[1], b2[1];
     fetch(0, a0, b0);
     fetch(1 < N ? 1 : N - 1, a1, b1);
     int k = 0;
@@ -838,6 +840,11 @@ __global__ __launch_bounds__(64, 1) void mpc_ipm3_kernel(const MpcConst c, const
             }
             wsync();
             // ---- forward solve L y = vb (block rows; L_JI tiles in acc, L_JJ in LDS) ----
+            // this lane's row of its row group's inverted diagonal block: the same for every J
+            // (only row group J's result is kept), so it is loaded once, not per block row
+            double Lr[16];
+#pragma unroll
+            for (int cc = 0; cc < 16; ++cc) Lr[cc] = Lme[(l & 15) * 17 + cc];
 #pragma unroll
             for (int J = 0; J < T; ++J) {
                 double pr4[4] = {0.0, 0.0, 0.0, 0.0};
@@ -858,9 +865,6 @@ __global__ __launch_bounds__(64, 1) void mpc_ipm3_kernel(const MpcConst c, const
                 }
                 double rv = 0.0;
                 if ((l >> 4) == J) rv = vb[J * 16 + (l & 15)] - (J > 0 ? red[l & 15] : 0.0);
-                double Lr[16];
-#pragma unroll
-                for (int cc = 0; cc < 16; ++cc) Lr[cc] = Lme[(l & 15) * 17 + cc];
                 {  // y_J = L_JJ^{-1} r_J: row J broadcasts its lanes, four independent fma chains
                     double y4[4] = {0.0, 0.0, 0.0, 0.0};
                     static_for<0, 16>([&](auto jc) __attribute__((always_inline)) {
@@ -873,6 +877,9 @@ __global__ __launch_bounds__(64, 1) void mpc_ipm3_kernel(const MpcConst c, const
                 wsync();
             }
             // ---- backward solve L' x = y ----
+            double Lc[16];  // column of the inverted diagonal block, loaded once (as Lr)
+#pragma unroll
+            for (int cc = 0; cc < 16; ++cc) Lc[cc] = Lme[cc * 17 + (l & 15)];
 #pragma unroll
             for (int J = T - 1; J >= 0; --J) {
                 double p = 0.0;
@@ -883,9 +890,6 @@ __global__ __launch_bounds__(64, 1) void mpc_ipm3_kernel(const MpcConst c, const
                         p = fma(acc[I * (I + 1) / 2 + J][r], vb[I * 16 + (l >> 4) + 4 * r], p);
                 if (J + 1 < T) p = sum_groups(p);
                 double rv = ((l >> 4) == J) ? vb[J * 16 + (l & 15)] - p : 0.0;
-                double Lc[16];
-#pragma unroll
-                for (int cc = 0; cc < 16; ++cc) Lc[cc] = Lme[cc * 17 + (l & 15)];
                 {  // x_J = L_JJ^{-T} r_J
                     double x4[4] = {0.0, 0.0, 0.0, 0.0};
                     static_for<0, 16>([&](auto jc) __attribute__((always_inline)) {
