@@ -562,7 +562,9 @@ __global__ __launch_bounds__(64, 1) void mpc_ipm3_kernel(const MpcConst c, const
                 }
             };
             fetchA(0, a0);
-            auto stage = [&](auto tau_c, int kk, const double* av) __attribute__((always_inline)) {
+            // W_k is loaded first, then the next stage's A (pf): LDS returns in order, so W_k's wait
+            // (after the Gamma chain) does not include the prefetch
+            auto stage = [&](auto tau_c, int kk, const double* av, auto pf) __attribute__((always_inline)) {
                 constexpr int tau = decltype(tau_c)::value;
                 const double* Ak = sA + kk * NX * NX;
                 const double* Wk = sW + kk * NX * NX;
@@ -571,6 +573,8 @@ __global__ __launch_bounds__(64, 1) void mpc_ipm3_kernel(const MpcConst c, const
 #pragma unroll
                     for (int i = 0; i < PA; ++i) wk[i] = Wk[i];
                 }
+                pf();
+                __builtin_amdgcn_sched_barrier(0);
                 auto A_ = [&](int i) __attribute__((always_inline)) {
                     if constexpr (kPf) return av[i];
                     else return Ak[i];
@@ -623,14 +627,13 @@ __global__ __launch_bounds__(64, 1) void mpc_ipm3_kernel(const MpcConst c, const
                 const int ke = ke0 < N ? ke0 : N;
                 int kk = kb;
                 for (; kk + 1 < ke; kk += 2) {
-                    fetchA(kk + 1, a1);
-                    stage(tau_c, kk, a0);
-                    fetchA(kk + 2 < N ? kk + 2 : N - 1, a0);
-                    stage(tau_c, kk + 1, a1);
+                    stage(tau_c, kk, a0, [&]() __attribute__((always_inline)) { fetchA(kk + 1, a1); });
+                    stage(tau_c, kk + 1, a1,
+                          [&]() __attribute__((always_inline)) { fetchA(kk + 2 < N ? kk + 2 : N - 1, a0); });
                 }
                 if (kk < ke) {
-                    fetchA(kk + 1 < N ? kk + 1 : N - 1, a1);
-                    stage(tau_c, kk, a0);
+                    stage(tau_c, kk, a0,
+                          [&]() __attribute__((always_inline)) { fetchA(kk + 1 < N ? kk + 1 : N - 1, a1); });
 #pragma unroll
                     for (int i = 0; i < PA; ++i) a0[i] = a1[i];
                 }
