@@ -1296,12 +1296,20 @@ static int solve_one(const shared_t* S, const agent_t* a, double tol, int max_it
                 for (int r = 0; r < m; ++r)
                     if (wk->act[r]) mu_aff += (t[r] + al * dt[r]) * (lam[r] + al * dl[r]);
                 mu_aff /= mact ? mact : 1;
+#ifdef SIGMA_EXP
+                sig_c = mu > 0 ? pow(mu_aff / mu, SIGMA_EXP) : 0.0;
+#else
                 sig_c = mu > 0 ? pow(mu_aff / mu, 3.0) : 0.0;
+#endif
 #ifdef SHORT_STEP
                 if (alpha_prev < SHORT_STEP) sig_c = fmax(sig_c, SIGMA_MIN);
 #endif
             } else {
+#ifdef ETA_ADAPT
+                al = fmax(0.995, 1.0 - ETA_ADAPT * mu) * al;
+#else
                 al = 0.995 * al;
+#endif
 #ifdef RETRY_SIGMA
                 const double al_free = al > 1.0 ? 1.0 : al;
 #endif
