@@ -82,6 +82,9 @@ static void adjoint(const shared_t* S, const agent_t* a, const double* ybar, dou
 /* NaN-propagating max (fmax would drop a NaN residual and report convergence) */
 static double nmax(double a, double b) { return (a > b || a != a) ? a : b; }
 
+#ifdef GONDZIO
+long cmpc_gz_solves = 0; /* lab: corrector solves performed */
+#endif
 #ifndef NBHD_GAMMA
 #define NBHD_GAMMA 0.01 /* wide-neighbourhood floor: t_r lambda_r >= gamma mu after a step */
 #endif
@@ -996,6 +999,18 @@ static int solve_one(const shared_t* S, const agent_t* a, double tol, int max_it
 #ifdef SHORT_STEP
     double alpha_prev = 1.0;
 #endif
+#ifdef GONDZIO
+    /* lab: Gondzio centrality correctors (up to GONDZIO per iteration) on the Mehrotra direction */
+    long gz_used = 0;
+    double* gz_corr = calloc((size_t)m, sizeof(double));
+    double* gz_save = malloc(sizeof(double) * ((size_t)n + (size_t)(N + 1) * nx + (size_t)N * ns + 2 * (size_t)m));
+#ifndef GZ_DA
+#define GZ_DA 0.2
+#endif
+#ifndef GZ_TRIG
+#define GZ_TRIG 0.9
+#endif
+#endif
     for (it = 1; it <= max_iter; ++it) {
         /* ---- residuals ---- */
         double* ybar = wk->ybar;
@@ -1167,11 +1182,18 @@ static int solve_one(const shared_t* S, const agent_t* a, double tol, int max_it
 #ifdef RETRY_SIGMA
         int retried = 0;
 #endif
+#ifdef GONDZIO
+        int gz_n = 0; double gz_al = 0.0;
+        memset(gz_corr, 0, sizeof(double) * m);
+#endif
         for (int pass = 0; pass < 2; ++pass) {
             for (int r = 0; r < m; ++r) {
                 if (!wk->act[r]) { wk->rho[r] = 0.0; continue; }
                 double rc = -t[r] * lam[r];
                 if (pass) rc += sig_c * mu - wk->dt_a[r] * wk->dl_a[r];
+#ifdef GONDZIO
+                if (pass) rc += gz_corr[r];
+#endif
                 wk->rho[r] = (rc + lam[r] * wk->rp[r]) / t[r];
             }
             /* rho~ (stable form) */
@@ -1305,6 +1327,41 @@ static int solve_one(const shared_t* S, const agent_t* a, double tol, int max_it
                 if (alpha_prev < SHORT_STEP) sig_c = fmax(sig_c, SIGMA_MIN);
 #endif
             } else {
+#ifdef GONDZIO
+                {
+                    const size_t nX = (size_t)(N + 1) * nx, nS = (size_t)N * ns;
+                    double* sv = gz_save;
+                    if (gz_n > 0 && al < gz_al + 0.1 * GZ_DA) {
+                        /* the correction did not lengthen the step enough: back to the saved direction */
+                        memcpy(wk->dU, sv, sizeof(double) * n); sv += n;
+                        memcpy(wk->dX, sv, sizeof(double) * nX); sv += nX;
+                        memcpy(wk->dsig, sv, sizeof(double) * nS); sv += nS;
+                        memcpy(dt, sv, sizeof(double) * m); sv += m;
+                        memcpy(dl, sv, sizeof(double) * m);
+                        al = gz_al;
+                    } else if (gz_n < GONDZIO && al < GZ_TRIG) {
+                        memcpy(sv, wk->dU, sizeof(double) * n); sv += n;
+                        memcpy(sv, wk->dX, sizeof(double) * nX); sv += nX;
+                        memcpy(sv, wk->dsig, sizeof(double) * nS); sv += nS;
+                        memcpy(sv, dt, sizeof(double) * m); sv += m;
+                        memcpy(sv, dl, sizeof(double) * m);
+                        const double at = fmin(1.0, al + GZ_DA), mt = sig_c * mu;
+                        for (int r = 0; r < m; ++r) {
+                            if (!wk->act[r]) continue;
+                            const double v = (t[r] + at * dt[r]) * (lam[r] + at * dl[r]);
+                            double c = 0.0;
+                            if (v < 0.1 * mt) c = 0.1 * mt - v;
+                            else if (v > 10.0 * mt) c = fmax(10.0 * mt - v, -10.0 * mt);
+                            gz_corr[r] += c;
+                        }
+                        gz_al = al;
+                        ++gz_n;
+                        ++gz_used;
+                        pass = 0;
+                        continue;
+                    }
+                }
+#endif
 #ifdef ETA_ADAPT
                 al = fmax(0.995, 1.0 - ETA_ADAPT * mu) * al;
 #else
@@ -1363,6 +1420,12 @@ static int solve_one(const shared_t* S, const agent_t* a, double tol, int max_it
             }
         }
     }
+#ifdef GONDZIO
+#pragma omp atomic
+    cmpc_gz_solves += gz_used;
+    free(gz_corr);
+    free(gz_save);
+#endif
     if (it > max_iter) it = max_iter;
     int status;
     if (stop == 1) {

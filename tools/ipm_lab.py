@@ -108,7 +108,8 @@ def run(flag_sets):
             lerr = max(lerr, float(np.abs(z - zref).max()))
             lit += it.tolist()
             lbad += int((st != 1).sum())
-        print(f"[{flags or 'base'}] DI rounds: sum(max it) {sum(mx)} max {max(mx)} mean {np.mean(mean):.2f} "
+        gz = ct.c_long.in_dll(CO._LIB, "cmpc_gz_solves").value if "GONDZIO" in flags else 0
+        print(f"[{flags or 'base'}] corrector solves {gz} DI rounds: sum(max it) {sum(mx)} max {max(mx)} mean {np.mean(mean):.2f} "
               f"unsolved {bad} |dz vs base| {dz} | LPV: max err {lerr:.1e} iters sum {sum(lit)} max {max(lit)} "
               f"not-solved {lbad}", flush=True)
 
