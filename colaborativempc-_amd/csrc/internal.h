@@ -68,6 +68,14 @@ constexpr int kStallIters = 3;
 // slowest agent's iteration count drops 1951 -> 1801 (the kernel time follows the slowest
 // agent) with no max-iteration agent (floors 0.4 and 0.7 each had one); mean 9.39 -> 9.32.
 constexpr double kT0Floor = 0.5;
+// Stall guard: after an iteration whose step was below kShortStep, the corrector's centring
+// parameter is at least kSigmaMin.  On the BASELINE cfg5 population (N=50, nx=6 nu=3) about 1
+// agent in 10^4 otherwise stalls at steps ~1e-3, blocked by a terminal collision row, and runs
+// to max_iter (tools/cfg5_diag.py: 21 such agents in 10 rounds; with the guard 0, all at most
+// 43 iterations); the cfg3 rounds and every captured reference QP never trigger it (identical
+// iterates, tools/ipm_lab.py).
+constexpr double kShortStep = 0.02;
+constexpr double kSigmaMin = 0.5;
 enum { kStopMaxIter = 0, kStopConverged = 1, kStopBreakdown = 2, kStopStalled = 3, kStopNonFinite = 4 };
 
 // Per-agent status of a solve that ended without meeting the tolerance (best merit best_m).

@@ -295,6 +295,7 @@ __global__ __launch_bounds__(kWave) void mpc_ipm_kernel(const MpcConst c, const 
     double best_m = INFINITY, best_kkt = INFINITY;
     int best_it = 0, stop = kStopMaxIter, it;
     double kkt = INFINITY;
+    double alpha_prev = 1;  // step of the previous iteration (kShortStep guard)
     for (it = 1; it <= c.max_iter; ++it) {
         // ================= residuals =================
         for (int i = l; i < (N + 1) * nx; i += kWave) {
@@ -588,6 +589,7 @@ __global__ __launch_bounds__(kWave) void mpc_ipm_kernel(const MpcConst c, const 
                 const double mu_aff = wave_sum(mua_l) / mact;
                 const double ratio = mu > 0.0 ? mu_aff / mu : 0.0;
                 sig_c = ratio * ratio * ratio;
+                if (alpha_prev < kShortStep) sig_c = fmax(sig_c, kSigmaMin);
             } else {
                 alpha = fmin(1.0, 0.995 * amax);
                 // stay in the wide neighbourhood t_r lam_r >= gamma mu(alpha) (see kNbhdGamma)
@@ -605,6 +607,7 @@ __global__ __launch_bounds__(kWave) void mpc_ipm_kernel(const MpcConst c, const 
             }
         }
         // ---- update (corrector direction: dU, dX, dsig, (rho, rt) = (dt, dl)) ----
+        alpha_prev = alpha;
         for (int i = l; i < n; i += kWave) U[i] = fma(alpha, dU[i], U[i]);
         for (int i = l; i < N * ns; i += kWave) sig[i] = fma(alpha, dsig[i], sig[i]);
         for (int i = l; i < (N + 1) * nx; i += kWave) X[i] = fma(alpha, dX[i], X[i]);

@@ -354,6 +354,7 @@ __global__ __launch_bounds__(64, 1) void mpc_ipm3_kernel(const MpcConst c, const
     double kkt = INFINITY;
     double Dsig[NS] = {1.0, 1.0, 1.0}, rsig[NS] = {0.0, 0.0, 0.0}, dsg[NS] = {0.0, 0.0, 0.0};
     v4d acc[NT];
+    double alpha_prev = 1;  // step of the previous iteration (kShortStep guard)
     for (it = 1; it <= c.max_iter; ++it) {
         // Opaque zero: the lane-index arithmetic and lane masks below are recomputed inside the
         // iteration instead of being hoisted out of it by LICM (hoisted, they held hundreds of
@@ -949,6 +950,7 @@ __global__ __launch_bounds__(64, 1) void mpc_ipm3_kernel(const MpcConst c, const
                 const double mu_aff = wave_sum(mua_l) / mact;
                 const double ratio = mu > 0.0 ? mu_aff / mu : 0.0;
                 sig_c = ratio * ratio * ratio;
+                if (alpha_prev < kShortStep) sig_c = fmax(sig_c, kSigmaMin);
                 STAMP(12);
             } else {
                 alpha = fmin(1.0, 0.995 * amax);
@@ -979,6 +981,7 @@ __global__ __launch_bounds__(64, 1) void mpc_ipm3_kernel(const MpcConst c, const
                 STAMP(12);
             }
         }
+        alpha_prev = alpha;
         for (int i = l; i < n; i += 64) U[i] = fma(alpha, dU[i], U[i]);
         for (int i = l; i < (N + 1) * NX; i += 64) X[i] = fma(alpha, dX[i], X[i]);
         wsync();

@@ -256,6 +256,7 @@ __global__ __launch_bounds__(kWgThreads) void mpc_ipm_wg_kernel(const MpcConst c
 
     R best_m = R(INFINITY), best_kkt = R(INFINITY), kkt = R(INFINITY);
     int best_it = 0, stop = kStopMaxIter, it;
+    R alpha_prev = 1;  // step of the previous iteration (kShortStep guard)
     for (it = 1; it <= c.max_iter; ++it) {
         // ================= residuals =================
         for (int i = tid; i < (N + 1) * nx; i += kWgThreads) {
@@ -543,6 +544,7 @@ __global__ __launch_bounds__(kWgThreads) void mpc_ipm_wg_kernel(const MpcConst c
                 const R mu_aff = red.sum(mua_l) / mact;
                 const R ratio = mu > 0 ? mu_aff / mu : R(0);
                 sig_c = ratio * ratio * ratio;
+                if (alpha_prev < R(kShortStep)) sig_c = fmax(sig_c, R(kSigmaMin));
             } else {
                 alpha = fmin(R(1), R(0.995) * amax);
                 for (int bt = 0; bt < kMaxBacktrack; ++bt) {
@@ -559,6 +561,7 @@ __global__ __launch_bounds__(kWgThreads) void mpc_ipm_wg_kernel(const MpcConst c
                 }
             }
         }
+        alpha_prev = alpha;
         for (int i = tid; i < n; i += kWgThreads) U[i] = fma(alpha, dU[i], U[i]);
         for (int i = tid; i < N * ns; i += kWgThreads) sig[i] = fma(alpha, dsig[i], sig[i]);
         for (int i = tid; i < (N + 1) * nx; i += kWgThreads) X[i] = fma(alpha, dX[i], X[i]);

@@ -1064,6 +1064,7 @@ __global__ __launch_bounds__(kWave) void mpc_riccati_kernel(const MpcConst c_arg
     int best_it = 0, stop = kStopMaxIter, it;
     double kkt = INFINITY;
     RSTAMP(14);
+    double alpha_prev = 1;  // step of the previous iteration (kShortStep guard)
     for (it = 1; it <= c.max_iter; ++it) {
         // ================= residuals (as mpc_ipm.hip) =================
         for (int i = l; i < (N + 1) * nx; i += kWave) {
@@ -1280,6 +1281,7 @@ __global__ __launch_bounds__(kWave) void mpc_riccati_kernel(const MpcConst c_arg
                 const double mu_aff = wave_sum(mua_l) / mact;
                 const double ratio = mu > 0.0 ? mu_aff / mu : 0.0;
                 sig_c = ratio * ratio * ratio;
+                if (alpha_prev < kShortStep) sig_c = fmax(sig_c, kSigmaMin);
             } else {
                 alpha = fmin(1.0, 0.995 * amax);
                 // stay in the wide neighbourhood t_r lam_r >= gamma mu(alpha) (see kNbhdGamma)
@@ -1298,6 +1300,7 @@ __global__ __launch_bounds__(kWave) void mpc_riccati_kernel(const MpcConst c_arg
             RSTAMP(7);
         }
         // ---- update (corrector direction: dU, dX, dsig, (rho, rt) = (dt, dl)) ----
+        alpha_prev = alpha;
         for (int i = l; i < n; i += kWave) U[i] = fma(alpha, dU[i], U[i]);
         for (int i = l; i < N * ns; i += kWave) sig[i] = fma(alpha, dsig[i], sig[i]);
         for (int i = l; i < (N + 1) * nx; i += kWave) X[i] = fma(alpha, dX[i], X[i]);

@@ -85,6 +85,14 @@ static double nmax(double a, double b) { return (a > b || a != a) ? a : b; }
 #ifdef GONDZIO
 long cmpc_gz_solves = 0; /* lab: corrector solves performed */
 #endif
+/* after a step shorter than SHORT_STEP the next corrector centres with sigma >= SIGMA_MIN
+   (kernels: kShortStep, kSigmaMin in internal.h) */
+#ifndef SHORT_STEP
+#define SHORT_STEP 0.02
+#endif
+#ifndef SIGMA_MIN
+#define SIGMA_MIN 0.5
+#endif
 #ifndef NBHD_GAMMA
 #define NBHD_GAMMA 0.01 /* wide-neighbourhood floor: t_r lambda_r >= gamma mu after a step */
 #endif
@@ -996,9 +1004,7 @@ static int solve_one(const shared_t* S, const agent_t* a, double tol, int max_it
     double *bU = wk->bU, *bsig = wk->bsig;
     int it;
     double kkt = INFINITY;
-#ifdef SHORT_STEP
-    double alpha_prev = 1.0;
-#endif
+    double alpha_prev = 1.0; /* step of the previous iteration (kShortStep rule) */
 #ifdef GONDZIO
     /* lab: Gondzio centrality correctors (up to GONDZIO per iteration) on the Mehrotra direction */
     long gz_used = 0;
@@ -1323,9 +1329,7 @@ static int solve_one(const shared_t* S, const agent_t* a, double tol, int max_it
 #else
                 sig_c = mu > 0 ? pow(mu_aff / mu, 3.0) : 0.0;
 #endif
-#ifdef SHORT_STEP
-                if (alpha_prev < SHORT_STEP) sig_c = fmax(sig_c, SIGMA_MIN);
-#endif
+                if (alpha_prev < SHORT_STEP) sig_c = fmax(sig_c, SIGMA_MIN); /* kShortStep / kSigmaMin */
             } else {
 #ifdef GONDZIO
                 {
@@ -1409,9 +1413,7 @@ static int solve_one(const shared_t* S, const agent_t* a, double tol, int max_it
                     continue;
                 }
 #endif
-#ifdef SHORT_STEP
                 alpha_prev = al;
-#endif
                 for (int c = 0; c < n; ++c) U[c] += al * wk->dU[c];
                 for (int q = 0; q < N * ns; ++q) sig[q] += al * wk->dsig[q];
                 for (int r = 0; r < m; ++r)
