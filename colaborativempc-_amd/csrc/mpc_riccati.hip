@@ -72,9 +72,12 @@ struct Dims {
 // (KP) and, when nonzero, the state / input / rows-per-stage counts.  With the dimensions
 // fixed the stage loops unroll and their independent loads issue together — the sweeps are
 // serial chains of short steps on one wavefront, so latency is all that counts.
-template <int KP_, int NX_, int NU_, int MC_>
+// GR: the six lane-owned row vectors (t, lam, w, rp, rho, GdU) live in the global scratch
+// instead of LDS (r_rows_global): fewer LDS bytes per wave, more waves per CU.
+template <int KP_, int NX_, int NU_, int MC_, bool GR_ = false>
 struct Cfg {
     static constexpr int KP = KP_, NX = NX_, NU = NU_, MC = MC_;
+    static constexpr bool GR = GR_;
     // values per lane of the [A | B | W] images of the factor and residual sweeps
     static constexpr int KPW = NX_ ? (2 * NX_ * NX_ + NX_ * NU_ + kWave - 1) / kWave
                                    : (2 * CMPC_MAX_NX * CMPC_MAX_NX + CMPC_MAX_NX * CMPC_MAX_NU + kWave - 1) / kWave;
@@ -115,7 +118,7 @@ __device__ __forceinline__ Dims dims_t(const MpcConst& c) {
 template <class G>
 __device__ __forceinline__ int mc_t(const MpcConst& c) { return G::MC ? G::MC : c.mc; }
 
-__host__ __device__ inline RLds r_layout(const MpcConst& c) {
+__host__ __device__ inline RLds r_layout_ex(const MpcConst& c, bool gr) {
     const Dims d = dims_of(c);
     RLds L;
     int o = 0;
@@ -125,14 +128,15 @@ __host__ __device__ inline RLds r_layout(const MpcConst& c) {
         return r;
     };
     const int m = c.m, n = c.n, N = c.N, nx = c.nx, ns = c.ns;
-    L.t = take(m);
-    L.lam = take(m);
+    const int mr = gr ? 0 : m;  // lane-owned rows: LDS, or (gr) the global scratch (r_glb)
+    L.t = take(mr);
+    L.lam = take(mr);
     L.th = take(m);
-    L.rp = take(m);
-    L.rho = take(m);
+    L.rp = take(mr);
+    L.rho = take(mr);
     L.rt = take(m);
-    L.w = take(m);
-    L.GdU = take(m);
+    L.w = take(mr);
+    L.GdU = take(mr);
     L.X = take((N + 1) * nx);
     L.dX = take((N + 1) * nx);
     L.yb = take((N + 1) * nx);
@@ -170,10 +174,25 @@ __host__ __device__ inline RLds r_layout(const MpcConst& c) {
     return L;
 }
 
+// Row vectors in the global scratch when that lifts the waves per CU (LDS-bound; the VGPR
+// budget of these kernels, > 256 per lane, caps it at one wave per SIMD = 4 per CU) and the
+// dimensions have a GR instantiation (BASELINE cfg5: nx 6, nu 3, 6 rows per stage; 67 KB ->
+// 39 KB of LDS at N = 50, 2 -> 4 waves per CU).
+__host__ __device__ inline bool r_rows_global(const MpcConst& c) {
+    if (!(c.nx == 6 && c.nu == 3 && c.mc == 6)) return false;
+    auto waves = [](int dbl) {
+        const int w = (int)(kMaxLdsBytes / (sizeof(double) * (size_t)dbl));
+        return w < 4 ? w : 4;
+    };
+    return waves(r_layout_ex(c, true).total) > waves(r_layout_ex(c, false).total);
+}
+
+__host__ __device__ inline RLds r_layout(const MpcConst& c) { return r_layout_ex(c, r_rows_global(c)); }
+
 // per-agent global scratch (doubles): predictor direction (dt, dl), Riccati factors, stage
 // weights W_k = 2Q + M_k of the state X_{k+1}, best iterate
 struct RGlb {
-    size_t dta, dla, F, Wk, bU, bsig, total;
+    size_t dta, dla, F, Wk, bU, bsig, t, lam, w, rp, rho, GdU, total;
 };
 
 __host__ __device__ inline RGlb r_glb(const MpcConst& c) {
@@ -191,6 +210,13 @@ __host__ __device__ inline RGlb r_glb(const MpcConst& c) {
     g.Wk = take((size_t)c.N * c.nx * c.nx);
     g.bU = take(c.n);
     g.bsig = take((size_t)c.N * c.ns);
+    const size_t mr = r_rows_global(c) ? c.m : 0;  // see RLds / r_rows_global
+    g.t = take(mr);
+    g.lam = take(mr);
+    g.w = take(mr);
+    g.rp = take(mr);
+    g.rho = take(mr);
+    g.GdU = take(mr);
     g.total = o;
     return g;
 }
@@ -987,14 +1013,18 @@ __global__ __launch_bounds__(kWave) void mpc_riccati_kernel(const MpcConst c_arg
     double* bsig = ws + gl.bsig;
     double* Wg = ws + gl.Wk;
 
-    double* t = sm + L.t;
-    double* lam = sm + L.lam;
+    constexpr bool GR = G::GR;  // lane-owned rows in the global scratch (cross-lane reads: gsync)
+    double* t = GR ? ws + gl.t : sm + L.t;
+    double* lam = GR ? ws + gl.lam : sm + L.lam;
     double* th = sm + L.th;
-    double* rp = sm + L.rp;
-    double* rho = sm + L.rho;
+    double* rp = GR ? ws + gl.rp : sm + L.rp;
+    double* rho = GR ? ws + gl.rho : sm + L.rho;
     double* rt = sm + L.rt;
-    double* w = sm + L.w;
-    double* GdU = sm + L.GdU;
+    double* w = GR ? ws + gl.w : sm + L.w;
+    double* GdU = GR ? ws + gl.GdU : sm + L.GdU;
+    auto rsync = [&]() {
+        if constexpr (GR) gsync(); else wsync();
+    };
     double* X = sm + L.X;
     double* dX = sm + L.dX;
     double* yb = sm + L.yb;
@@ -1058,7 +1088,7 @@ __global__ __launch_bounds__(kWave) void mpc_riccati_kernel(const MpcConst c_arg
     }
     const double mact = fmax(wave_sum(mact_l), 1.0);
     const double scale_p = wave_max(sp_l);
-    wsync();
+    rsync();  // lam: read across lanes by the residuals
 
     double best_m = INFINITY, best_kkt = INFINITY;
     int best_it = 0, stop = kStopMaxIter, it;
@@ -1178,7 +1208,7 @@ __global__ __launch_bounds__(kWave) void mpc_riccati_kernel(const MpcConst c_arg
                 if (pass) rc += sig_c * mu - dta[r] * dla[r];
                 rho[r] = (rc + lam[r] * rp[r]) / t[r];
             }
-            wsync();
+            rsync();  // rho: read across lanes (same-stage rows, slack directions)
             for (int r = l; r < m; r += kWave) {
                 double v = rho[r];
                 if (r < ms) {
@@ -1237,7 +1267,7 @@ __global__ __launch_bounds__(kWave) void mpc_riccati_kernel(const MpcConst c_arg
                 RSTAMP(6);
             }
             for (int r = l; r < m; r += kWave) GdU[r] = row_value<G>(c, C, r, dX, dU, nullptr);
-            wsync();
+            rsync();  // GdU: read across lanes by the slack directions
             for (int i = l; i < N * ns; i += kWave) {
                 const int k = i / ns, j = i - k * ns;
                 double v = rsig[i];
@@ -1309,7 +1339,7 @@ __global__ __launch_bounds__(kWave) void mpc_riccati_kernel(const MpcConst c_arg
                 t[r] = fma(alpha, rho[r], t[r]);
                 lam[r] = fma(alpha, rt[r], lam[r]);
             }
-        wsync();
+        rsync();  // lam: read across lanes by the next residuals
         RSTAMP(8);
     }
     if (it > c.max_iter) it = c.max_iter;
@@ -1380,7 +1410,8 @@ hipError_t mpc_riccati_launch(const MpcConst& c, const MpcPtrs& p, int batch, hi
     else if (c.nx == 9 && c.nu == 2 && c.mc == 6) e = go(Cfg<kPerSmall, 9, 2, 6>{});
     else if (c.nx == 9 && c.nu == 2 && c.mc == 7) e = go(Cfg<kPerSmall, 9, 2, 7>{});
     else if (c.nx == 4 && c.nu == 2) e = go(Cfg<kPerSmall, 4, 2, 0>{});
-    else if (c.nx == 6 && c.nu == 3 && c.mc == 6) e = go(Cfg<kPerSmall, 6, 3, 6>{});   // BASELINE cfg5
+    else if (c.nx == 6 && c.nu == 3 && c.mc == 6)   // BASELINE cfg5
+        e = r_rows_global(c) ? go(Cfg<kPerSmall, 6, 3, 6, true>{}) : go(Cfg<kPerSmall, 6, 3, 6>{});
     else if (small) e = go(Cfg<kPerSmall, 0, 0, 0>{});
     else e = go(Cfg<kPerMax, 0, 0, 0>{});
     if (e != hipSuccess) return e;
