@@ -82,6 +82,9 @@ static void adjoint(const shared_t* S, const agent_t* a, const double* ybar, dou
 /* NaN-propagating max (fmax would drop a NaN residual and report convergence) */
 static double nmax(double a, double b) { return (a > b || a != a) ? a : b; }
 
+#ifdef DD_COUNT
+long cmpc_dd_iters = 0; /* lab: double-double iterations */
+#endif
 #ifdef GONDZIO
 long cmpc_gz_solves = 0; /* lab: corrector solves performed */
 #endif
@@ -1116,6 +1119,12 @@ static int solve_one(const shared_t* S, const agent_t* a, double tol, int max_it
                 double thm = 0.0;
                 for (int r = 0; r < m; ++r) if (wk->act[r] && wk->th[r] > thm) thm = wk->th[r];
                 hp = thm > RIC_DD_TH;
+#ifdef DD_COUNT
+                if (hp) {
+#pragma omp atomic
+                    cmpc_dd_iters += 1;
+                }
+#endif
             }
 #ifdef RIC_QUAD
             if (ric_factor_q(S, a, wk->th, wk->Dsig, wk->F)) { stop = 2; break; }

@@ -1,6 +1,7 @@
 """Diagnostic: per-section shader-clock breakdown of the Riccati kernel (mpc_riccati.hip) on the
 reference's N = 125 captured QPs (tests/golden/lpv_n125_a3.npz), or a synthetic long horizon.
-Usage: python tools/ric_stamps.py [lpv_case] | python tools/ric_stamps.py --di n N"""
+Usage: python tools/ric_stamps.py [lpv_case] | python tools/ric_stamps.py --cfg5 [agents]
+(--cfg5: the first round of the BASELINE cfg5 population, N = 50, nx 6, nu 3; means over agents)"""
 import os
 import sys
 import time
@@ -61,5 +62,36 @@ def lpv(name):
                ms)
 
 
+def cfg5(agents):
+    from cmpc import scenarios as S
+    from cmpc.rounds import DIRounds
+
+    R = DIRounds(S.make_di(agents, 50, 2, 3))
+    R.build()
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
+    ev[0].record()
+    R.solve()
+    ev[1].record()
+    st = torch.zeros((agents, SLOTS), dtype=torch.int64, device="cuda")
+    plain = R.opts
+    R.opts = L.opts(flags=0, stamps=st.data_ptr())
+    ev[2].record()
+    R.solve()
+    ev[3].record()
+    torch.cuda.synchronize()
+    R.opts = plain
+    a = st.cpu().numpy().astype(np.float64)
+    it = a[:, SLOTS - 1]
+    print(f"cfg5 {agents} agents: kernel {ev[0].elapsed_time(ev[1]):.2f} ms (stamped {ev[2].elapsed_time(ev[3]):.2f} ms); "
+          f"iterations mean {it.mean():.2f} max {int(it.max())}; dd iterations {int(a[:, 12].sum())}")
+    tot = a[:, list(NAMES)].sum(1)
+    for k, nm in NAMES.items():
+        print(f"  {nm:34s} {a[:, k].sum() / it.sum() / 1e3:9.1f}k clk/iter  {a[:, k].sum() / tot.sum() * 100:5.1f} %")
+    print(f"  {'total':34s} {tot.sum() / it.sum() / 1e3:9.1f}k clk/iter; slowest agent {tot.max() / 1e6:.2f}M clk")
+
+
 if __name__ == "__main__":
-    lpv(sys.argv[1] if len(sys.argv) > 1 else "lpv_n125_a3")
+    if len(sys.argv) > 1 and sys.argv[1] == "--cfg5":
+        cfg5(int(sys.argv[2]) if len(sys.argv) > 2 else 8192)
+    else:
+        lpv(sys.argv[1] if len(sys.argv) > 1 else "lpv_n125_a3")
