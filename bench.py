@@ -122,9 +122,10 @@ def main():
     max_err = None
     if rank == 0 and world == 1 and not args.no_cpu:
         cpu, max_err = cpu_baseline(R, args.cpu_seconds)
-    ref_line = None
+    ref_line = osqp_line = None
     if rank == 0 and world == 1 and not args.no_ref and not cfg5:
         ref_line = reference_config(ctx)
+        osqp_line = osqp_dropin(ctx)
 
     if rank == 0:
         out = {
@@ -171,6 +172,7 @@ def main():
             },
             "cpu_baseline": cpu,
             "reference_config": ref_line,
+            "osqp_dropin": osqp_line,
         }
         print(json.dumps(out))
     if world > 1:
@@ -220,6 +222,50 @@ def reference_config(ctx, reps=10):
                         "host arrays)", "steps": steps,
             "reference_ms_per_agent_solve": ref_ms, "reference_ms_per_step_3_agents_sequential": 3 * ref_ms,
             "speedup_vs_reference_step": 3 * ref_ms / worst, "reps": reps}
+
+
+def osqp_dropin(ctx, reps=20):
+    """The literal reference boundary, osqp_solve_qp(P, q, G, h, A, b) (LPV_Planner.py:192-249),
+    timed on the reference-captured N=30 QPs of tests/golden/lpv_n30_a3.npz (3 agents, several
+    closed-loop steps): csr matrices in, (res, feasible) out, as PlannerLPV.solve calls it
+    (LPV_Planner.py:156-157).  One call per QP (host arrays, structure recognition, one
+    structured launch each) and all QPs in one osqp_solve_qp_batch call; z against the
+    KKT-certified optimum."""
+    import scipy.sparse as sp
+
+    import cmpc
+
+    d = np.load(os.path.join(ROOT, "tests", "golden", "lpv_n30_a3.npz"), allow_pickle=False)
+
+    def mat(nm, j):
+        shp = tuple(int(v) for v in d[f"{nm}_{j}_shape"])
+        return sp.csr_matrix((d[f"{nm}_{j}_data"], (d[f"{nm}_{j}_row"], d[f"{nm}_{j}_col"])), shape=shp)
+
+    qps = []
+    for j in range(len(d["step"])):
+        Aall, l, u = mat("A", j), d["l"][j], d["u"][j]
+        eq = np.isfinite(l) & (l == u)
+        qps.append((mat("P", j), d["q"][j], Aall[np.flatnonzero(~eq)], u[~eq], Aall[np.flatnonzero(eq)], u[eq]))
+    out = [cmpc.osqp_solve_qp(*qp, ctx=ctx) for qp in qps]
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        out = [cmpc.osqp_solve_qp(*qp, ctx=ctx) for qp in qps]
+    one_ms = (time.perf_counter() - t0) / (reps * len(qps)) * 1e3
+    cmpc.osqp_solve_qp_batch(qps, ctx=ctx)
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        bat = cmpc.osqp_solve_qp_batch(qps, ctx=ctx)
+    bat_ms = (time.perf_counter() - t0) / reps * 1e3
+    err = max(float(np.abs(r.x - d["z"][j]).max()) for j, (r, _) in enumerate(out))
+    berr = max(float(np.abs(r.x - d["z"][j]).max()) for j, (r, _) in enumerate(bat))
+    return {"workload": f"osqp_solve_qp drop-in on the {len(qps)} reference-captured N=30 agent QPs of "
+                        f"lpv_n30_a3 (nx=9 nu=2, n={qps[0][0].shape[0]} vars, "
+                        f"{qps[0][2].shape[0] + qps[0][4].shape[0]} rows, csr in)",
+            "ms_per_call": one_ms, "batch_call_ms": bat_ms, "qps": len(qps),
+            "status_val": sorted({int(r.info.status_val) for r, _ in out}),
+            "max_kkt": max(float(r.info.kkt) for r, _ in out),
+            "max_abs_err_vs_certified_optimum": err, "batch_max_abs_err_vs_certified_optimum": berr,
+            "reps": reps}
 
 
 def pmc_traffic():
