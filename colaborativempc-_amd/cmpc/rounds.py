@@ -55,11 +55,13 @@ def exchange_positions(traj_all, traj_local, world=1, group=None, comm=None):
 
 class DIRounds:
     def __init__(self, scen, rank=0, world=1, device=None, ctx=None, tol=None, max_iter=None, group=None,
-                 fp32=False, comm=None):
+                 fp32=False, comm=None, fused=True):
         import torch
 
         self.torch = torch
         self.scen, self.rank, self.world, self.group, self.comm = scen, rank, world, group, comm
+        # step(): rows built inside the solver launch (cmpc_di_solve_dev) instead of build() + solve()
+        self.fused = fused
         if scen.n_agents % world:
             raise ValueError("n_agents must be divisible by the number of ranks")
         self.dev = torch.device("cuda", torch.cuda.current_device() if device is None else device)
@@ -127,6 +129,16 @@ class DIRounds:
                                                              ct.byref(self.data), ct.byref(self.out),
                                                              ct.byref(self.opts), self._stream()))
 
+    def build_solve(self):
+        """build() + solve() as one launch where the v3 kernel covers the problem (the rows go
+        from traj_all straight into the solver's LDS, bit-identical to build()); qlin / C / h are
+        then left untouched — call build() before snapshot() to materialise them."""
+        lib = self.ctx.lib
+        self.ctx.check(lib.cmpc_di_solve_dev(self.ctx.h, ct.byref(self.dprm), ct.byref(self.ddims), _tptr(self.nbr),
+                                             _tptr(self.lane), _tptr(self.traj_all), ct.byref(self.mdims),
+                                             ct.byref(self.w), ct.byref(self.data), ct.byref(self.out),
+                                             ct.byref(self.opts), self._stream()))
+
     def advance(self):
         self.ctx.check(self.ctx.lib.cmpc_di_advance_dev(self.ctx.h, ct.byref(self.dprm), ct.byref(self.ddims),
                                                         _tptr(self.z), _tptr(self.x0), _tptr(self.u_prev),
@@ -136,11 +148,16 @@ class DIRounds:
         exchange_positions(self.traj_all, self.traj_local, self.world, self.group, self.comm)
 
     def step(self, timer=None):
-        """One consensus round.  `timer` (start, stop) events bracket the solve launch."""
-        self.build()
+        """One consensus round.  `timer` (start, stop) events bracket the solve launch (with
+        `fused`, the launch that builds and solves)."""
+        if not self.fused:
+            self.build()
         if timer is not None:
             timer[0].record()
-        self.solve()
+        if self.fused:
+            self.build_solve()
+        else:
+            self.solve()
         if timer is not None:
             timer[1].record()
         self.advance()

@@ -394,6 +394,44 @@ int cmpc_di_build_dev(cmpc_ctx* ctx, const cmpc_di_params* prm, const cmpc_di_di
     return CMPC_OK;
 }
 
+int cmpc_di_solve_dev(cmpc_ctx* ctx, const cmpc_di_params* prm, const cmpc_di_dims* dd, const int* nbr,
+                      const double* lane, const double* traj_all, const cmpc_mpc_dims* dims,
+                      const cmpc_mpc_weights* w, const cmpc_mpc_data* in, const cmpc_mpc_out* out,
+                      const cmpc_opts* opts, void* stream) {
+    if (!ctx) return CMPC_ERR_ARG;
+    if (!lane || !traj_all || !dims || !in || !out || !out->z || (dd && dd->nb > 0 && !nbr))
+        return fail(ctx, CMPC_ERR_ARG, "null argument");
+    cmpc::DiConst dc;
+    int rc = di_const(ctx, prm, dd, &dc);
+    if (rc != CMPC_OK) return rc;
+    cmpc::MpcConst c;
+    const char* msg = nullptr;
+    rc = cmpc::mpc_prepare(dims, w, opts, &c, &msg);
+    if (rc != CMPC_OK) return fail(ctx, rc, msg);
+    if (dims->batch != dd->batch || dims->N != dd->N || dims->nx != dc.nx || dims->nu != dc.nu ||
+        dims->mc != 4 + dd->nb)
+        return fail(ctx, CMPC_ERR_ARG, "double-integrator and solver dimensions differ");
+    if (dims->batch == 0) return CMPC_OK;
+    const int flags = opts ? opts->flags : 0;
+    hipStream_t s = (hipStream_t)stream;
+    if (!c.wg && !c.riccati && !(flags & CMPC_FLAG_GENERIC)) {
+        cmpc::MpcPtrs p{in->A, in->B, in->x0, in->u_prev, nullptr, nullptr, nullptr, out->z, out->kkt, out->iters,
+                        out->status, opts ? (unsigned long long*)opts->stamps : nullptr, nullptr};
+        p.fuse = cmpc::DiFuse{nbr, lane, traj_all, dc, 1};
+        hipError_t e = hipSuccess;
+        if (cmpc::mpc3_try_launch(c, p, dims->batch, s, &e)) {
+            HIP_TRY(e);
+            return CMPC_OK;
+        }
+    }
+    // no fused instantiation for these dimensions: build into data's qlin / C / h, then solve
+    if (!in->qlin || !in->C || !in->h) return fail(ctx, CMPC_ERR_ARG, "unfused round needs qlin / C / h buffers");
+    cmpc::DiPtrs dp{nbr, lane, traj_all, const_cast<double*>(in->qlin), const_cast<double*>(in->C),
+                    const_cast<double*>(in->h)};
+    HIP_TRY(cmpc::di_build_launch(dc, dp, dd->batch, s));
+    return cmpc_solve_mpc_batch_dev(ctx, dims, w, in, out, opts, stream);
+}
+
 int cmpc_di_advance_dev(cmpc_ctx* ctx, const cmpc_di_params* prm, const cmpc_di_dims* d, const double* z,
                         double* x0, double* u_prev, double* traj_local, void* stream) {
     if (!ctx) return CMPC_ERR_ARG;

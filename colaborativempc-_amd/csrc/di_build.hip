@@ -11,54 +11,24 @@
 // exchanged positions <- predicted p_k).  Element-wise per (agent, stage).
 #include <cmath>
 
+#include "di_rows.h"
 #include "internal.h"
 
 namespace cmpc {
 
 __global__ __launch_bounds__(kWave) void di_build_kernel(const DiConst c, const DiPtrs P) {
     const int b = blockIdx.x;
-    const int N = c.N, nb = c.nb, nx = c.nx, mc = 4 + nb, d = c.dim;
-    const int ivx = d, ipy = 1;  // state = [p (dim) | v (dim)]
+    const int N = c.N, nx = c.nx, mc = 4 + c.nb;
     const double lane = P.lane[b];
     const double* own = P.traj_all + (size_t)(c.self_offset + b) * (N + 1) * 2;
-    const int* nbr = P.nbr + (size_t)b * nb;
+    const int* nbr = P.nbr + (size_t)b * c.nb;
     double* qlin = P.qlin + (size_t)b * (N + 1) * nx;
     double* C = P.C + (size_t)b * N * mc * nx;
     double* h = P.h + (size_t)b * N * mc;
     for (int k = threadIdx.x; k <= N; k += kWave) {
-        double* pk = qlin + (size_t)k * nx;
-        for (int s = 0; s < nx; ++s) pk[s] = 0.0;
-        pk[ivx] = -c.v_ref * c.q_v;
-        pk[ipy] = -lane * c.q_lane;
-        if (k == 0) continue;
-        const int h1 = k - 1;
-        double* Ck = C + (size_t)h1 * mc * nx;
-        double* hk = h + (size_t)h1 * mc;
-        for (int i = 0; i < mc * nx; ++i) Ck[i] = 0.0;
-        Ck[0 * nx + ivx] = -1.0; hk[0] = -c.min_vel;
-        Ck[1 * nx + ivx] = 1.0;  hk[1] = c.max_vel;
-        Ck[2 * nx + ipy] = 1.0;  hk[2] = c.hw + lane;
-        Ck[3 * nx + ipy] = -1.0; hk[3] = c.hw - lane;
-        double px = 0.0, py = 0.0;
-        for (int i = 0; i < nb; ++i) {
-            const double* nt = P.traj_all + (size_t)nbr[i] * (N + 1) * 2;
-            const double ex = own[h1 * 2], ey = own[h1 * 2 + 1];
-            const double nx_ = nt[h1 * 2], ny_ = nt[h1 * 2 + 1];
-            const double dx = nx_ - ex, dy = ny_ - ey;
-            const double nrm = sqrt(dx * dx + dy * dy);
-            const double ax = dx / nrm, ay = dy / nrm;
-            const double bb = -0.5 * (ax * (ex + nx_) + ay * (ey + ny_));
-            const double qx = own[k * 2] - nt[k * 2], qy = own[k * 2 + 1] - nt[k * 2 + 1];
-            const double wgt = (2.0 * c.min_dist - sqrt(qx * qx + qy * qy)) / nb;
-            double* cr = Ck + (4 + i) * nx;
-            cr[0] = ax;
-            cr[1] = ay;
-            hk[4 + i] = -c.min_dist / 2 - bb;
-            px = px + c.wq * wgt * ax;
-            py = py + c.wq * wgt * ay;
-        }
-        pk[0] += px;
-        pk[1] += py;
+        const int h1 = k > 0 ? k - 1 : 0;
+        di_stage_rows(c, nbr, lane, P.traj_all, own, k, qlin + (size_t)k * nx, C + (size_t)h1 * mc * nx,
+                      h + (size_t)h1 * mc);
     }
 }
 

@@ -36,6 +36,22 @@ struct MpcConst {
     int row_sign[CMPC_MAX_MC];
 };
 
+struct DiConst {
+    int N, nb, nx, nu, ns, dim, self_offset;
+    double v_ref, q_v, q_lane, hw, min_vel, max_vel, min_dist, wq;
+};
+
+// Fused double-integrator round (cmpc_di_solve_dev): when `on`, the v3 kernel builds each
+// agent's stage rows and linear cost from the exchanged trajectories straight into LDS
+// (di_rows.h, the arithmetic of di_build_kernel) instead of reading qlin / C / h.
+struct DiFuse {
+    const int* nbr;
+    const double* lane;
+    const double* traj_all;
+    DiConst c;
+    int on;
+};
+
 struct MpcPtrs {
     const double* A;
     const double* B;
@@ -50,6 +66,7 @@ struct MpcPtrs {
     int* status;
     unsigned long long* stamps;  // optional: batch x kStampSlots per-section s_memtime counts (v3 kernel)
     double* ws;                  // device scratch, batch x mpc_ws_doubles(c) (Riccati kernel; else unused)
+    DiFuse fuse;                 // fused row build (v3 kernel only; on = 0 elsewhere)
 };
 
 // Interior-point safeguards shared by both solver kernels and the C oracle (oracle/cmpc_oracle.c).
@@ -135,10 +152,6 @@ hipError_t lpv_build_launch(const LpvConst& c, const LpvPtrs& p, int batch, hipS
 hipError_t lpv_mark_launch(const int* err, int* status, double* z, int nz, int batch, hipStream_t s);
 
 // Synthetic double-integrator family (bench workload).
-struct DiConst {
-    int N, nb, nx, nu, ns, dim, self_offset;
-    double v_ref, q_v, q_lane, hw, min_vel, max_vel, min_dist, wq;
-};
 
 struct DiPtrs {
     const int* nbr;

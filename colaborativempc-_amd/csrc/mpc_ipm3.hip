@@ -23,6 +23,7 @@
 //    kept in LDS for the triangular solves.
 #include <cmath>
 
+#include "di_rows.h"
 #include "internal.h"
 #include "wave_ops.h"
 
@@ -263,9 +264,22 @@ __global__ __launch_bounds__(64, 1) void mpc_ipm3_kernel(const MpcConst c, const
         const double* gP = P.p + (size_t)b * (N + 1) * NX;
         for (int i = l; i < N * NX * NX; i += 64) sA[i] = gA[i];
         for (int i = l; i < N * NX * NU; i += 64) sB[i] = gB[i];
-        for (int i = l; i < N * MC * NX; i += 64) sC[i] = gC[i];
-        for (int i = l; i < ms; i += 64) sH[i] = P.h[(size_t)b * ms + i];
-        for (int i = l; i < (N + 1) * NX; i += 64) sP[i] = gP[i];
+        if (P.fuse.on) {
+            // fused round: this agent's rows and linear cost built from the exchanged
+            // trajectories straight into LDS (bit-identical to di_build_kernel's)
+            const DiFuse& F = P.fuse;
+            const double* own = F.traj_all + (size_t)(F.c.self_offset + b) * (N + 1) * 2;
+            const int* nbr = F.nbr + (size_t)b * NB;
+            const double ln = F.lane[b];
+            for (int kk = l; kk <= N; kk += 64) {
+                const int h1 = kk > 0 ? kk - 1 : 0;
+                di_stage_rows(F.c, nbr, ln, F.traj_all, own, kk, sP + kk * NX, sC + h1 * MC * NX, sH + h1 * MC);
+            }
+        } else {
+            for (int i = l; i < N * MC * NX; i += 64) sC[i] = gC[i];
+            for (int i = l; i < ms; i += 64) sH[i] = P.h[(size_t)b * ms + i];
+            for (int i = l; i < (N + 1) * NX; i += 64) sP[i] = gP[i];
+        }
         if (l < NX) sx0[l] = P.x0[(size_t)b * NX + l];
         if (l < NU) sup[l] = P.up[(size_t)b * NU + l];
         for (int i = l; i < NX * NX; i += 64) Q2[i] = 2.0 * c.Q[i];

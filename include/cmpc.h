@@ -245,6 +245,16 @@ int cmpc_di_build_dev(cmpc_ctx* ctx, const cmpc_di_params* prm, const cmpc_di_di
                       const double* traj_all /* n_total x (N+1) x 2 */,
                       double* qlin /* batch x (N+1) x nx */, double* C /* batch x N x (4+nb) x nx */,
                       double* h /* batch x N x (4+nb) */, void* hip_stream);
+/* Fused build + solve of one round (LPV_HP_N_main.py:96-117, build and solve of every agent):
+ * where the v3 one-wave kernel covers the problem, each agent's rows and linear cost are built
+ * from traj_all straight into the solver's LDS (bit-identical to cmpc_di_build_dev) — qlin / C
+ * / h of `data` are then neither written nor read; otherwise this is cmpc_di_build_dev into
+ * data->qlin / C / h (written despite the const) followed by cmpc_solve_mpc_batch_dev.
+ * dims must describe the same agents: batch and N equal, nx = 2 dim, nu = dim, mc = 4 + nb. */
+int cmpc_di_solve_dev(cmpc_ctx* ctx, const cmpc_di_params* prm, const cmpc_di_dims* ddims, const int* nbr,
+                      const double* lane, const double* traj_all, const cmpc_mpc_dims* dims,
+                      const cmpc_mpc_weights* w, const cmpc_mpc_data* data, const cmpc_mpc_out* out,
+                      const cmpc_opts* opts, void* hip_stream);
 int cmpc_di_advance_dev(cmpc_ctx* ctx, const cmpc_di_params* prm, const cmpc_di_dims* dims,
                         const double* z /* batch x nz */, double* x0 /* batch x nx */,
                         double* u_prev /* batch x nu */, double* traj_local /* batch x (N+1) x 2 */,

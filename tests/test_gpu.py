@@ -162,6 +162,29 @@ def test_gpu_builder_matches_oracle_and_rounds(gpu_ctx):
         assert np.array_equal(R.u_prev.cpu().numpy(), zg[:, ne * (N + 1):ne * (N + 1) + 2])
 
 
+@pytest.mark.parametrize("n,N,nb,dim", [(1024, 30, 2, 2), (96, 20, 1, 2), (64, 20, 2, 3), (32, 50, 2, 3)])
+def test_fused_round_bit_equal_to_build_then_solve(gpu_ctx, n, N, nb, dim):
+    """cmpc_di_solve_dev (rows built from traj_all inside the v3 solver launch) against
+    cmpc_di_build_dev + cmpc_solve_mpc_batch_dev: five consecutive rounds (build, solve,
+    advance, exchange), z / kkt / iterations / status and the exchanged trajectories
+    bit-equal; the N = 50 nx = 6 case has no v3 instantiation and takes the unfused fallback
+    (rows written to qlin / C / h, then the Riccati kernel)."""
+    import torch
+    from cmpc import scenarios as S
+    from cmpc.rounds import DIRounds
+
+    sc = S.make_di(n, N, nb, dim)
+    F = DIRounds(sc, ctx=gpu_ctx, fused=True)
+    U = DIRounds(sc, ctx=gpu_ctx, fused=False)
+    for rnd in range(5):
+        F.step()
+        U.step()
+        torch.cuda.synchronize()
+        for a in ("z", "kkt", "iters", "status", "traj_all", "x0", "u_prev"):
+            assert torch.equal(getattr(F, a), getattr(U, a)), (rnd, a)
+    assert (U.status.cpu().numpy() == 1).mean() > 0.9
+
+
 def test_deterministic_and_permutation_invariant(gpu_ctx):
     import cmpc
     from cmpc import scenarios as S
