@@ -984,7 +984,11 @@ static int solve_one(const shared_t* S, const agent_t* a, double tol, int max_it
         double g; ROWVAL(X, U, sig, r, g);
         double s0 = wk->w[r] - g;
         t[r] = s0 > T0_FLOOR ? s0 : T0_FLOOR; /* kT0Floor of the kernels (internal.h) */
+#ifdef LAM0_CENTRE
+        lam[r] = LAM0_CENTRE / t[r]; /* lab: centred start, t lambda equal on every row */
+#else
         lam[r] = 1.0;
+#endif
 #ifdef SIGMA_START
         if (r < ms) {
             const int j = S->row_slack[r % mc];
@@ -1377,6 +1381,8 @@ static int solve_one(const shared_t* S, const agent_t* a, double tol, int max_it
 #endif
 #ifdef ETA_ADAPT
                 al = fmax(0.995, 1.0 - ETA_ADAPT * mu) * al;
+#elif defined(ETA_END)
+                al = (merit < ETA_END ? ETA_FRAC : 0.995) * al; /* lab: longer steps near convergence */
 #else
                 al = 0.995 * al;
 #endif
