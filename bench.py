@@ -125,6 +125,7 @@ def main():
     ref_line = osqp_line = None
     if rank == 0 and world == 1 and not args.no_ref and not cfg5:
         ref_line = reference_config(ctx)
+        ref_line["lpv_rounds"] = lpv_rounds(ctx)
         osqp_line = osqp_dropin(ctx)
 
     if rank == 0:
@@ -222,6 +223,69 @@ def reference_config(ctx, reps=10):
                         "host arrays)", "steps": steps,
             "reference_ms_per_agent_solve": ref_ms, "reference_ms_per_step_3_agents_sequential": 3 * ref_ms,
             "speedup_vs_reference_step": 3 * ref_ms / worst, "reps": reps}
+
+
+def lpv_rounds(ctx, replicas=341, rounds=20, warmup=2):
+    """The reference's own agent model in device-resident consensus rounds (cmpc.rounds.LPVRounds:
+    gather -> LPV scheduling + planes + QP build + solve -> advance -> exchange, all in HBM), at
+    N = 30 (nx 9, nu 2, 2 neighbours: the v3 kernel).  Population: `replicas` copies of the
+    reference's 3-agent Highway scenario at its captured step 0 (tests/golden/lpv_n30_a3:
+    x0, Last_xPredicted, uPred, OldSteering/OldAccelera, positions), each copy's initial v_x
+    scaled by a seeded factor in [0.98, 1.02]; an agent's neighbours are the other two agents of
+    its copy (LPV_HP_N_main.py:82-85)."""
+    import torch
+
+    import cmpc
+    from cmpc.rounds import LPVRounds
+
+    d = np.load(os.path.join(ROOT, "tests", "golden", "lpv_n30_a3.npz"), allow_pickle=False)
+    t = np.load(os.path.join(ROOT, "tests", "golden", "track_highway.npz"), allow_pickle=False)
+    import types
+
+    track = types.SimpleNamespace(PointAndTangent=t["PointAndTangent"], halfWidth=t["halfWidth"], lane=int(t["lane"]))
+    N, dt = int(d["N"]), float(d["dt"])
+    sel = [j for j in range(len(d["step"])) if d["step"][j] == 0]
+    order = np.argsort(d["agent"][sel])
+    sel = [sel[i] for i in order]
+    x0 = np.tile(d["x0"][sel], (replicas, 1))
+    x0[:, 0] *= np.repeat(1.0 + 0.02 * np.random.default_rng(5).uniform(-1, 1, replicas), 3)
+    x_last = np.tile(np.stack([d[f"x_last_{j}"] for j in sel]), (replicas, 1, 1))
+    u_last = np.tile(np.stack([d[f"u_last_{j}"] for j in sel]), (replicas, 1, 1))
+    u_old = np.tile(d["u_old"][sel], (replicas, 1))
+    traj = np.tile(d["pose"][sel], (replicas, 1, 1))
+    g = np.arange(3 * replicas) // 3 * 3
+    nbr = np.stack([g + (np.arange(3 * replicas) + 1) % 3, g + (np.arange(3 * replicas) + 2) % 3], 1)
+    nbr = np.sort(nbr, 1)   # the reference's ns[i]: the other agents in index order
+    Q = np.diag([10.0, 0.0, 0.0, 25.0, 10.0, 0.0, 0.0, 0.0, 0.0])
+    model = dict(lf=0.125, lr=0.125, m=1.98, I=0.09, Cf=70.0, Cr=70.0, mu=0.05)
+    lim = dict(vx_ref=float(d["vx_ref"]), min_dist=0.25, max_vel=5.5, min_vel=0.0, max_rs=0.3, max_ls=0.3,
+               max_ac=5.0, max_dc=10.0, sm=0.9)
+    bp = cmpc.PlannerLPVBatch(Q, 1e7 * np.eye(3), 0.0 * np.eye(2), 50.0 * np.eye(2), N, dt, track, 5.0, model, lim,
+                              ctx=ctx)
+    R = LPVRounds(bp, x0, x_last, u_last, nbr, u_old=u_old, traj=traj)
+    dev = R.dev
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(rounds)]
+    for _ in range(warmup):
+        R.step()
+    torch.cuda.synchronize(dev)
+    st, it = [], []
+    t0 = time.perf_counter()
+    for k in range(rounds):
+        R.step(timer=ev[k])
+        st.append(R.status.clone())
+        it.append(R.iters.clone())
+    torch.cuda.synchronize(dev)
+    el = time.perf_counter() - t0
+    st = torch.stack(st).cpu().numpy()
+    it = torch.stack(it).cpu().numpy()
+    B = 3 * replicas
+    return {"workload": f"device-resident LPV rounds: {B} agents ({replicas} copies of the reference's 3-agent "
+                        f"Highway scenario, lpv_n30_a3 step 0, v_x0 x U[0.98, 1.02]), N={N}, nx=9 nu=2 nb=2, fp64; "
+                        f"round = gather + LPV build + solve + advance + exchange",
+            "agent_qp_per_s": B * rounds / el, "ms_per_round": el / rounds * 1e3,
+            "build_solve_ms": sum(a.elapsed_time(b) for a, b in ev) / rounds, "rounds": rounds,
+            "mean_ipm_iters": float(it.mean()), "max_ipm_iters": int(it.max()),
+            "status_counts": {int(k): int(v) for k, v in zip(*np.unique(st, return_counts=True))}}
 
 
 def osqp_dropin(ctx, reps=20):

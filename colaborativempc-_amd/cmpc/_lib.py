@@ -154,6 +154,9 @@ SIGNATURES = {
                                      _DP, ct.POINTER(cmpc_mpc_dims), ct.POINTER(cmpc_mpc_weights),
                                      ct.POINTER(cmpc_mpc_data), ct.POINTER(cmpc_mpc_out), ct.POINTER(cmpc_opts),
                                      ct.c_void_p]),
+    "cmpc_lpv_gather_dev": (ct.c_int, [ct.c_void_p, ct.POINTER(cmpc_di_dims), _IP, _DP, _DP, _DP, ct.c_void_p]),
+    "cmpc_lpv_advance_dev": (ct.c_int, [ct.c_void_p, ct.POINTER(cmpc_di_dims), _DP, _DP, _DP, _DP, _DP, _DP,
+                                        ct.c_void_p]),
     "cmpc_di_advance_dev": (ct.c_int, [ct.c_void_p, ct.POINTER(cmpc_di_params), ct.POINTER(cmpc_di_dims),
                                        _DP, _DP, _DP, _DP, ct.c_void_p]),
     "cmpc_solve_qp_batch": (ct.c_int, [ct.c_void_p, ct.POINTER(cmpc_qp_dims), ct.POINTER(cmpc_qp_data),

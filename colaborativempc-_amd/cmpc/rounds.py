@@ -170,3 +170,95 @@ class DIRounds:
                      ("C", self.C), ("h", self.h)):
             p[k] = t.detach().cpu().numpy().copy()
         return p
+
+
+class LPVRounds:
+    """Device-resident consensus rounds of the reference's LPV agents (LPV_HP_N_main.py:96-117):
+    per round gather (neighbour and own positions from the exchange buffer) -> build + solve
+    (cmpc_solve_lpv_batch_dev: scheduling, planes, weights, rows, the QP) -> advance (x0 <-
+    xPred[1], Last_xPredicted <- xPred[1:], uPred, [OldSteering, OldAccelera] <- u_0) -> exchange
+    (all-gather of the predicted X, Y).  Everything stays in HBM; the host only launches.
+
+    ``bp``: a ``PlannerLPVBatch`` (gains, map, horizon, options, context).  Population arrays
+    (all ranks' agents, sharded contiguously): x0 (n, 9), x_last (n, N+1, 9) (the first
+    round's Last_xPredicted), u_last (n, N, 2), nbr (n, nb) neighbour indices (the reference: all
+    other agents, :82-85), u_old (n, 2) (default 0, PlannerLPV's initial OldSteering /
+    OldAccelera), traj (n, N+1, 2) (default x_last[:, :, 7:9], the reference's initial
+    ``agents``)."""
+
+    def __init__(self, bp, x0, x_last, u_last, nbr, u_old=None, traj=None, rank=0, world=1, group=None, comm=None):
+        import torch
+
+        self.torch, self.bp, self.ctx = torch, bp, bp.ctx
+        self.rank, self.world, self.group, self.comm = rank, world, group, comm
+        x0 = np.asarray(x0, np.float64)
+        n, N = x0.shape[0], bp.N
+        if n % world:
+            raise ValueError("agents must be divisible by the number of ranks")
+        nbr = np.asarray(nbr, np.int32).reshape(n, -1)
+        self.N, self.nb = N, nbr.shape[1]
+        self.B = n // world
+        sl = slice(rank * self.B, (rank + 1) * self.B)
+        self.off = sl.start
+        self.dev = torch.device("cuda", self.ctx.device)
+        T = lambda a, dt=torch.float64: torch.as_tensor(np.ascontiguousarray(a), dtype=dt, device=self.dev)  # noqa
+        x_last = np.asarray(x_last, np.float64)
+        if x_last.shape[1:] != (N + 1, 9):
+            raise ValueError("x_last: the first round's Last_xPredicted, (n, N+1, 9)")
+        self.x0 = T(x0[sl])
+        self.x_last = T(x_last[sl])
+        self.u_last = T(np.asarray(u_last, np.float64)[sl])
+        self.u_old = T(np.zeros((n, 2)) if u_old is None else np.asarray(u_old, np.float64))[sl].contiguous()
+        self.nbr = T(nbr[sl], torch.int32)
+        self.traj_all = T(x_last[:, :, 7:9] if traj is None else traj)
+        self.traj_local = torch.empty((self.B, N + 1, 2), dtype=torch.float64, device=self.dev)
+        self.pose = torch.empty((self.B, N + 1, 2), dtype=torch.float64, device=self.dev)
+        self.x_agents = torch.empty((self.B, N + 1, max(self.nb, 1), 2), dtype=torch.float64, device=self.dev)
+        nz = 12 * (N + 1) + 4 * N
+        self.z = torch.empty((self.B, nz), dtype=torch.float64, device=self.dev)
+        self.planes = torch.zeros((self.B, N, 3, max(self.nb, 1)), dtype=torch.float64, device=self.dev)
+        self.kkt = torch.empty(self.B, dtype=torch.float64, device=self.dev)
+        self.iters = torch.empty(self.B, dtype=torch.int32, device=self.dev)
+        self.status = torch.empty(self.B, dtype=torch.int32, device=self.dev)
+        self.last_rows = N + 1
+        self.rdims = L.cmpc_di_dims(self.B, N, self.nb, self.off)
+
+    def _stream(self):
+        return ct.c_void_p(self.torch.cuda.current_stream(self.dev).cuda_stream)
+
+    def gather(self):
+        lib = self.ctx.lib
+        self.ctx.check(lib.cmpc_lpv_gather_dev(self.ctx.h, ct.byref(self.rdims), _tptr(self.nbr), _tptr(self.traj_all),
+                                               _tptr(self.x_agents) if self.nb else None, _tptr(self.pose),
+                                               self._stream()))
+
+    def solve(self):
+        lib, bp = self.ctx.lib, self.bp
+        dims = L.cmpc_lpv_dims(self.B, self.N, self.nb, self.last_rows)
+        data = L.cmpc_lpv_data(_tptr(self.x0), _tptr(self.x_last), _tptr(self.u_last), _tptr(self.u_old),
+                               _tptr(self.x_agents) if self.nb else None, _tptr(self.pose))
+        out = L.cmpc_lpv_out(_tptr(self.z), _tptr(self.planes) if self.nb else None, _tptr(self.kkt),
+                             ct.cast(self.iters.data_ptr(), L._IP), ct.cast(self.status.data_ptr(), L._IP))
+        self.ctx.check(lib.cmpc_solve_lpv_batch_dev(self.ctx.h, ct.byref(bp.prm), ct.byref(bp.track), ct.byref(dims),
+                                                    ct.byref(data), ct.byref(out), ct.byref(bp.opts),
+                                                    self._stream()))
+
+    def advance(self):
+        self.ctx.check(self.ctx.lib.cmpc_lpv_advance_dev(self.ctx.h, ct.byref(self.rdims), _tptr(self.z),
+                                                         _tptr(self.x0), _tptr(self.x_last), _tptr(self.u_last),
+                                                         _tptr(self.u_old), _tptr(self.traj_local), self._stream()))
+        self.last_rows = self.N   # x_old = xPred[1:] from now on (LPV_HP_N_main.py:115)
+
+    def exchange(self):
+        exchange_positions(self.traj_all, self.traj_local, self.world, self.group, self.comm)
+
+    def step(self, timer=None):
+        """One consensus round.  `timer` (start, stop) events bracket the build + solve launch."""
+        self.gather()
+        if timer is not None:
+            timer[0].record()
+        self.solve()
+        if timer is not None:
+            timer[1].record()
+        self.advance()
+        self.exchange()

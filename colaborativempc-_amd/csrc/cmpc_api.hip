@@ -312,6 +312,30 @@ int cmpc_solve_lpv_batch_dev(cmpc_ctx* ctx, const cmpc_lpv_params* prm, const cm
     return lpv_run(ctx, prm, tr, d, in, out, opts, (hipStream_t)stream, cv);
 }
 
+int cmpc_lpv_gather_dev(cmpc_ctx* ctx, const cmpc_di_dims* d, const int* nbr, const double* traj_all,
+                        double* x_agents, double* pose, void* stream) {
+    if (!ctx) return CMPC_ERR_ARG;
+    if (!d || !traj_all || !pose || (d->nb > 0 && (!nbr || !x_agents)))
+        return fail(ctx, CMPC_ERR_ARG, "null argument");
+    if (d->N < 1 || d->nb < 0 || d->batch < 0 || d->self_offset < 0) return fail(ctx, CMPC_ERR_ARG, "bad dimensions");
+    int rc = set_device(ctx);
+    if (rc != CMPC_OK) return rc;
+    HIP_TRY(cmpc::lpv_gather_launch(d->N, d->nb, d->self_offset, nbr, traj_all, d->nb ? x_agents : nullptr, pose,
+                                    d->batch, (hipStream_t)stream));
+    return CMPC_OK;
+}
+
+int cmpc_lpv_advance_dev(cmpc_ctx* ctx, const cmpc_di_dims* d, const double* z, double* x0, double* x_last,
+                         double* u_last, double* u_old, double* traj_local, void* stream) {
+    if (!ctx) return CMPC_ERR_ARG;
+    if (!d || !z || !x0 || !x_last || !u_last || !u_old || !traj_local) return fail(ctx, CMPC_ERR_ARG, "null argument");
+    if (d->N < 1 || d->batch < 0) return fail(ctx, CMPC_ERR_ARG, "bad dimensions");
+    int rc = set_device(ctx);
+    if (rc != CMPC_OK) return rc;
+    HIP_TRY(cmpc::lpv_advance_launch(d->N, z, x0, x_last, u_last, u_old, traj_local, d->batch, (hipStream_t)stream));
+    return CMPC_OK;
+}
+
 int cmpc_lpv_build_dev(cmpc_ctx* ctx, const cmpc_lpv_params* prm, const cmpc_track* tr, const cmpc_lpv_dims* d,
                        const cmpc_lpv_data* in, const cmpc_lpv_build_out* out, void* stream) {
     if (!ctx || !in || !out || !d) return fail(ctx, CMPC_ERR_ARG, "null argument");

@@ -150,6 +150,12 @@ hipError_t lpv_build_launch(const LpvConst& c, const LpvPtrs& p, int batch, hipS
 // Where the builder flagged agent b (track lookup failed, the reference raises): status[b] =
 // CMPC_UNSOLVED (status may be null) and z[b, :] = NaN.
 hipError_t lpv_mark_launch(const int* err, int* status, double* z, int nz, int batch, hipStream_t s);
+// device-resident LPV round (lpv_round.hip): neighbour / own positions from the exchange buffer,
+// and the round update from the solution
+hipError_t lpv_gather_launch(int N, int nb, int self_offset, const int* nbr, const double* traj_all, double* x_agents,
+                             double* pose, int batch, hipStream_t s);
+hipError_t lpv_advance_launch(int N, const double* z, double* x0, double* x_last, double* u_last, double* u_old,
+                              double* traj_local, int batch, hipStream_t s);
 
 // Synthetic double-integrator family (bench workload).
 

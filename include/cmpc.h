@@ -260,6 +260,23 @@ int cmpc_di_advance_dev(cmpc_ctx* ctx, const cmpc_di_params* prm, const cmpc_di_
                         double* u_prev /* batch x nu */, double* traj_local /* batch x (N+1) x 2 */,
                         void* hip_stream);
 
+/* Device-resident LPV consensus round (LPV_HP_N_main.py:96-117), DEVICE pointers, dims =
+ * {batch, N, nb, self_offset} of the cmpc_di_dims struct:
+ *   cmpc_lpv_gather_dev:  x_agents (batch x (N+1) x nb x 2) <- traj_all rows nbr[b][j] and pose
+ *     (batch x (N+1) x 2) <- traj_all row self_offset + b — agents[:, ns[i], :] / agents[:, i, :]
+ *     (:99-104); traj_all is n_total x (N+1) x 2, nbr batch x nb global agent indices;
+ *   cmpc_solve_lpv_batch_dev on those buffers;
+ *   cmpc_lpv_advance_dev: from z (reference layout): x0 <- xPred[1], x_last <- xPred[1:] written
+ *     DENSE as batch x N x 9 (last_rows = N from the second round on, :115), u_last <- uPred
+ *     (batch x N x 2, not shifted), u_old <- uPred[0] (:179-180), traj_local (batch x (N+1) x 2)
+ *     <- xPred[:, X, Y] (:117);
+ *   then the all-gather of traj_local into traj_all (cmpc_allgather_trajectories or torch). */
+int cmpc_lpv_gather_dev(cmpc_ctx* ctx, const cmpc_di_dims* dims, const int* nbr, const double* traj_all,
+                        double* x_agents, double* pose, void* hip_stream);
+int cmpc_lpv_advance_dev(cmpc_ctx* ctx, const cmpc_di_dims* dims, const double* z, double* x0, double* x_last,
+                         double* u_last, double* u_old, double* traj_local, void* hip_stream);
+
+
 /* ------------------------------------------------------------------------
  * Dense standard-form QP batch with MATLAB quadprog semantics (the MEX drop-in
  * for quadprog(H,f,A,b,Aeq,beq,lb,ub) as YALMIP calls it, callquadprog.m:63-69,

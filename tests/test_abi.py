@@ -20,7 +20,7 @@ def test_header_declares_the_boundary():
     fns = declared_functions()
     for need in ("cmpc_create", "cmpc_destroy", "cmpc_solve_mpc_batch", "cmpc_solve_mpc_batch_dev",
                  "cmpc_solve_lpv_batch", "cmpc_solve_lpv_batch_dev", "cmpc_di_build_dev", "cmpc_di_solve_dev",
-                 "cmpc_di_advance_dev"):
+                 "cmpc_di_advance_dev", "cmpc_lpv_gather_dev", "cmpc_lpv_advance_dev"):
         assert need in fns
 
 

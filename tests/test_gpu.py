@@ -92,6 +92,49 @@ def test_planner_lpv_dropin_closed_loop(gpu_ctx):
         agents = np.swapaxes(np.asarray(xp)[:, :, -2:], 0, 1)
 
 
+def test_lpv_rounds_device_resident_vs_reference_loop(gpu_ctx):
+    """LPVRounds (gather -> cmpc_solve_lpv_batch_dev -> advance -> exchange, all in HBM) on the
+    reference's 3-agent N = 30 Highway run: every round's z matches the reference-captured
+    optimum (tests/golden/lpv_n30_a3, all captured steps) and is bit-equal to the host-array
+    loop of PlannerLPVBatch with the reference loop semantics (LPV_HP_N_main.py:96-117)."""
+    import torch
+
+    import cmpc
+    from cmpc.rounds import LPVRounds
+    from oracle import lpv_ref as L
+
+    d = golden("lpv_n30_a3")
+    N, n, steps, dt = int(d["N"]), int(d["n_agents"]), int(d["steps"]), float(d["dt"])
+    g, model = _gains()
+    tr = L.Track.build("Highway")
+    lim = L.scaled_car_limits(float(d["vx_ref"]))
+    agents, x_old, u_old = L.initialise_agents(L.X0_DATABASE[:n], N, dt, tr)
+    ns = L.neighbour_lists(n)
+    bp = cmpc.PlannerLPVBatch(g["Q"], g["Qs"], g["R"], g["dR"], N, dt, tr, g["wq"], model, lim, ctx=gpu_ctx)
+    hx0 = np.stack([x_old[i][0] for i in range(n)])
+    hxl, hul, huo, hag = np.stack(x_old), np.stack(u_old), np.zeros((n, 2)), agents.copy()
+    R = LPVRounds(bp, hx0, hxl, hul, ns, traj=np.swapaxes(agents, 0, 1))
+    captured = {(c["step"], c["agent"]): c for _, c in lpv_qps("lpv_n30_a3")}
+    base = 12 * (N + 1)
+    for step in range(steps):
+        R.step()
+        torch.cuda.synchronize()
+        res = bp.solve(hx0, hxl, hul, huo, np.stack([hag[:, ns[i], :] for i in range(n)]),
+                       np.stack([hag[:, i, :] for i in range(n)]))
+        zg = R.z.cpu().numpy()
+        assert np.array_equal(zg, res["z"]), step
+        assert np.array_equal(R.planes.cpu().numpy(), res["planes"]), step
+        for i in range(n):
+            assert_matches_optimum(zg[i], captured[(step, i)], Z_TOL)
+        xp = res["z"][:, :base].reshape(n, N + 1, 12)[:, :, :9]
+        up = res["z"][:, base: base + 2 * N].reshape(n, N, 2)
+        hx0, hxl, hul, huo = xp[:, 1].copy(), xp[:, 1:].copy(), up.copy(), up[:, 0].copy()
+        hag = np.swapaxes(xp[:, :, 7:9], 0, 1).copy()
+        assert np.array_equal(R.x0.cpu().numpy(), hx0) and np.array_equal(R.u_old.cpu().numpy(), huo)
+        assert np.array_equal(R.x_last.cpu().numpy().reshape(-1)[: n * N * 9], hxl.reshape(-1))
+        assert np.array_equal(R.traj_all.cpu().numpy(), np.swapaxes(hag, 0, 1))
+
+
 @pytest.mark.parametrize("n,N,nb,dim", [(2, 10, 1, 2), (64, 20, 2, 2), (1024, 30, 2, 2), (16, 10, 2, 3)])
 def test_synthetic_batch_vs_c_oracle(gpu_ctx, n, N, nb, dim):
     import cmpc
