@@ -40,6 +40,7 @@ _IP = ct.POINTER(ct.c_int)
 CMPC_FLAG_GENERIC = 1
 CMPC_FLAG_FP32 = 8
 CMPC_FLAG_RICCATI = 16
+CMPC_FLAG_RESCUE = 32   # Riccati re-solve of agents whose condensed factorisation broke down
 
 
 class cmpc_opts(ct.Structure):

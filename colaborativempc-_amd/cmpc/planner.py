@@ -75,7 +75,9 @@ class PlannerLPVBatch:
         self.ctx = ctx or L.default_context()
         self.prm = lpv_params(Q, Qs, R, dR, dt, wq, model_param, sys_lim)
         self.track, self._track_keep = track_of(map)
-        self.opts = L.opts(tol, max_iter, L.CMPC_FLAG_RICCATI if riccati else 0)
+        # rescue pass on: an agent whose condensed factorisation breaks down (theta ~ 1e18 on
+        # saturated rows) is re-solved by the Riccati kernel instead of returning its best iterate
+        self.opts = L.opts(tol, max_iter, L.CMPC_FLAG_RICCATI if riccati else L.CMPC_FLAG_RESCUE)
 
     def solve(self, x0, x_last, u_last, u_old, x_agents, pose):
         """x0 (B,9); x_last (B,N or N+1,9); u_last (B,N,2); u_old (B,2);

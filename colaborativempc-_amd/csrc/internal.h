@@ -24,6 +24,7 @@ struct MpcConst {
     int max_iter;
     int wg;       // 0: one-wave kernels; 2: workgroup kernel in fp32 (CMPC_FLAG_FP32)
     int riccati;  // 1: stage-wise Riccati kernel (fp64, N*nu > 64 or CMPC_FLAG_RICCATI)
+    int rescue;   // 1: CMPC_FLAG_RESCUE on a condensed solve (Riccati re-solve of broken-down agents)
     double tol;
     double qs_max;  // max(1, 2*max(Qs)) — slack residual scale
     double Q[CMPC_MAX_NX * CMPC_MAX_NX];
@@ -111,7 +112,7 @@ size_t mpc_riccati_lds_bytes(const MpcConst& c);
 size_t mpc_riccati_ws_doubles(const MpcConst& c);
 hipError_t mpc_riccati_launch(const MpcConst& c, const MpcPtrs& p, int batch, hipStream_t s);
 // Device scratch (doubles per agent) the solver chosen for c needs in MpcPtrs::ws (0: none).
-inline size_t mpc_ws_doubles(const MpcConst& c) { return c.riccati ? mpc_riccati_ws_doubles(c) : 0; }
+inline size_t mpc_ws_doubles(const MpcConst& c) { return (c.riccati || c.rescue) ? mpc_riccati_ws_doubles(c) : 0; }
 
 // Fills the derived fields of MpcConst; returns CMPC_OK or an error code with msg.
 int mpc_prepare(const cmpc_mpc_dims* d, const cmpc_mpc_weights* w, const cmpc_opts* o,

@@ -711,6 +711,9 @@ int mpc_prepare(const cmpc_mpc_dims* d, const cmpc_mpc_weights* wt, const cmpc_o
         *msg = "the per-agent rows of this horizon do not fit the Riccati solver's 160 KB of LDS";
         return CMPC_ERR_UNSUPPORTED;
     }
+    // rescue pass (CMPC_FLAG_RESCUE): only for condensed fp64 solves whose rows fit the Riccati kernel
+    c->rescue = (!fp32 && !c->riccati && (o && (o->flags & CMPC_FLAG_RESCUE)) && mpc_riccati_lds_bytes(*c) <= kMaxLdsBytes)
+                    ? 1 : 0;
     for (int i = 0; i < d->nu; ++i) {
         c->u_ub[i] = wt->u_ub[i];
         c->u_lb[i] = wt->u_lb[i];
@@ -740,14 +743,21 @@ hipError_t mpc_launch(const MpcConst& c, const MpcPtrs& p, int batch, hipStream_
     if (batch == 0) return hipSuccess;
     if (c.wg) return mpc_wg_launch(c, p, batch, s, c.wg == 2);
     if (c.riccati) return mpc_riccati_launch(c, p, batch, s);
-    hipError_t e2;
-    if (!(flags & CMPC_FLAG_GENERIC) && mpc3_try_launch(c, p, batch, s, &e2)) return e2;
-    switch (c.npad / 16) {
-        case 1: return launch_t<1>(c, p, batch, s);
-        case 2: return launch_t<2>(c, p, batch, s);
-        case 3: return launch_t<3>(c, p, batch, s);
-        default: return launch_t<4>(c, p, batch, s);
+    hipError_t e;
+    if (flags & CMPC_FLAG_GENERIC || !mpc3_try_launch(c, p, batch, s, &e)) {
+        switch (c.npad / 16) {
+            case 1: e = launch_t<1>(c, p, batch, s); break;
+            case 2: e = launch_t<2>(c, p, batch, s); break;
+            case 3: e = launch_t<3>(c, p, batch, s); break;
+            default: e = launch_t<4>(c, p, batch, s); break;
+        }
     }
+    if (e != hipSuccess || !c.rescue || !p.status || !p.ws) return e;
+    // rescue pass: the Riccati kernel re-solves, on the same problems, exactly the agents the
+    // condensed solve left CMPC_UNSOLVED (its other workgroups return at once)
+    MpcConst cr = c;
+    cr.riccati = 1;
+    return mpc_riccati_launch(cr, p, batch, s);
 }
 
 // ---- f64 MFMA fragment-map self test: D(16x16) = A(16x4) * B(4x16) ----

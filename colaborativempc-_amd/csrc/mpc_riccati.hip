@@ -983,6 +983,7 @@ template <class G>
 __global__ __launch_bounds__(kWave) void mpc_riccati_kernel(const MpcConst c_arg, const MpcPtrs P) {
     extern __shared__ __attribute__((aligned(16))) double sm[];
     const int b = blockIdx.x;
+    if (c_arg.rescue && P.status[b] != CMPC_UNSOLVED) return;  // rescue pass: broken-down agents only
     const int l = threadIdx.x;
     const RLds L = r_layout(c_arg);
     // the weights are indexed by lane-dependent expressions: read them from an LDS copy (a

@@ -135,6 +135,56 @@ def test_lpv_rounds_device_resident_vs_reference_loop(gpu_ctx):
         assert np.array_equal(R.traj_all.cpu().numpy(), np.swapaxes(hag, 0, 1))
 
 
+def test_rescue_pass_resolves_factorisation_breakdowns(gpu_ctx):
+    """CMPC_FLAG_RESCUE: in closed-loop LPV rounds (341 jittered copies of the reference's
+    3-agent N = 30 run) run without it until a round has agents whose condensed factorisation
+    broke down (status CMPC_UNSOLVED); the same round re-solved with the flag: every other
+    agent's z / status bit-identical, every broken-down agent now solved or at the rounding
+    floor with KKT <= 1e-6 (the Riccati kernel, double-double near the solution)."""
+    import torch
+
+    import cmpc
+    from cmpc import _lib as L
+    from cmpc.rounds import LPVRounds
+    from oracle import lpv_ref as LR
+
+    d = golden("lpv_n30_a3")
+    N, dt, reps = int(d["N"]), float(d["dt"]), 341
+    sel = sorted([j for j in range(len(d["step"])) if d["step"][j] == 0], key=lambda j: d["agent"][j])
+    x0 = np.tile(d["x0"][sel], (reps, 1))
+    x0[:, 0] *= np.repeat(1.0 + 0.02 * np.random.default_rng(5).uniform(-1, 1, reps), 3)
+    g3 = np.arange(3 * reps) // 3 * 3
+    nbr = np.sort(np.stack([g3 + (np.arange(3 * reps) + 1) % 3, g3 + (np.arange(3 * reps) + 2) % 3], 1), 1)
+    g, model = _gains()
+    bp = cmpc.PlannerLPVBatch(g["Q"], g["Qs"], g["R"], g["dR"], N, dt, LR.Track.build("Highway"), g["wq"], model,
+                              LR.scaled_car_limits(float(d["vx_ref"])), ctx=gpu_ctx)
+    plain, rescue = L.opts(), L.opts(flags=L.CMPC_FLAG_RESCUE)
+    R = LPVRounds(bp, x0, np.tile(np.stack([d[f"x_last_{j}"] for j in sel]), (reps, 1, 1)),
+                  np.tile(np.stack([d[f"u_last_{j}"] for j in sel]), (reps, 1, 1)), nbr,
+                  u_old=np.tile(d["u_old"][sel], (reps, 1)), traj=np.tile(d["pose"][sel], (reps, 1, 1)))
+    for rnd in range(30):
+        R.gather()
+        bp.opts = plain
+        R.solve()
+        torch.cuda.synchronize()
+        st = R.status.cpu().numpy()
+        bad = st == cmpc.CMPC_UNSOLVED
+        if bad.any():
+            z0 = R.z.cpu().numpy()
+            bp.opts = rescue
+            R.solve()
+            torch.cuda.synchronize()
+            st1, z1, k1 = R.status.cpu().numpy(), R.z.cpu().numpy(), R.kkt.cpu().numpy()
+            assert np.array_equal(st1[~bad], st[~bad]) and np.array_equal(z1[~bad], z0[~bad])
+            assert np.isin(st1[bad], (cmpc.CMPC_SOLVED, cmpc.CMPC_SOLVED_INACCURATE)).all(), st1[bad]
+            assert (k1[bad] <= 1e-6).all(), k1[bad]
+            print(f"round {rnd}: {int(bad.sum())} broken-down agents rescued")
+            return
+        R.advance()
+        R.exchange()
+    pytest.fail("no factorisation breakdown in 30 rounds: the rescue pass was not exercised")
+
+
 @pytest.mark.parametrize("n,N,nb,dim", [(2, 10, 1, 2), (64, 20, 2, 2), (1024, 30, 2, 2), (16, 10, 2, 3)])
 def test_synthetic_batch_vs_c_oracle(gpu_ctx, n, N, nb, dim):
     import cmpc
