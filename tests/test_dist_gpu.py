@@ -60,6 +60,33 @@ def test_two_rank_hip_rounds_match_single_process(tmp_path, gpu_ctx):
     assert np.array_equal(d0["z0"], z0)
 
 
+def test_two_rank_lpv_rounds_match_single_process(tmp_path, gpu_ctx):
+    """The reference's agent model in device-resident rounds (cmpc.rounds.LPVRounds) on two
+    ranks: 12 copies of the 3-agent N = 30 Highway run, ring neighbours that cross the rank
+    boundary; four rounds of traj_all and every agent's z bit-equal to one process."""
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    from dist_rounds import run_lpv
+
+    reps, rounds = 12, 4
+    port = _free_port()
+    procs = []
+    for r in range(2):
+        env = dict(os.environ, RANK=str(r), WORLD_SIZE="2", LOCAL_RANK="0", MASTER_ADDR="127.0.0.1",
+                   MASTER_PORT=str(port), CMPC_DIST_BACKEND="gloo")
+        procs.append(subprocess.Popen([sys.executable, os.path.join(ROOT, "tools", "dist_rounds.py"), "lpv",
+                                       str(tmp_path / f"lpv{r}.npz"), str(reps), str(rounds)], env=env,
+                                      stdout=subprocess.PIPE, stderr=subprocess.STDOUT))
+    trajs, zs = run_lpv(reps, rounds)
+    for p in procs:
+        out, _ = p.communicate(timeout=240)
+        assert p.returncode == 0, out.decode()[-3000:]
+    half = 3 * reps // 2
+    for r in range(2):
+        d = np.load(tmp_path / f"lpv{r}.npz")
+        assert np.array_equal(d["trajs"], trajs), f"rank {r}: exchanged trajectories differ"
+        assert np.array_equal(d["zs"], zs[:, r * half:(r + 1) * half]), f"rank {r}: solutions differ"
+
+
 def test_c_abi_rccl_allgather_single_rank(gpu_ctx):
     """cmpc_comm_init / cmpc_allgather_trajectories (the C-ABI exchange a MATLAB / C host uses
     instead of torch.distributed), one rank: the gather is the identity, and rounds driven
