@@ -112,7 +112,13 @@ static int chol(double* K, int n) {
     for (int j = 0; j < n; ++j) {
         double d = K[IDX2(j, j, n)];
         for (int p = 0; p < j; ++p) d -= K[IDX2(j, p, n)] * K[IDX2(j, p, n)];
+#ifdef WRIGHT_PIVOT
+        /* lab: Wright's modified Cholesky — a pivot lost to cancellation (<= WRIGHT_PIVOT times the
+           original diagonal) is replaced by a huge one, which drops that component of the step */
+        if (!(d > WRIGHT_PIVOT * K[IDX2(j, j, n)])) d = 1e128;
+#else
         if (!(d > 0.0)) return -1;
+#endif
         d = sqrt(d);
         K[IDX2(j, j, n)] = d;
         for (int i = j + 1; i < n; ++i) {
