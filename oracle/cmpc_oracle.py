@@ -49,6 +49,20 @@ def nz_of(p):
     return (p["nx"] + p["ns"]) * (p["N"] + 1) + 2 * p["nu"] * p["N"]
 
 
+def solve_batch_rescue(p, tol=1e-9, max_iter=60, nthreads=0):
+    """The product's CMPC_FLAG_RESCUE policy restated: the condensed method (newton 0); agents it
+    leaves status -10 (factorisation breakdown) re-solved by the Riccati method with the
+    kernel's double-double mode (newton 3) on the same problems."""
+    z, kkt, it, st = solve_batch(p, tol, max_iter, nthreads)
+    bad = np.flatnonzero(st == -10)
+    if len(bad):
+        q = dict(p)
+        for k in ("A", "B", "x0", "u_prev", "qlin", "C", "h"):
+            q[k] = p[k][bad]
+        z[bad], kkt[bad], it[bad], st[bad] = solve_batch(q, tol, max_iter, nthreads, newton=3)
+    return z, kkt, it, st
+
+
 def solve_batch(p, tol=1e-9, max_iter=60, nthreads=0, newton=0, refine=0, U0=None):
     nb = p["A"].shape[0]
     keep = []

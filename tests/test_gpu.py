@@ -178,6 +178,22 @@ def test_rescue_pass_resolves_factorisation_breakdowns(gpu_ctx):
             assert np.array_equal(st1[~bad], st[~bad]) and np.array_equal(z1[~bad], z0[~bad])
             assert np.isin(st1[bad], (cmpc.CMPC_SOLVED, cmpc.CMPC_SOLVED_INACCURATE)).all(), st1[bad]
             assert (k1[bad] <= 1e-6).all(), k1[bad]
+            # the same policy in the C restatement, on the GPU builder's problems of these agents
+            from oracle import cmpc_oracle as CO
+
+            rows = R.last_rows
+            xl = R.x_last.cpu().numpy().reshape(-1)[: R.B * rows * 9].reshape(R.B, rows, 9)[bad]
+            b = bp.build(xl, R.u_last.cpu().numpy()[bad], R.x_agents.cpu().numpy()[bad], R.pose.cpu().numpy()[bad])
+            P = dict(nx=9, nu=2, N=N, ns=3, mc=6, Q=g["Q"], R=g["R"], dR=g["dR"], Qs=np.diag(g["Qs"]).copy(),
+                     u_ub=np.array([0.3, 5.0]), u_lb=np.array([-0.3, -10.0]), row_slack=np.array([-1, 0, 1, 1, 2, 2]),
+                     row_sign=np.array([1, 1, 1, 1, -1, -1]), A=b["A"], B=b["B"], x0=R.x0.cpu().numpy()[bad],
+                     u_prev=R.u_old.cpu().numpy()[bad], qlin=b["qlin"], C=b["C"], h=b["h"])
+            zc, kc, ic, sc = CO.solve_batch_rescue(P, nthreads=8)
+            both = (sc == 1) & (st1[bad] == 1)
+            assert both.sum() >= bad.sum() // 2, (sc, st1[bad])
+            err = np.abs(zc - z1[bad]).max(1)
+            print(f"rescued vs C restatement: {int(both.sum())} both solved, max |dz| {err[both].max():.1e}")
+            assert err[both].max() < 1e-6
             print(f"round {rnd}: {int(bad.sum())} broken-down agents rescued")
             return
         R.advance()
