@@ -46,6 +46,25 @@ def dims_of(nz, m_ineq, m_eq, layout=LPV_LAYOUT):
     return (N, mc) if mc >= 0 else None
 
 
+_COST_CACHE = {}
+
+
+def _cost_matrix(N, ne, nu, qt, r, dr):
+    """P = 2 blkdiag(Qt^(N+1), R^N, dR^N) (LPV_Planner.py:382-427) as canonical csr, memoised on
+    the exact bytes of its blocks (the gains are fixed per planner, the block_diag rebuild was
+    the largest part of a recognition)."""
+    key = (N, ne, nu, qt, r, dr)
+    P = _COST_CACHE.get(key)
+    if P is None:
+        blocks = [np.frombuffer(qt).reshape(ne, ne)] * (N + 1) + [np.frombuffer(r).reshape(nu, nu)] * N + \
+                 [np.frombuffer(dr).reshape(nu, nu)] * N
+        P = _csr(sp.block_diag(blocks, format="csr") * 2.0)
+        if len(_COST_CACHE) > 64:
+            _COST_CACHE.clear()
+        _COST_CACHE[key] = P
+    return P.copy()
+
+
 def reference_form(p, a=0):
     """Sparse reference-form QP (P, q, G, h, Aeq, beq) of agent ``a`` of a structured problem
     dict (the keys of include/cmpc.h; row_slack / row_sign give the slack pattern)."""
@@ -57,8 +76,8 @@ def reference_form(p, a=0):
     Qt = np.zeros((ne, ne))
     Qt[:nx, :nx] = p["Q"]
     Qt[nx:, nx:] = np.diag(np.asarray(p["Qs"], float))
-    P = sp.block_diag([Qt] * (N + 1) + [np.asarray(p["R"], float)] * N + [np.asarray(p["dR"], float)] * N,
-                      format="csr") * 2.0
+    R_, dR_ = np.ascontiguousarray(p["R"], float), np.ascontiguousarray(p["dR"], float)
+    P = _cost_matrix(N, Qt.shape[0], R_.shape[0], Qt.tobytes(), R_.tobytes(), dR_.tobytes())
     q = np.zeros(nz)
     q[: ne * (N + 1)].reshape(N + 1, ne)[:, :nx] = 2.0 * np.asarray(p["qlin"][a], float)
     # inequalities: stage rows, then input rows
