@@ -92,38 +92,45 @@ def test_planner_lpv_dropin_closed_loop(gpu_ctx):
         agents = np.swapaxes(np.asarray(xp)[:, :, -2:], 0, 1)
 
 
-def test_lpv_rounds_device_resident_vs_reference_loop(gpu_ctx):
-    """LPVRounds (gather -> cmpc_solve_lpv_batch_dev -> advance -> exchange, all in HBM) on the
-    reference's 3-agent N = 30 Highway run: every round's z matches the reference-captured
-    optimum (tests/golden/lpv_n30_a3, all captured steps) and is bit-equal to the host-array
-    loop of PlannerLPVBatch with the reference loop semantics (LPV_HP_N_main.py:96-117)."""
+@pytest.mark.parametrize("name", ["lpv_n30_a3", "lpv_n10_a1", "lpv_n10_a2", "lpv_n20_a4", "lpv_n10_lowspeed"])
+def test_lpv_rounds_device_resident_vs_reference_loop(gpu_ctx, name):
+    """LPVRounds (gather -> cmpc_solve_lpv_batch_dev -> advance -> exchange, all in HBM) started
+    from a captured reference run's step-0 inputs (1-4 agents, 0-3 neighbours, the vx < 0.2
+    branch): every round's z matches the reference-captured optimum of that step and agent, and
+    is bit-equal to the host-array loop of PlannerLPVBatch with the reference loop semantics
+    (LPV_HP_N_main.py:96-117)."""
     import torch
 
     import cmpc
     from cmpc.rounds import LPVRounds
     from oracle import lpv_ref as L
 
-    d = golden("lpv_n30_a3")
+    d = golden(name)
     N, n, steps, dt = int(d["N"]), int(d["n_agents"]), int(d["steps"]), float(d["dt"])
     g, model = _gains()
     tr = L.Track.build("Highway")
     lim = L.scaled_car_limits(float(d["vx_ref"]))
-    agents, x_old, u_old = L.initialise_agents(L.X0_DATABASE[:n], N, dt, tr)
     ns = L.neighbour_lists(n)
     bp = cmpc.PlannerLPVBatch(g["Q"], g["Qs"], g["R"], g["dR"], N, dt, tr, g["wq"], model, lim, ctx=gpu_ctx)
-    hx0 = np.stack([x_old[i][0] for i in range(n)])
-    hxl, hul, huo, hag = np.stack(x_old), np.stack(u_old), np.zeros((n, 2)), agents.copy()
-    R = LPVRounds(bp, hx0, hxl, hul, ns, traj=np.swapaxes(agents, 0, 1))
-    captured = {(c["step"], c["agent"]): c for _, c in lpv_qps("lpv_n30_a3")}
+    sel = sorted([j for j in range(len(d["step"])) if d["step"][j] == 0], key=lambda j: d["agent"][j])
+    hx0 = d["x0"][sel].copy()
+    hxl = np.stack([d[f"x_last_{j}"] for j in sel])
+    hul = np.stack([d[f"u_last_{j}"] for j in sel])
+    huo = d["u_old"][sel].copy()
+    hag = np.swapaxes(d["pose"][sel], 0, 1).copy()          # agents (N+1, n, 2)
+    R = LPVRounds(bp, hx0, hxl, hul, np.array(ns, np.int32).reshape(n, n - 1), u_old=huo,
+                  traj=d["pose"][sel])
+    captured = {(c["step"], c["agent"]): c for _, c in lpv_qps(name)}
     base = 12 * (N + 1)
     for step in range(steps):
         R.step()
         torch.cuda.synchronize()
-        res = bp.solve(hx0, hxl, hul, huo, np.stack([hag[:, ns[i], :] for i in range(n)]),
-                       np.stack([hag[:, i, :] for i in range(n)]))
+        xa = np.stack([hag[:, ns[i], :] for i in range(n)])
+        res = bp.solve(hx0, hxl, hul, huo, xa, np.stack([hag[:, i, :] for i in range(n)]))
         zg = R.z.cpu().numpy()
         assert np.array_equal(zg, res["z"]), step
-        assert np.array_equal(R.planes.cpu().numpy(), res["planes"]), step
+        if n > 1:
+            assert np.array_equal(R.planes.cpu().numpy(), res["planes"]), step
         for i in range(n):
             assert_matches_optimum(zg[i], captured[(step, i)], Z_TOL)
         xp = res["z"][:, :base].reshape(n, N + 1, 12)[:, :, :9]
