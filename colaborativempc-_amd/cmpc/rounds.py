@@ -196,6 +196,11 @@ class LPVRounds:
         if n % world:
             raise ValueError("agents must be divisible by the number of ranks")
         nbr = np.asarray(nbr, np.int32).reshape(n, -1)
+        if nbr.size and (nbr.min() < 0 or nbr.max() >= n):
+            raise ValueError("nbr: neighbour indices must address the population (0 <= j < n)")
+        if np.shape(u_last) != (n, N, 2) or (u_old is not None and np.shape(u_old) != (n, 2)) or \
+                (traj is not None and np.shape(traj) != (n, N + 1, 2)) or x0.shape != (n, 9):
+            raise ValueError("x0 (n, 9), u_last (n, N, 2), u_old (n, 2), traj (n, N+1, 2) expected")
         self.N, self.nb = N, nbr.shape[1]
         self.B = n // world
         sl = slice(rank * self.B, (rank + 1) * self.B)
