@@ -121,7 +121,8 @@ def main():
     cpu = None
     max_err = None
     if rank == 0 and world == 1 and not args.no_cpu:
-        cpu, max_err = cpu_baseline(R, args.cpu_seconds)
+        cpu, max_err = cpu_baseline(R, args.cpu_seconds, rounds=1 if cfg5 else 4, newton=3 if cfg5 else 0,
+                                    label=args.config)
     ref_line = osqp_line = None
     if rank == 0 and world == 1 and not args.no_ref and not cfg5:
         ref_line = reference_config(ctx)
@@ -373,14 +374,16 @@ def host_cpu():
     return model, nproc, usable
 
 
-def cpu_baseline(R, seconds, rounds=4):
+def cpu_baseline(R, seconds, rounds=4, newton=0, label="cfg3"):
     """The oracle's plain-C restatement (oracle/cmpc_oracle.c, OpenMP, one agent-QP per
     thread) timed on this host over whole rounds of the SAME workload the GPU solves:
     `rounds` consecutive consensus rounds are built and solved on the device, each round's
     full structured problem (every agent of this rank) is copied to the host, and the CPU
     solves all of them, repeated until about `seconds` of CPU time.  Threads: every CPU this
     process may use, capped by OMP_NUM_THREADS when it is set (the GPU box grants each job a
-    16-CPU share of a larger host, so nproc there is not the usable count)."""
+    16-CPU share of a larger host, so nproc there is not the usable count).  `newton` selects the
+    restated method: 0 the condensed IPM of the v3 kernel (cfg3), 3 the stage-wise Riccati IPM
+    with the kernel's double-double mode (cfg5)."""
     import torch
 
     from oracle import cmpc_oracle as CO
@@ -403,7 +406,7 @@ def cpu_baseline(R, seconds, rounds=4):
     passes = 0
     while True:
         for p, zg in zip(probs, zs):
-            zc, _, _, _ = CO.solve_batch(p, nthreads=threads)
+            zc, _, _, _ = CO.solve_batch(p, nthreads=threads, newton=newton)
             if passes == 0:
                 err = max(err, float(np.abs(zg - zc).max()))
         passes += 1
@@ -413,7 +416,7 @@ def cpu_baseline(R, seconds, rounds=4):
     solved = passes * rounds * B
     return ({"value": solved / el, "unit": "agent-QP/s", "cores": threads, "kind": "port",
              "nproc": nproc, "cpu_model": model,
-             "sample": f"{passes} pass(es) over {rounds} consecutive full cfg3 rounds of {B} agents "
+             "sample": f"{passes} pass(es) over {rounds} consecutive full {label} rounds of {B} agents "
                        f"(device-built problems copied to the host), oracle/cmpc_oracle.c fp64, OpenMP "
                        f"{threads} threads, {el:.1f} s"}, err)
 
