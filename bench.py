@@ -226,23 +226,19 @@ def reference_config(ctx, reps=10):
             "speedup_vs_reference_step": 3 * ref_ms / worst, "reps": reps}
 
 
-def lpv_rounds(ctx, replicas=341, rounds=20, warmup=2):
-    """The reference's own agent model in device-resident consensus rounds (cmpc.rounds.LPVRounds:
-    gather -> LPV scheduling + planes + QP build + solve -> advance -> exchange, all in HBM), at
-    N = 30 (nx 9, nu 2, 2 neighbours: the v3 kernel).  Population: `replicas` copies of the
-    reference's 3-agent Highway scenario at its captured step 0 (tests/golden/lpv_n30_a3:
-    x0, Last_xPredicted, uPred, OldSteering/OldAccelera, positions), each copy's initial v_x
-    scaled by a seeded factor in [0.98, 1.02]; an agent's neighbours are the other two agents of
-    its copy (LPV_HP_N_main.py:82-85)."""
-    import torch
+def lpv_population(ctx, replicas=341, rescue=True):
+    """The population of the `lpv_rounds` line: `replicas` copies of the reference's 3-agent
+    Highway scenario at its captured step 0 (tests/golden/lpv_n30_a3: x0, Last_xPredicted, uPred,
+    OldSteering/OldAccelera, positions), each copy's initial v_x scaled by a seeded factor in
+    [0.98, 1.02]; an agent's neighbours are the other two agents of its copy
+    (LPV_HP_N_main.py:82-85).  Returns (PlannerLPVBatch, LPVRounds constructor arguments)."""
+    import types
 
     import cmpc
-    from cmpc.rounds import LPVRounds
+    from cmpc import _lib as L
 
     d = np.load(os.path.join(ROOT, "tests", "golden", "lpv_n30_a3.npz"), allow_pickle=False)
     t = np.load(os.path.join(ROOT, "tests", "golden", "track_highway.npz"), allow_pickle=False)
-    import types
-
     track = types.SimpleNamespace(PointAndTangent=t["PointAndTangent"], halfWidth=t["halfWidth"], lane=int(t["lane"]))
     N, dt = int(d["N"]), float(d["dt"])
     sel = [j for j in range(len(d["step"])) if d["step"][j] == 0]
@@ -263,30 +259,93 @@ def lpv_rounds(ctx, replicas=341, rounds=20, warmup=2):
                max_ac=5.0, max_dc=10.0, sm=0.9)
     bp = cmpc.PlannerLPVBatch(Q, 1e7 * np.eye(3), 0.0 * np.eye(2), 50.0 * np.eye(2), N, dt, track, 5.0, model, lim,
                               ctx=ctx)
-    R = LPVRounds(bp, x0, x_last, u_last, nbr, u_old=u_old, traj=traj)
+    if not rescue:
+        bp.opts = L.opts()
+    return bp, (x0, x_last, u_last, nbr), dict(u_old=u_old, traj=traj)
+
+
+def lpv_check_round(bp, R, sample):
+    """The current round's problems of the `sample` agents (the GPU builder's A, B, qlin, C, h,
+    read back) solved by the C restatement with the product's rescue policy
+    (oracle.cmpc_oracle.solve_batch_rescue); returns (z_cpu, status_cpu) of the sample."""
+    from oracle import cmpc_oracle as CO
+
+    rows = R.last_rows
+    xl = R.x_last.cpu().numpy().reshape(-1)[: R.B * rows * 9].reshape(R.B, rows, 9)[sample]
+    b = bp.build(xl, R.u_last.cpu().numpy()[sample], R.x_agents.cpu().numpy()[sample], R.pose.cpu().numpy()[sample])
+    prm = bp.prm
+    P = dict(nx=9, nu=2, N=bp.N, ns=3, mc=4 + R.nb, Q=np.array(prm.Q[:]).reshape(9, 9), R=np.array(prm.R[:]).reshape(2, 2),
+             dR=np.array(prm.dR[:]).reshape(2, 2), Qs=np.array(prm.Qs[:]), u_ub=np.array([prm.max_rs, prm.max_ac]),
+             u_lb=np.array([-prm.max_ls, -prm.max_dc]), row_slack=np.array([-1, 0, 1, 1] + [2] * R.nb),
+             row_sign=np.array([1, 1, 1, 1] + [-1] * R.nb), A=b["A"], B=b["B"], x0=R.x0.cpu().numpy()[sample],
+             u_prev=R.u_old.cpu().numpy()[sample], qlin=b["qlin"], C=b["C"], h=b["h"])
+    zc, _, _, sc = CO.solve_batch_rescue(P, nthreads=min(16, os.cpu_count() or 1))
+    return zc, sc
+
+
+def lpv_rounds(ctx, replicas=341, rounds=20, warmup=2, rescue=True, check=True, sample=128):
+    """The reference's own agent model in device-resident consensus rounds (cmpc.rounds.LPVRounds:
+    gather -> LPV scheduling + planes + QP build + solve -> advance -> exchange, all in HBM), at
+    N = 30 (nx 9, nu 2, 2 neighbours: the v3 kernel), on lpv_population's 1023 agents.  Timed
+    over `rounds` rounds after `warmup`; then (``check``) the same rounds are replayed from the
+    start (the GPU path is deterministic) and each round's `sample` seeded agents are re-solved by
+    the C restatement with the same rescue policy: max |z - z_cpu| over the agents both solve to
+    tolerance, and the max scaled KKT residual over every agent of every round."""
+    import torch
+
+    from cmpc.rounds import LPVRounds
+
+    bp, args, kw = lpv_population(ctx, replicas, rescue)
+    N = bp.N
+    R = LPVRounds(bp, *args, **kw)
     dev = R.dev
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(rounds)]
     for _ in range(warmup):
-        R.step()
+        R.step(halt=False)
     torch.cuda.synchronize(dev)
-    st, it = [], []
+    st, it, kk = [], [], []
     t0 = time.perf_counter()
     for k in range(rounds):
-        R.step(timer=ev[k])
+        R.step(timer=ev[k], halt=False)   # (no per-round host check: the statuses are tallied after the loop)
         st.append(R.status.clone())
         it.append(R.iters.clone())
+        kk.append(R.kkt.clone())
     torch.cuda.synchronize(dev)
     el = time.perf_counter() - t0
     st = torch.stack(st).cpu().numpy()
     it = torch.stack(it).cpu().numpy()
+    kk = torch.stack(kk).cpu().numpy()
     B = 3 * replicas
-    return {"workload": f"device-resident LPV rounds: {B} agents ({replicas} copies of the reference's 3-agent "
-                        f"Highway scenario, lpv_n30_a3 step 0, v_x0 x U[0.98, 1.02]), N={N}, nx=9 nu=2 nb=2, fp64; "
-                        f"round = gather + LPV build + solve + advance + exchange",
-            "agent_qp_per_s": B * rounds / el, "ms_per_round": el / rounds * 1e3,
-            "build_solve_ms": sum(a.elapsed_time(b) for a, b in ev) / rounds, "rounds": rounds,
-            "mean_ipm_iters": float(it.mean()), "max_ipm_iters": int(it.max()),
-            "status_counts": {int(k): int(v) for k, v in zip(*np.unique(st, return_counts=True))}}
+    out = {"workload": f"device-resident LPV rounds: {B} agents ({replicas} copies of the reference's 3-agent "
+                       f"Highway scenario, lpv_n30_a3 step 0, v_x0 x U[0.98, 1.02]), N={N}, nx=9 nu=2 nb=2, fp64; "
+                       f"round = gather + LPV build + solve + advance + exchange",
+           "agent_qp_per_s": B * rounds / el, "ms_per_round": el / rounds * 1e3,
+           "build_solve_ms": sum(a.elapsed_time(b) for a, b in ev) / rounds, "rounds": rounds, "warmup": warmup,
+           "rescue": rescue, "mean_ipm_iters": float(it.mean()), "max_ipm_iters": int(it.max()),
+           "max_ipm_iters_per_round": it.max(1).tolist(), "max_kkt": float(kk.max()),
+           "status_counts": {int(k): int(v) for k, v in zip(*np.unique(st, return_counts=True))}}
+    if check:
+        R = LPVRounds(bp, *args, **kw)
+        rng = np.random.default_rng(11)
+        err, both, n = 0.0, 0, 0
+        for k in range(warmup + rounds):
+            R.gather()
+            R.solve()
+            torch.cuda.synchronize(dev)
+            if k >= warmup:
+                smp = np.sort(rng.choice(B, sample, replace=False))
+                zc, sc = lpv_check_round(bp, R, smp)
+                zg, sg = R.z.cpu().numpy()[smp], R.status.cpu().numpy()[smp]
+                ok = (sc == 1) & (sg == 1)
+                if ok.any():
+                    err = max(err, float(np.abs(zg[ok] - zc[ok]).max()))
+                both += int(ok.sum())
+                n += sample
+            R.advance()
+            R.exchange()
+        out["oracle_sample"] = {"agents_per_round": sample, "checked": n, "both_solved": both,
+                                "max_abs_err_vs_cpu": err}
+    return out
 
 
 def osqp_dropin(ctx, reps=20):

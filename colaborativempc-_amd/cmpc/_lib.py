@@ -100,6 +100,22 @@ class cmpc_di_dims(ct.Structure):
     _fields_ = [(k, ct.c_int) for k in ("batch", "N", "nb", "self_offset")]
 
 
+CMPC_ROUNDS_HOST_EXCHANGE = 1
+CMPC_ROUNDS_NO_HALT = 2
+
+
+class cmpc_lpv_rounds_dims(ct.Structure):
+    _fields_ = [(k, ct.c_int) for k in ("n_total", "batch", "self_offset", "N", "nb", "flags")]
+
+
+class cmpc_lpv_rounds_init(ct.Structure):
+    _fields_ = [("x0", _DP), ("x_last", _DP), ("u_last", _DP), ("u_old", _DP), ("nbr", _IP), ("traj", _DP)]
+
+
+class cmpc_lpv_rounds_out(ct.Structure):
+    _fields_ = [("z", _DP), ("kkt", _DP), ("iters", _IP), ("status", _IP), ("x0", _DP), ("planes", _DP)]
+
+
 class cmpc_qp_dims(ct.Structure):
     _fields_ = [(k, ct.c_int) for k in ("n", "m_ineq", "m_eq", "batch", "col_major")]
 
@@ -157,7 +173,7 @@ SIGNATURES = {
                                      ct.c_void_p]),
     "cmpc_lpv_gather_dev": (ct.c_int, [ct.c_void_p, ct.POINTER(cmpc_di_dims), _IP, _DP, _DP, _DP, ct.c_void_p]),
     "cmpc_lpv_advance_dev": (ct.c_int, [ct.c_void_p, ct.POINTER(cmpc_di_dims), _DP, _DP, _DP, _DP, _DP, _DP,
-                                        ct.c_void_p]),
+                                        _IP, _IP, ct.c_void_p]),
     "cmpc_di_advance_dev": (ct.c_int, [ct.c_void_p, ct.POINTER(cmpc_di_params), ct.POINTER(cmpc_di_dims),
                                        _DP, _DP, _DP, _DP, ct.c_void_p]),
     "cmpc_solve_qp_batch": (ct.c_int, [ct.c_void_p, ct.POINTER(cmpc_qp_dims), ct.POINTER(cmpc_qp_data),
@@ -174,6 +190,14 @@ SIGNATURES = {
     "cmpc_comm_init": (ct.c_int, [ct.c_void_p, ct.c_int, ct.c_int, ct.c_char_p]),
     "cmpc_allgather_trajectories": (ct.c_int, [ct.c_void_p, _DP, _DP, ct.c_ulonglong, ct.c_void_p]),
     "cmpc_comm_destroy": (ct.c_int, [ct.c_void_p]),
+    "cmpc_lpv_rounds_create": (ct.c_int, [ct.c_void_p, ct.POINTER(cmpc_lpv_params), ct.POINTER(cmpc_track),
+                                          ct.POINTER(cmpc_lpv_rounds_dims), ct.POINTER(cmpc_lpv_rounds_init),
+                                          ct.POINTER(cmpc_opts), ct.POINTER(ct.c_void_p)]),
+    "cmpc_lpv_rounds_step": (ct.c_int, [ct.c_void_p, ct.c_int, _IP, _IP]),
+    "cmpc_lpv_rounds_read": (ct.c_int, [ct.c_void_p, ct.POINTER(cmpc_lpv_rounds_out)]),
+    "cmpc_lpv_rounds_get_traj": (ct.c_int, [ct.c_void_p, _DP]),
+    "cmpc_lpv_rounds_set_traj": (ct.c_int, [ct.c_void_p, _DP]),
+    "cmpc_lpv_rounds_destroy": (ct.c_int, [ct.c_void_p]),
 }
 
 CMPC_COMM_ID_BYTES = 128

@@ -208,7 +208,7 @@ class LPVRounds:
         self.dev = torch.device("cuda", self.ctx.device)
         T = lambda a, dt=torch.float64: torch.as_tensor(np.ascontiguousarray(a), dtype=dt, device=self.dev)  # noqa
         x_last = np.asarray(x_last, np.float64)
-        if x_last.shape[1:] != (N + 1, 9):
+        if x_last.shape != (n, N + 1, 9):   # the gather / builder kernels trust these extents
             raise ValueError("x_last: the first round's Last_xPredicted, (n, N+1, 9)")
         self.x0 = T(x0[sl])
         self.x_last = T(x_last[sl])
@@ -216,7 +216,9 @@ class LPVRounds:
         self.u_old = T(np.zeros((n, 2)) if u_old is None else np.asarray(u_old, np.float64))[sl].contiguous()
         self.nbr = T(nbr[sl], torch.int32)
         self.traj_all = T(x_last[:, :, 7:9] if traj is None else traj)
-        self.traj_local = torch.empty((self.B, N + 1, 2), dtype=torch.float64, device=self.dev)
+        # this rank's rows of the exchange buffer; an agent that is not advanced (no finite
+        # solution) keeps them, so they start as the initial trajectories
+        self.traj_local = self.traj_all[sl].clone()
         self.pose = torch.empty((self.B, N + 1, 2), dtype=torch.float64, device=self.dev)
         self.x_agents = torch.empty((self.B, N + 1, max(self.nb, 1), 2), dtype=torch.float64, device=self.dev)
         nz = 12 * (N + 1) + 4 * N
@@ -227,6 +229,8 @@ class LPVRounds:
         self.status = torch.empty(self.B, dtype=torch.int32, device=self.dev)
         self.last_rows = N + 1
         self.rdims = L.cmpc_di_dims(self.B, N, self.nb, self.off)
+        # agents of the latest round the reference calls infeasible (status not in {1, 2, -2})
+        self.n_infeasible = torch.zeros(1, dtype=torch.int32, device=self.dev)
 
     def _stream(self):
         return ct.c_void_p(self.torch.cuda.current_stream(self.dev).cuda_stream)
@@ -249,16 +253,24 @@ class LPVRounds:
                                                     self._stream()))
 
     def advance(self):
+        """x0 <- xPred[1], Last_xPredicted <- xPred[1:], uPred, u_old <- u_0, the exchanged X, Y; an agent
+        without a finite solution keeps its state and trajectory; infeasible agents are counted."""
+        self.n_infeasible.zero_()
         self.ctx.check(self.ctx.lib.cmpc_lpv_advance_dev(self.ctx.h, ct.byref(self.rdims), _tptr(self.z),
                                                          _tptr(self.x0), _tptr(self.x_last), _tptr(self.u_last),
-                                                         _tptr(self.u_old), _tptr(self.traj_local), self._stream()))
+                                                         _tptr(self.u_old), _tptr(self.traj_local),
+                                                         _tptr(self.status), _tptr(self.n_infeasible),
+                                                         self._stream()))
         self.last_rows = self.N   # x_old = xPred[1:] from now on (LPV_HP_N_main.py:115)
 
     def exchange(self):
         exchange_positions(self.traj_all, self.traj_local, self.world, self.group, self.comm)
 
-    def step(self, timer=None):
-        """One consensus round.  `timer` (start, stop) events bracket the build + solve launch."""
+    def step(self, timer=None, halt=True):
+        """One consensus round.  `timer` (start, stop) events bracket the build + solve launch.
+        ``halt``: like the reference (LPV_HP_N_main.py:102-111, "QUIT..."), raise InfeasibleRound when an
+        agent of this rank is infeasible (reads a device counter: one host synchronisation per round;
+        ``halt=False`` leaves the check to the caller, ``infeasible()``)."""
         self.gather()
         if timer is not None:
             timer[0].record()
@@ -267,3 +279,88 @@ class LPVRounds:
             timer[1].record()
         self.advance()
         self.exchange()
+        if halt:
+            bad = self.infeasible()
+            if bad:
+                raise InfeasibleRound(bad)
+
+    def infeasible(self):
+        """Infeasible agents of this rank in the latest round (synchronises)."""
+        return int(self.n_infeasible.item())
+
+
+class InfeasibleRound(RuntimeError):
+    """A round left agents infeasible (status not in {1, 2, -2}, LPV_Planner.py:243-249); the
+    reference stops the experiment there (LPV_HP_N_main.py:102-111)."""
+
+    def __init__(self, count):
+        super().__init__(f"{count} agent(s) infeasible in this round: QUIT (LPV_HP_N_main.py:102-111)")
+        self.count = count
+
+
+class LPVRoundsHandle:
+    """The same rounds through the C ABI's round handle (cmpc_lpv_rounds_*): the library owns the
+    device state; no torch.  What a MATLAB (MEX) or C host drives.  Arguments as LPVRounds;
+    ``host_exchange``: the caller exchanges positions between steps (get_traj / set_traj)."""
+
+    def __init__(self, bp, x0, x_last, u_last, nbr, u_old=None, traj=None, rank=0, world=1, host_exchange=False,
+                 halt=True):
+        self.bp, self.ctx = bp, bp.ctx
+        x0 = L.f64(x0)
+        n, N = x0.shape[0], bp.N
+        nbr = L.i32(np.asarray(nbr).reshape(n, -1))
+        if n % world:
+            raise ValueError("agents must be divisible by the number of ranks")
+        B = n // world
+        sl = slice(rank * B, (rank + 1) * B)
+        self.N, self.nb, self.B, self.n = N, nbr.shape[1], B, n
+        flags = (L.CMPC_ROUNDS_HOST_EXCHANGE if host_exchange else 0) | (0 if halt else L.CMPC_ROUNDS_NO_HALT)
+        self.dims = L.cmpc_lpv_rounds_dims(n, B, rank * B, N, self.nb, flags)
+        keep = [L.f64(x0[sl]), L.f64(np.asarray(x_last)[sl]), L.f64(np.asarray(u_last)[sl]),
+                None if u_old is None else L.f64(np.asarray(u_old)[sl]), L.i32(nbr[sl]),
+                None if traj is None else L.f64(traj)]
+        init = L.cmpc_lpv_rounds_init(L.dptr(keep[0]), L.dptr(keep[1]), L.dptr(keep[2]), L.dptr(keep[3]),
+                                      L.iptr(keep[4]), L.dptr(keep[5]))
+        h = ct.c_void_p()
+        self.ctx.check(self.ctx.lib.cmpc_lpv_rounds_create(self.ctx.h, ct.byref(bp.prm), ct.byref(bp.track),
+                                                           ct.byref(self.dims), ct.byref(init), ct.byref(bp.opts),
+                                                           ct.byref(h)))
+        self.h = h
+
+    def step(self, rounds=1):
+        """Runs up to `rounds` rounds; returns (rounds done, infeasible agents of the last one)."""
+        done, bad = ct.c_int(), ct.c_int()
+        self.ctx.check(self.ctx.lib.cmpc_lpv_rounds_step(self.h, int(rounds), ct.byref(done), ct.byref(bad)))
+        return done.value, bad.value
+
+    def read(self):
+        nz = 12 * (self.N + 1) + 4 * self.N
+        r = dict(z=np.zeros((self.B, nz)), kkt=np.zeros(self.B), iters=np.zeros(self.B, np.int32),
+                 status=np.zeros(self.B, np.int32), x0=np.zeros((self.B, 9)),
+                 planes=np.zeros((self.B, self.N, 3, self.nb)))
+        o = L.cmpc_lpv_rounds_out(L.dptr(r["z"]), L.dptr(r["kkt"]), L.iptr(r["iters"]), L.iptr(r["status"]),
+                                  L.dptr(r["x0"]), L.dptr(r["planes"]) if self.nb else None)
+        self.ctx.check(self.ctx.lib.cmpc_lpv_rounds_read(self.h, ct.byref(o)))
+        return r
+
+    def get_traj(self):
+        t = np.zeros((self.B, self.N + 1, 2))
+        self.ctx.check(self.ctx.lib.cmpc_lpv_rounds_get_traj(self.h, L.dptr(t)))
+        return t
+
+    def set_traj(self, traj_all):
+        t = L.f64(traj_all)
+        if t.shape != (self.n, self.N + 1, 2):
+            raise ValueError("traj_all: (n_total, N+1, 2)")
+        self.ctx.check(self.ctx.lib.cmpc_lpv_rounds_set_traj(self.h, L.dptr(t)))
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.ctx.lib.cmpc_lpv_rounds_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

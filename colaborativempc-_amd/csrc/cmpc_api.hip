@@ -6,35 +6,9 @@
 #include <cstring>
 #include <string>
 
-#include <rccl/rccl.h>
-
-#include "internal.h"
-
-struct cmpc_ctx {
-    int device = 0;
-    hipStream_t stream = nullptr;  // private stream for the host-pointer entry points
-    char* ws = nullptr;            // device arena
-    size_t ws_bytes = 0;
-    ncclComm_t comm = nullptr;     // RCCL communicator of cmpc_comm_init (multi-GPU exchange)
-    std::string err;
-};
+#include "ctx.h"
 
 namespace {
-
-int fail(cmpc_ctx* c, int code, const std::string& msg) {
-    if (c) c->err = msg;
-    return code;
-}
-
-int hip_fail(cmpc_ctx* c, hipError_t e, const char* where) {
-    return fail(c, CMPC_ERR_DEVICE, std::string(where) + ": " + hipGetErrorString(e));
-}
-
-#define HIP_TRY(expr)                                    \
-    do {                                                 \
-        hipError_t e_ = (expr);                          \
-        if (e_ != hipSuccess) return hip_fail(ctx, e_, #expr); \
-    } while (0)
 
 // Ensure the device arena holds `bytes`; returns base pointer or nullptr.
 char* arena(cmpc_ctx* ctx, size_t bytes) {
@@ -102,10 +76,15 @@ int build_lpv_const(cmpc_ctx* ctx, const cmpc_lpv_params* prm, const cmpc_track*
 
 int lpv_solver_const(cmpc_ctx* ctx, const cmpc_lpv_params* prm, const cmpc_lpv_dims* d, const cmpc_opts* o,
                      cmpc::MpcConst* mc) {
+    // checked here as well as in build_lpv_const: this runs first in both LPV entry points and
+    // fills fixed-size row tables
+    if (!prm || !d) return fail(ctx, CMPC_ERR_ARG, "null argument");
+    if (d->N < 1 || d->nb < 0 || 4 + d->nb > CMPC_MAX_MC || d->batch < 0)
+        return fail(ctx, CMPC_ERR_ARG, "bad LPV dimensions (N >= 1, 0 <= nb <= 12)");
     cmpc_mpc_dims md{9, 2, d->N, 3, 4 + d->nb, d->batch};
     int slack[CMPC_MAX_MC], sign[CMPC_MAX_MC];
     const int base_slack[4] = {-1, 0, 1, 1};
-    for (int r = 0; r < md.mc; ++r) {
+    for (int r = 0; r < md.mc && r < CMPC_MAX_MC; ++r) {
         slack[r] = r < 4 ? base_slack[r] : 2;
         sign[r] = r < 4 ? 1 : -1;
     }
@@ -177,6 +156,8 @@ int cmpc_comm_init(cmpc_ctx* ctx, int nranks, int rank, const unsigned char id[C
         ctx->comm = nullptr;
         return fail(ctx, CMPC_ERR_DEVICE, std::string("ncclCommInitRank: ") + ncclGetErrorString(r));
     }
+    ctx->nranks = nranks;
+    ctx->rank = rank;
     return CMPC_OK;
 }
 
@@ -198,6 +179,8 @@ int cmpc_comm_destroy(cmpc_ctx* ctx) {
         (void)set_device(ctx);
         (void)ncclCommDestroy(ctx->comm);
         ctx->comm = nullptr;
+        ctx->nranks = 1;
+        ctx->rank = 0;
     }
     return CMPC_OK;
 }
@@ -326,13 +309,15 @@ int cmpc_lpv_gather_dev(cmpc_ctx* ctx, const cmpc_di_dims* d, const int* nbr, co
 }
 
 int cmpc_lpv_advance_dev(cmpc_ctx* ctx, const cmpc_di_dims* d, const double* z, double* x0, double* x_last,
-                         double* u_last, double* u_old, double* traj_local, void* stream) {
+                         double* u_last, double* u_old, double* traj_local, const int* status, int* infeasible,
+                         void* stream) {
     if (!ctx) return CMPC_ERR_ARG;
     if (!d || !z || !x0 || !x_last || !u_last || !u_old || !traj_local) return fail(ctx, CMPC_ERR_ARG, "null argument");
     if (d->N < 1 || d->batch < 0) return fail(ctx, CMPC_ERR_ARG, "bad dimensions");
     int rc = set_device(ctx);
     if (rc != CMPC_OK) return rc;
-    HIP_TRY(cmpc::lpv_advance_launch(d->N, z, x0, x_last, u_last, u_old, traj_local, d->batch, (hipStream_t)stream));
+    HIP_TRY(cmpc::lpv_advance_launch(d->N, z, x0, x_last, u_last, u_old, traj_local, d->batch, (hipStream_t)stream,
+                                     status, infeasible));
     return CMPC_OK;
 }
 

@@ -155,8 +155,11 @@ hipError_t lpv_mark_launch(const int* err, int* status, double* z, int nz, int b
 // and the round update from the solution
 hipError_t lpv_gather_launch(int N, int nb, int self_offset, const int* nbr, const double* traj_all, double* x_agents,
                              double* pose, int batch, hipStream_t s);
+// status / infeasible (both may be null): count the agents the reference calls infeasible
+// (status not in {1, 2, -2}) into *infeasible; an agent with a non-finite z is not advanced
 hipError_t lpv_advance_launch(int N, const double* z, double* x0, double* x_last, double* u_last, double* u_old,
-                              double* traj_local, int batch, hipStream_t s);
+                              double* traj_local, int batch, hipStream_t s, const int* status = nullptr,
+                              int* infeasible = nullptr);
 
 // Synthetic double-integrator family (bench workload).
 

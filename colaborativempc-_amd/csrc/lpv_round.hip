@@ -32,11 +32,22 @@ __global__ __launch_bounds__(kWave) void lpv_gather_kernel(int N, int nb, int se
 
 __global__ __launch_bounds__(kWave) void lpv_advance_kernel(int N, const double* __restrict__ z, double* x0,
                                                             double* x_last, double* u_last, double* u_old,
-                                                            double* traj_local) {
+                                                            double* traj_local, const int* __restrict__ status,
+                                                            int* infeasible) {
     const int b = blockIdx.x;
     const size_t nz = (size_t)kNexp * (N + 1) + 2 * (size_t)kNu * N;
     const double* zb = z + (size_t)b * nz;
     const double* up = zb + (size_t)kNexp * (N + 1);
+    // the reference's feasibility rule (LPV_Planner.py:243-249): status in {1, 2, -2}
+    if (status && infeasible && threadIdx.x == 0) {
+        const int st = status[b];
+        if (st != CMPC_SOLVED && st != CMPC_SOLVED_INACCURATE && st != CMPC_MAX_ITER_REACHED) atomicAdd(infeasible, 1);
+    }
+    // an agent without a finite solution (the builder's track lookup failed: the reference raises,
+    // misc.py:97) keeps its state and its previous trajectory: no NaN reaches a neighbour
+    bool bad = false;
+    for (size_t i = threadIdx.x; i < nz; i += kWave) bad |= !isfinite(zb[i]);
+    if (__any(bad)) return;
     for (int i = threadIdx.x; i < N * kNs; i += kWave) {  // xPred[1:], rows 1..N
         const int k = i / kNs + 1, s = i - (k - 1) * kNs;
         x_last[(size_t)b * N * kNs + i] = zb[(size_t)k * kNexp + s];  // dense (B, N, 9) from now on
@@ -60,10 +71,10 @@ hipError_t lpv_gather_launch(int N, int nb, int self_offset, const int* nbr, con
 }
 
 hipError_t lpv_advance_launch(int N, const double* z, double* x0, double* x_last, double* u_last, double* u_old,
-                              double* traj_local, int batch, hipStream_t s) {
+                              double* traj_local, int batch, hipStream_t s, const int* status, int* infeasible) {
     if (batch == 0) return hipSuccess;
     hipLaunchKernelGGL(lpv_advance_kernel, dim3(batch), dim3(kWave), 0, s, N, z, x0, x_last, u_last, u_old,
-                       traj_local);
+                       traj_local, status, infeasible);
     return hipGetLastError();
 }
 

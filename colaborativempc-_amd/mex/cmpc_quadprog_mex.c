@@ -192,7 +192,9 @@ static void ensure_ctx(void) {
 }
 
 void mexFunction(int nlhs, mxArray* plhs[], int nrhs, const mxArray* prhs[]) {
-    free_dense();
+    /* forget (do not free) the list: a previous call that ended in mexErrMsgIdAndTxt left its
+       mxCalloc buffers to MATLAB, which frees non-persistent memory when a MEX call errors out */
+    g_ndense = 0;
     if (nrhs == 1 && mxIsStruct(prhs[0])) {
         ensure_ctx();
         mpc_struct(nlhs, plhs, prhs[0]);

@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define CMPC_ABI_VERSION 1
+#define CMPC_ABI_VERSION 2   /* 2: cmpc_lpv_advance_dev status / infeasible, cmpc_lpv_rounds_* */
 
 /* API error codes */
 #define CMPC_OK 0
@@ -272,12 +272,83 @@ int cmpc_di_advance_dev(cmpc_ctx* ctx, const cmpc_di_params* prm, const cmpc_di_
  *   cmpc_lpv_advance_dev: from z (reference layout): x0 <- xPred[1], x_last <- xPred[1:] written
  *     DENSE as batch x N x 9 (last_rows = N from the second round on, :115), u_last <- uPred
  *     (batch x N x 2, not shifted), u_old <- uPred[0] (:179-180), traj_local (batch x (N+1) x 2)
- *     <- xPred[:, X, Y] (:117);
+ *     <- xPred[:, X, Y] (:117); status (may be NULL) / infeasible (may be NULL, DEVICE int): the
+ *     count of agents the reference calls infeasible (status not in {1, 2, -2}, LPV_Planner.py:243-249)
+ *     is added to *infeasible; an agent whose z is not finite is not advanced (no NaN is exchanged);
  *   then the all-gather of traj_local into traj_all (cmpc_allgather_trajectories or torch). */
 int cmpc_lpv_gather_dev(cmpc_ctx* ctx, const cmpc_di_dims* dims, const int* nbr, const double* traj_all,
                         double* x_agents, double* pose, void* hip_stream);
 int cmpc_lpv_advance_dev(cmpc_ctx* ctx, const cmpc_di_dims* dims, const double* z, double* x0, double* x_last,
-                         double* u_last, double* u_old, double* traj_local, void* hip_stream);
+                         double* u_last, double* u_old, double* traj_local, const int* status, int* infeasible,
+                         void* hip_stream);
+
+/* ------------------------------------------------------------------------
+ * Consensus rounds behind a handle (LPV_HP_N_main.py:96-117; the one-process-per-agent ROS
+ * variant ROS/src/planner_experiments/src/LPV_ROS_main.py:66-77,124-150), for hosts without
+ * torch or device memory of their own (MATLAB through the MEX gateway, plain C).  The handle
+ * owns every device buffer of this rank's agents and the node-global exchange buffer; a round
+ * is gather -> cmpc_solve_lpv_batch_dev -> cmpc_lpv_advance_dev -> exchange, all on the
+ * context's stream, so consecutive rounds never touch the host.
+ *
+ * Sharding: this rank holds agents [self_offset, self_offset + batch) of n_total.  The exchange
+ * of a round is the identity when batch == n_total; otherwise an RCCL all-gather over the
+ * context's communicator (cmpc_comm_init; ranks hold equal contiguous shards in rank order),
+ * or — CMPC_ROUNDS_HOST_EXCHANGE — the host's: after cmpc_lpv_rounds_step the host reads this
+ * rank's positions (cmpc_lpv_rounds_get_traj), exchanges them its own way (MPI, sockets) and
+ * hands the gathered buffer back (cmpc_lpv_rounds_set_traj) before the next step.
+ *
+ * Failure semantics (LPV_Planner.py:243-249, LPV_HP_N_main.py:102-111): an agent is
+ * infeasible when its status is not in {1, 2, -2}; the reference quits the experiment there.
+ * cmpc_lpv_rounds_step counts infeasible agents per round on the device and stops after the
+ * first round that has any (rounds_done < rounds); an agent whose solution is not finite
+ * (track lookup failed, the reference raises) keeps its previous state and trajectory, so no
+ * NaN reaches a neighbour.
+ * ---------------------------------------------------------------------- */
+typedef struct cmpc_lpv_rounds cmpc_lpv_rounds;
+
+#define CMPC_ROUNDS_HOST_EXCHANGE 1  /* the host exchanges positions between steps */
+#define CMPC_ROUNDS_NO_HALT 2        /* run all requested rounds even after an infeasible agent */
+
+typedef struct {
+    int n_total;      /* agents over all ranks */
+    int batch;        /* agents of this rank */
+    int self_offset;  /* global index of this rank's agent 0 */
+    int N, nb;        /* horizon, neighbours per agent */
+    int flags;        /* CMPC_ROUNDS_* */
+} cmpc_lpv_rounds_dims;
+
+typedef struct {   /* HOST pointers, this rank's agents, batch-major (copied at create) */
+    const double* x0;      /* batch x 9 */
+    const double* x_last;  /* batch x (N+1) x 9: the first round's Last_xPredicted */
+    const double* u_last;  /* batch x N x 2 */
+    const double* u_old;   /* batch x 2, or NULL (zeros: PlannerLPV's initial OldSteering/OldAccelera) */
+    const int* nbr;        /* batch x nb global agent indices (the reference: all other agents) */
+    const double* traj;    /* n_total x (N+1) x 2 initial exchange buffer (the reference's `agents`);
+                              NULL: only valid when batch == n_total, taken from x_last[:, :, 7:9] */
+} cmpc_lpv_rounds_init;
+
+typedef struct {   /* HOST pointers (any may be NULL): the latest round of this rank's agents */
+    double* z;       /* batch x nz (nz = 12(N+1) + 4N) */
+    double* kkt;     /* batch */
+    int* iters;      /* batch */
+    int* status;     /* batch */
+    double* x0;      /* batch x 9: the next round's initial states */
+    double* planes;  /* batch x N x 3 x nb */
+} cmpc_lpv_rounds_out;
+
+int cmpc_lpv_rounds_create(cmpc_ctx* ctx, const cmpc_lpv_params* prm, const cmpc_track* track,
+                           const cmpc_lpv_rounds_dims* dims, const cmpc_lpv_rounds_init* init,
+                           const cmpc_opts* opts, cmpc_lpv_rounds** out);
+/* Runs up to `rounds` rounds; *rounds_done (may be NULL) receives the number completed and
+ * *infeasible (may be NULL) the infeasible-agent count of the last one.  Synchronises the host. */
+int cmpc_lpv_rounds_step(cmpc_lpv_rounds* h, int rounds, int* rounds_done, int* infeasible);
+int cmpc_lpv_rounds_read(cmpc_lpv_rounds* h, const cmpc_lpv_rounds_out* host_out);
+/* Host exchange: this rank's predicted positions (batch x (N+1) x 2) / the gathered buffer
+ * (n_total x (N+1) x 2, rank order). */
+int cmpc_lpv_rounds_get_traj(cmpc_lpv_rounds* h, double* traj_local);
+int cmpc_lpv_rounds_set_traj(cmpc_lpv_rounds* h, const double* traj_all);
+/* Destroy every handle of a context before cmpc_destroy(ctx). */
+int cmpc_lpv_rounds_destroy(cmpc_lpv_rounds* h);
 
 
 /* ------------------------------------------------------------------------

@@ -17,7 +17,7 @@
  * (oracle/qp_ipm.py) on QPs captured from the reference (tests/golden).
  */
 #include <math.h>
-#if defined(ORACLE_TRACE) || defined(RIC_DEBUG)
+#if defined(ORACLE_TRACE) || defined(RIC_DEBUG) || defined(LAB_THDUMP) || defined(DIRCHECK)
 #include <stdio.h>
 #endif
 #include <stdlib.h>
@@ -104,6 +104,12 @@ long cmpc_gz_solves = 0; /* lab: corrector solves performed */
 #define REF_TOL 1e-13 /* refinement stops once |correction| <= REF_TOL |dU| (kernel: kRefineTol) */
 #endif
 
+#ifndef LR_MAX
+#define LR_MAX 4
+#endif
+#ifndef CREF_TH
+#define CREF_TH 1e10
+#endif
 #ifndef T0_FLOOR
 #define T0_FLOOR 0.5    /* starting slacks t_r = max(w_r - g_r, T0_FLOOR) (internal.h kT0Floor) */
 #endif
@@ -1142,6 +1148,28 @@ static int solve_one(const shared_t* S, const agent_t* a, double tol, int max_it
             if (hp ? ric_factor_dd(S, a, wk->th, wk->Dsig, wk->F) : ric_factor(S, a, wk->th, wk->Dsig, wk->F)) { stop = 2; break; }
 #endif
         }
+#ifdef LOWRANK
+        /* lab: slack-free state rows whose weight exceeds LOWRANK leave the normal matrix (M) and
+           return as a rank-|L| correction (Sherman-Morrison-Woodbury on the augmented system):
+           K = M + G_L' Th_L G_L,  K^-1 r = M^-1 r - Y S^-1 G_L M^-1 r,  Y = M^-1 G_L',
+           S = Th_L^-1 + G_L Y.  A dense row with theta ~ 1e20 no longer swamps M. */
+        int nL = 0, Lr[LR_MAX];
+        double Lth[LR_MAX];
+        for (int r = 0; r < ms && !S->newton; ++r) {
+            if (!wk->act[r] || S->row_slack[r % mc] >= 0 || !(wk->th[r] > LOWRANK)) continue;
+            int pos = nL < LR_MAX ? nL++ : -1;
+            if (pos < 0) { /* keep the LR_MAX largest */
+                int mn = 0;
+                for (int l = 1; l < LR_MAX; ++l) if (Lth[l] < Lth[mn]) mn = l;
+                if (wk->th[r] <= Lth[mn]) continue;
+                wk->th[Lr[mn]] = Lth[mn];
+                pos = mn;
+            }
+            Lr[pos] = r;
+            Lth[pos] = wk->th[r];
+            wk->th[r] = 0.0;
+        }
+#endif
         if (!NEWTON_C) memset(K, 0, sizeof(double) * n * n);
         for (int k = 0; k < N && !NEWTON_C; ++k) {
             /* W = 2Q + M_{k+1} (stable group Schur forms) */
@@ -1199,7 +1227,46 @@ static int solve_one(const shared_t* S, const agent_t* a, double tol, int max_it
         const int chol_bad = chol(K, n);
         if (!S->newton && chol_bad) { stop = 2; break; }
 #else
-        if (!S->newton && chol(K, n)) { stop = 2; break; }
+        if (!S->newton && chol(K, n)) {
+#ifdef LAB_THDUMP
+            /* lab: the rows whose weight broke the factorisation */
+            fprintf(stderr, "breakdown it %d:", it);
+            for (int r = 0; r < m; ++r)
+                if (wk->act[r] && wk->th[r] > LAB_THDUMP)
+                    fprintf(stderr, " r%d(k%d,%s%d th%.1e)", r, r < ms ? r / mc : (r - ms) / (2 * nu), r < ms ? "row" : "in",
+                            r < ms ? r % mc : (r - ms) % (2 * nu), wk->th[r]);
+            fprintf(stderr, "\n");
+#endif
+            stop = 2;
+            break;
+        }
+#endif
+#ifdef LOWRANK
+        double *LG = NULL, *LY = NULL, LS[LR_MAX * LR_MAX];
+        if (nL) {
+            for (int l = 0; l < nL; ++l) wk->th[Lr[l]] = Lth[l];
+            LG = malloc(sizeof(double) * 2 * (size_t)nL * n);
+            LY = LG + (size_t)nL * n;
+            for (int l = 0; l < nL; ++l) {
+                const int k = Lr[l] / mc;
+                const double* c_ = a->C + (size_t)Lr[l] * nx;
+                const double* G = Gam + (size_t)(k + 1) * nx * n;
+                for (int c = 0; c < n; ++c) {
+                    double v = 0.0;
+                    for (int s = 0; s < nx; ++s) v += c_[s] * G[s * n + c];
+                    LG[(size_t)l * n + c] = v;
+                }
+                memcpy(LY + (size_t)l * n, LG + (size_t)l * n, sizeof(double) * n);
+                chol_solve(K, n, LY + (size_t)l * n);
+            }
+            for (int l = 0; l < nL; ++l)
+                for (int l2 = 0; l2 < nL; ++l2) {
+                    double v = l == l2 ? 1.0 / Lth[l] : 0.0;
+                    for (int c = 0; c < n; ++c) v += LG[(size_t)l * n + c] * LY[(size_t)l2 * n + c];
+                    LS[l * nL + l2] = v;
+                }
+            if (chol(LS, nL)) { free(LG); stop = 2; break; }
+        }
 #endif
 
         /* ---- predictor / corrector ---- */
@@ -1236,6 +1303,10 @@ static int solve_one(const shared_t* S, const agent_t* a, double tol, int max_it
                     }
                     wk->rt[R1] = v / wk->Dsig[k * ns + j];
                 }
+#ifdef LOWRANK
+            /* the separated rows' rho enters through the small system (bounded: rho/theta = rc/lam + rp) */
+            for (int l = 0; l < nL; ++l) wk->rt[Lr[l]] = 0.0;
+#endif
             memset(ybar, 0, sizeof(double) * (N + 1) * nx);
             for (int k = 0; k < N; ++k)
                 for (int r = 0; r < mc; ++r) {
@@ -1307,6 +1378,53 @@ static int solve_one(const shared_t* S, const agent_t* a, double tol, int max_it
             } else {
                 memcpy(wk->dU, wk->rhs, sizeof(double) * n);
                 chol_solve(K, n, wk->dU);
+#ifdef LOWRANK
+                if (nL) {
+                    double v[LR_MAX];
+                    for (int l = 0; l < nL; ++l) {
+                        double s = 0.0;
+                        for (int c = 0; c < n; ++c) s += LG[(size_t)l * n + c] * wk->dU[c];
+                        v[l] = s + wk->rho[Lr[l]] / Lth[l];
+                    }
+                    chol_solve(LS, nL, v);
+                    for (int l = 0; l < nL; ++l)
+                        for (int c = 0; c < n; ++c) wk->dU[c] -= LY[(size_t)l * n + c] * v[l];
+                }
+#endif
+#ifdef DIRCHECK
+                {   /* lab: relative Newton residual |rhs - K dU| / |rhs| of the direction, in double-double */
+                    double* kv = wk->Yk;
+#ifdef LOWRANK
+                    for (int l = 0; l < nL; ++l)
+                        for (int c = 0; c < n; ++c) wk->rhs[c] -= wk->rho[Lr[l]] * LG[(size_t)l * n + c];
+#endif
+                    kres_dd(S, a, wk->th, wk->Dsig, wk->dU, wk->rhs, kv, wk->Xdd);
+                    double rn = 0.0, bn = 0.0, thm = 0.0;
+                    for (int c = 0; c < n; ++c) { rn = fmax(rn, fabs(kv[c])); bn = fmax(bn, fabs(wk->rhs[c])); }
+                    for (int r = 0; r < m; ++r) if (wk->act[r] && wk->th[r] > thm) thm = wk->th[r];
+                    fprintf(stderr, "   it %d pass %d newton residual %.2e (|rhs| %.2e) thmax %.1e\n", it, pass, rn / bn, bn, thm);
+                }
+#endif
+#ifdef CREFINE
+                /* lab: iterative refinement of the condensed direction against the Newton residual
+                   evaluated in double-double (the fp64 Cholesky as the preconditioner) */
+                {
+                    double thm = 0.0;
+                    for (int r = 0; r < m; ++r) if (wk->act[r] && wk->th[r] > thm) thm = wk->th[r];
+                    for (int ir = 0; ir < CREFINE && thm > CREF_TH; ++ir) {
+                        double* kv = wk->Yk;
+                        kres_dd(S, a, wk->th, wk->Dsig, wk->dU, wk->rhs, kv, wk->Xdd);
+                        chol_solve(K, n, kv);
+                        double cn = 0.0, un = 0.0;
+                        for (int c = 0; c < n; ++c) {
+                            wk->dU[c] += kv[c];
+                            cn = fmax(cn, fabs(kv[c]));
+                            un = fmax(un, fabs(wk->dU[c]));
+                        }
+                        if (cn <= REF_TOL * un) break;
+                    }
+                }
+#endif
                 fwd_sim(S, a, NULL, wk->dU, wk->dX);
             }
             for (int r = 0; r < m; ++r) {
@@ -1442,6 +1560,9 @@ static int solve_one(const shared_t* S, const agent_t* a, double tol, int max_it
                 for (int q = 0; q < (N + 1) * nx; ++q) X[q] += al * wk->dX[q];
             }
         }
+#ifdef LOWRANK
+        free(LG);
+#endif
     }
 #ifdef GONDZIO
 #pragma omp atomic

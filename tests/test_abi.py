@@ -20,7 +20,8 @@ def test_header_declares_the_boundary():
     fns = declared_functions()
     for need in ("cmpc_create", "cmpc_destroy", "cmpc_solve_mpc_batch", "cmpc_solve_mpc_batch_dev",
                  "cmpc_solve_lpv_batch", "cmpc_solve_lpv_batch_dev", "cmpc_di_build_dev", "cmpc_di_solve_dev",
-                 "cmpc_di_advance_dev", "cmpc_lpv_gather_dev", "cmpc_lpv_advance_dev"):
+                 "cmpc_di_advance_dev", "cmpc_lpv_gather_dev", "cmpc_lpv_advance_dev", "cmpc_lpv_rounds_create",
+                 "cmpc_lpv_rounds_step", "cmpc_lpv_rounds_read", "cmpc_lpv_rounds_destroy"):
         assert need in fns
 
 
@@ -32,7 +33,7 @@ def test_library_exports_every_declared_symbol():
 
 
 def test_abi_version():
-    assert L.load().cmpc_abi_version() == 1
+    assert L.load().cmpc_abi_version() == 2
 
 
 def test_no_cpu_fallback_without_device():

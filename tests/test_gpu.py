@@ -406,6 +406,53 @@ def test_unsupported_sizes_are_rejected(gpu_ctx):
         cmpc.solve_mpc(p, gpu_ctx)
 
 
+def test_lpv_too_many_neighbours_is_an_argument_error(gpu_ctx):
+    """4 + nb rows per stage must fit CMPC_MAX_MC (16): a PlannerLPV batch with nb = 13 (14 agents
+    all-to-all, LPV_HP_N_main.py:82-85) is rejected with CMPC_ERR_ARG before any table is filled,
+    on both LPV entry points; nb = 12 still runs."""
+    import ctypes as ct
+
+    import torch
+
+    import cmpc
+    from cmpc import _lib as L
+    from oracle import lpv_ref as LR
+
+    g, model = _gains()
+    N = 10
+    bp = cmpc.PlannerLPVBatch(g["Q"], g["Qs"], g["R"], g["dR"], N, 0.025, LR.Track.build("Highway"), g["wq"], model,
+                              LR.scaled_car_limits(), ctx=gpu_ctx)
+    x0 = np.tile([1.3, 0, 0, 0, 0, 0, 0.5, 1.0, 1.5], (1, 1))
+    x_last = np.tile(x0[:, None, :], (1, N + 1, 1))
+    x_last[0, :, 6] += 0.03 * np.arange(N + 1)
+    for nb, ok in ((13, False), (12, True)):
+        xa = np.tile(x_last[:, :, None, 7:9], (1, 1, nb, 1)) + 0.5 * (1 + np.arange(nb))[None, None, :, None]
+        args = (x0, x_last, np.zeros((1, N, 2)), np.zeros((1, 2)), xa, x_last[:, :, 7:9])
+        if ok:
+            assert bp.solve(*args)["status"][0] in (cmpc.CMPC_SOLVED, cmpc.CMPC_SOLVED_INACCURATE)
+            continue
+        with pytest.raises(cmpc.CmpcError) as ei:
+            bp.solve(*args)
+        assert ei.value.code == L.CMPC_ERR_ARG
+        dev = torch.device("cuda", gpu_ctx.device)
+        T = lambda a: torch.as_tensor(np.ascontiguousarray(a, np.float64), device=dev)  # noqa: E731
+        tz = torch.zeros((1, 12 * (N + 1) + 4 * N), dtype=torch.float64, device=dev)
+        ins = [T(a) for a in (x0, x_last, args[2], args[3], xa, args[5])]
+        p = lambda t: ctypes_ptr(t, L)  # noqa: E731
+        data = L.cmpc_lpv_data(*[p(t) for t in ins])
+        out = L.cmpc_lpv_out(p(tz), None, None, None, None)
+        rc = gpu_ctx.lib.cmpc_solve_lpv_batch_dev(gpu_ctx.h, ct.byref(bp.prm), ct.byref(bp.track),
+                                                  ct.byref(L.cmpc_lpv_dims(1, N, nb, N + 1)), ct.byref(data),
+                                                  ct.byref(out), ct.byref(bp.opts), None)
+        assert rc == L.CMPC_ERR_ARG
+
+
+def ctypes_ptr(t, L):
+    import ctypes as ct
+
+    return ct.cast(ct.c_void_p(t.data_ptr()), L._DP)
+
+
 @pytest.mark.parametrize("n,N,nb,dim", [(48, 40, 2, 2), (8, 130, 1, 2), (64, 50, 2, 3)])
 def test_long_horizon_riccati_solver(gpu_ctx, n, N, nb, dim):
     """N*nu > 64: the stage-wise Riccati solver (fp64) vs the C restatement — including

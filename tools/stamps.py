@@ -1,5 +1,7 @@
-"""Diagnostic: per-section shader-clock breakdown of the v3 solver kernel (cfg3 round-0
-problem).  Usage: python tools/stamps.py [agents] [N]"""
+"""Diagnostic: per-section shader-clock breakdown of the v3 solver kernel.
+Usage: python tools/stamps.py [agents] [N]          cfg3 round-0 problem (double integrator)
+       python tools/stamps.py --lpv [round]         bench.py's lpv_rounds population (nx 9) at that
+                                                    round (default 6: the slowest of the line)"""
 import os
 import sys
 
@@ -19,11 +21,29 @@ NAMES = {14: "setup", 0: "residual: Q X, C'lam", 1: "residual: 2 adjoints", 2: "
          3: "W_k build", 4: "K: Gamma rec + MFMA", 5: "K: diag adds", 6: "chol: 16x16 factors",
          7: "chol: panel + SYRK", 8: "solve: rho, C'rho", 9: "solve: adjoint", 10: "solve: tri-solves",
          11: "solve: fwd sim", 12: "solve: rows, step", 13: "update"}
-n = int(sys.argv[1]) if len(sys.argv) > 1 else 1024
-N = int(sys.argv[2]) if len(sys.argv) > 2 else 30
-sc = S.make_di(n, N, 2, 2)
-R = DIRounds(sc)
-R.build()
+LPV = len(sys.argv) > 1 and sys.argv[1] == "--lpv"
+if LPV:
+    import bench
+    from cmpc.rounds import LPVRounds
+
+    bp, args, kw = bench.lpv_population(None, rescue=False)
+    R = LPVRounds(bp, *args, **kw)
+    for _ in range(int(sys.argv[2]) if len(sys.argv) > 2 else 6):
+        R.step(halt=False)
+    R.gather()
+    n, N = R.B, R.N
+
+    class _Opt:   # R.opts -> the planner's options (the LPV solve reads bp.opts)
+        def __set__(self, obj, v):
+            bp.opts = v
+
+    type(R).opts = _Opt()
+else:
+    n = int(sys.argv[1]) if len(sys.argv) > 1 else 1024
+    N = int(sys.argv[2]) if len(sys.argv) > 2 else 30
+    sc = S.make_di(n, N, 2, 2)
+    R = DIRounds(sc)
+    R.build()
 st = torch.zeros((n, SLOTS), dtype=torch.int64, device="cuda")
 R.opts = L.opts(stamps=st.data_ptr())
 for _ in range(3):
