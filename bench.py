@@ -181,7 +181,7 @@ def main():
         dist.destroy_process_group()
 
 
-def reference_config(ctx, reps=10):
+def reference_config(ctx, reps=10, cpu=True):
     """The reference's own shipped configuration, timed beside its recorded number: N = 125,
     3 agents on the Highway map (planner/scripts/config_files/config_LPV.py:13-24), through the
     PlannerLPV drop-in (host arrays in and out, LPV scheduling + planes + QP build + the
@@ -215,15 +215,57 @@ def reference_config(ctx, reps=10):
         for _ in range(reps):
             res = bp.solve(*args)
         ms = (time.perf_counter() - t0) / reps * 1e3
-        steps.append({"step": int(step), "agents": len(sel), "ms_per_step": ms,
-                      "ipm_iters": res["iters"].tolist(), "status": res["status"].tolist(),
-                      "max_abs_err_vs_certified_optimum": float(np.abs(res["z"] - d["z"][sel]).max())})
+        row = {"step": int(step), "agents": len(sel), "ms_per_step": ms,
+               "ipm_iters": res["iters"].tolist(), "status": res["status"].tolist(),
+               "max_abs_err_vs_certified_optimum": float(np.abs(res["z"] - d["z"][sel]).max())}
+        if cpu:
+            row["cpu"] = reference_config_cpu(bp, args, res, d["z"][sel])
+        steps.append(row)
     ref_ms = 111.9
     worst = max(s_["ms_per_step"] for s_ in steps)
-    return {"workload": "reference config_LPV.py: N=125, 3 agents, Highway, nx=9 nu=2 nb=2, fp64 (PlannerLPV drop-in, "
-                        "host arrays)", "steps": steps,
-            "reference_ms_per_agent_solve": ref_ms, "reference_ms_per_step_3_agents_sequential": 3 * ref_ms,
-            "speedup_vs_reference_step": 3 * ref_ms / worst, "reps": reps}
+    out = {"workload": "reference config_LPV.py: N=125, 3 agents, Highway, nx=9 nu=2 nb=2, fp64 (PlannerLPV drop-in, "
+                       "host arrays)", "steps": steps,
+           "reference_ms_per_agent_solve": ref_ms, "reference_ms_per_step_3_agents_sequential": 3 * ref_ms,
+           "speedup_vs_reference_step": 3 * ref_ms / worst, "reps": reps}
+    if cpu:
+        model_name, nproc, usable = host_cpu()
+        out["cpu_baseline"] = {
+            "kind": "port", "cores": 1, "cpu_model": model_name, "nproc": nproc,
+            "ms_per_step_sequential": [sum(s_["cpu"]["ms_per_agent"]) for s_ in steps],
+            "sample": "the same six N=125 agent-QPs (GPU builder's problems read back), solved one after another on "
+                      "one core by oracle/cmpc_oracle.c with the stage-wise Riccati method in the kernel's "
+                      "double-double mode (newton 3, the method the GPU runs at this horizon), best of 3"}
+    return out
+
+
+def reference_config_cpu(bp, args, res, z_cert):
+    """One control step of the reference configuration on the host: the structured problems the GPU
+    builder made (read back), each agent solved by the C restatement of the same stage-wise Riccati
+    method (oracle/cmpc_oracle.c, newton 3) on one thread, as the reference solves its agents one
+    after another; per-agent wall time (best of 3) and z against the certified optimum and the GPU."""
+    from oracle import cmpc_oracle as CO
+
+    x0, x_last, u_last, u_old, x_agents, pose = args
+    b = bp.build(x_last, u_last, x_agents, pose)
+    prm, nb = bp.prm, x_agents.shape[2]
+    ms, errs, errg, st = [], [], [], []
+    for a in range(x0.shape[0]):
+        P = dict(nx=9, nu=2, N=bp.N, ns=3, mc=4 + nb, Q=np.array(prm.Q[:]).reshape(9, 9),
+                 R=np.array(prm.R[:]).reshape(2, 2), dR=np.array(prm.dR[:]).reshape(2, 2), Qs=np.array(prm.Qs[:]),
+                 u_ub=np.array([prm.max_rs, prm.max_ac]), u_lb=np.array([-prm.max_ls, -prm.max_dc]),
+                 row_slack=np.array([-1, 0, 1, 1] + [2] * nb), row_sign=np.array([1, 1, 1, 1] + [-1] * nb),
+                 **{k: b[k][a:a + 1] for k in ("A", "B", "qlin", "C", "h")}, x0=x0[a:a + 1], u_prev=u_old[a:a + 1])
+        best = np.inf
+        for _ in range(3):
+            t0 = time.perf_counter()
+            zc, _, _, sc = CO.solve_batch(P, nthreads=1, newton=3)
+            best = min(best, time.perf_counter() - t0)
+        ms.append(best * 1e3)
+        st.append(int(sc[0]))
+        errs.append(float(np.abs(zc[0] - z_cert[a]).max()))
+        errg.append(float(np.abs(zc[0] - res["z"][a]).max()))
+    return {"ms_per_agent": ms, "status": st, "max_abs_err_vs_certified_optimum": max(errs),
+            "max_abs_err_vs_gpu": max(errg)}
 
 
 def lpv_population(ctx, replicas=341, rescue=True):

@@ -25,6 +25,7 @@ struct MpcConst {
     int wg;       // 0: one-wave kernels; 2: workgroup kernel in fp32 (CMPC_FLAG_FP32)
     int riccati;  // 1: stage-wise Riccati kernel (fp64, N*nu > 64 or CMPC_FLAG_RICCATI)
     int rescue;   // 1: CMPC_FLAG_RESCUE on a condensed solve (Riccati re-solve of broken-down agents)
+    unsigned long long ws_stride;  // doubles of MpcPtrs::ws per agent (set by mpc_launch; 0: no scratch)
     double tol;
     double qs_max;  // max(1, 2*max(Qs)) — slack residual scale
     double Q[CMPC_MAX_NX * CMPC_MAX_NX];
@@ -106,6 +107,25 @@ __host__ __device__ inline int stop_status(int stop, double best_m, double tol) 
 size_t mpc_wg_lds_bytes(const MpcConst& c, bool fp32);
 hipError_t mpc_wg_launch(const MpcConst& c, const MpcPtrs& p, int batch, hipStream_t s, bool fp32);
 constexpr size_t kMaxLdsBytes = 160 * 1024;
+
+// Rescue hand-over (CMPC_FLAG_RESCUE).  A condensed kernel whose factorisation breaks down leaves
+// its iterate at the start of the agent's scratch (MpcPtrs::ws + b * ws_stride):
+//   [flag, iterations done, U (n), sig (N ns), t (m), lam (m)]   (rows in the oracle's order)
+// and the Riccati rescue launch continues the same interior-point solve from it (double-double
+// Newton solves near the solution) instead of starting cold; flag 0: no hand-over (cold start).
+// oracle/cmpc_oracle.c restates it (newton 4).
+__host__ __device__ inline size_t hand_doubles(const MpcConst& c) {
+    return 2 + (size_t)c.n + (size_t)c.N * c.ns + 2 * (size_t)c.m;
+}
+__host__ __device__ inline size_t hand_t(const MpcConst& c) { return 2 + (size_t)c.n + (size_t)c.N * c.ns; }
+// A continued (handed-over) solve without a new best iterate for kWarmStall iterations ends there
+// (best iterate; CMPC_UNSOLVED above the rounding floor, which the cold second pass re-solves).
+// Over 22 closed-loop rounds of bench.py's lpv_rounds population (tools/lpv_lab.py, the C
+// restatement): no unsolved or max-iteration agent, 279 of 22 506 at the rounding floor (714 with
+// the cold rescue alone); without it two continued solves ran to max_iter.  Every continued
+// iteration runs in double-double: 3 (the kStallIters of the condensed solve) and 8 gave the same
+// statuses in the lab, so the short one is kept.
+constexpr int kWarmStall = 3;
 
 // Stage-wise Riccati kernel (mpc_riccati.hip): any horizon whose per-agent rows fit LDS.
 size_t mpc_riccati_lds_bytes(const MpcConst& c);

@@ -483,6 +483,17 @@ __global__ __launch_bounds__(kWave) void mpc_ipm_kernel(const MpcConst c, const 
         }
         if (!chol_ok) {
             stop = kStopBreakdown;
+            if (c.rescue && P.ws) {  // hand the iterate to the Riccati rescue (hand_doubles)
+                double* hd = P.ws + (size_t)b * c.ws_stride;
+                const size_t ht = hand_t(c);
+                if (l == 0) hd[1] = it - 1;
+                for (int i = l; i < n; i += kWave) hd[2 + i] = U[i];
+                for (int i = l; i < N * ns; i += kWave) hd[2 + n + i] = sig[i];
+                for (int r = l; r < m; r += kWave) {
+                    hd[ht + r] = t[r];
+                    hd[ht + m + r] = lam[r];
+                }
+            }
             break;
         }
 
@@ -649,6 +660,8 @@ __global__ __launch_bounds__(kWave) void mpc_ipm_kernel(const MpcConst c, const 
         if (P.kkt) P.kkt[b] = kkt;
         if (P.iters) P.iters[b] = it;
         if (P.status) P.status[b] = status;
+        // rescue hand-over flag: set only by a breakdown (the iterate was written there)
+        if (c.rescue && P.ws) P.ws[(size_t)b * c.ws_stride] = stop == kStopBreakdown ? 1.0 : 0.0;
     }
 }
 
@@ -739,8 +752,10 @@ static hipError_t launch_t(const MpcConst& c, const MpcPtrs& p, int batch, hipSt
     return hipGetLastError();
 }
 
-hipError_t mpc_launch(const MpcConst& c, const MpcPtrs& p, int batch, hipStream_t s, int flags) {
+hipError_t mpc_launch(const MpcConst& c_in, const MpcPtrs& p, int batch, hipStream_t s, int flags) {
     if (batch == 0) return hipSuccess;
+    MpcConst c = c_in;
+    c.ws_stride = p.ws ? mpc_ws_doubles(c) : 0;
     if (c.wg) return mpc_wg_launch(c, p, batch, s, c.wg == 2);
     if (c.riccati) return mpc_riccati_launch(c, p, batch, s);
     hipError_t e;
@@ -754,9 +769,12 @@ hipError_t mpc_launch(const MpcConst& c, const MpcPtrs& p, int batch, hipStream_
     }
     if (e != hipSuccess || !c.rescue || !p.status || !p.ws) return e;
     // rescue pass: the Riccati kernel re-solves, on the same problems, exactly the agents the
-    // condensed solve left CMPC_UNSOLVED (its other workgroups return at once)
+    // condensed solve left CMPC_UNSOLVED (its other workgroups return at once) — continuing from
+    // the iterate a breakdown handed over (hand_doubles); a second pass restarts cold the rare
+    // agent the continued solve leaves CMPC_UNSOLVED (the hand-over flag is consumed by then)
     MpcConst cr = c;
     cr.riccati = 1;
+    if ((e = mpc_riccati_launch(cr, p, batch, s)) != hipSuccess) return e;
     return mpc_riccati_launch(cr, p, batch, s);
 }
 

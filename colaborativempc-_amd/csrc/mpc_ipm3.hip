@@ -770,6 +770,29 @@ __global__ __launch_bounds__(64, 1) void mpc_ipm3_kernel(const MpcConst c, const
         }
         if (!chol_ok) {
             stop = kStopBreakdown;
+            if (c.rescue && P.ws) {  // hand the iterate to the Riccati rescue (hand_doubles, internal.h)
+                double* hd = P.ws + (size_t)b * c.ws_stride;
+                const int m = c.m, ht = (int)hand_t(c);
+                if (l == 0) hd[1] = it - 1;
+                for (int i = l; i < n; i += 64) hd[2 + i] = U[i];
+                if (own) {
+                    if (lo) {
+#pragma unroll
+                        for (int j = 0; j < NS; ++j) hd[2 + n + k * NS + j] = sg[j];
+#pragma unroll
+                        for (int r = 0; r < MC; ++r) {
+                            hd[ht + k * MC + r] = t[r];
+                            hd[ht + m + k * MC + r] = lam[r];
+                        }
+                    } else {
+#pragma unroll
+                        for (int r = 0; r < NI; ++r) {  // input rows of u_k: ms + (k nu + i) 2 + (lb ? 1 : 0)
+                            hd[ht + ms + k * NI + r] = t[r];
+                            hd[ht + m + ms + k * NI + r] = lam[r];
+                        }
+                    }
+                }
+            }
             break;
         }
         // diagonal blocks L_JJ -> L_JJ^{-1} in place (LDS, lower triangle; zeros above): row q of the
@@ -1039,6 +1062,8 @@ __global__ __launch_bounds__(64, 1) void mpc_ipm3_kernel(const MpcConst c, const
         if (P.kkt) P.kkt[b] = kkt;
         if (P.iters) P.iters[b] = it;
         if (P.status) P.status[b] = status;
+        // rescue hand-over flag: set only by a breakdown (the iterate was written there)
+        if (c.rescue && P.ws) P.ws[(size_t)b * c.ws_stride] = stop == kStopBreakdown ? 1.0 : 0.0;
         if (stamp) {
             unsigned long long* st = P.stamps + (size_t)b * kStampSlots;
             for (int i = 0; i < kStampSlots - 1; ++i) st[i] = tsum[i];

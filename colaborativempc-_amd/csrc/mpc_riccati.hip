@@ -192,7 +192,7 @@ __host__ __device__ inline RLds r_layout(const MpcConst& c) { return r_layout_ex
 // per-agent global scratch (doubles): predictor direction (dt, dl), Riccati factors, stage
 // weights W_k = 2Q + M_k of the state X_{k+1}, best iterate
 struct RGlb {
-    size_t dta, dla, F, Wk, bU, bsig, t, lam, w, rp, rho, GdU, total;
+    size_t hand, dta, dla, F, Wk, bU, bsig, t, lam, w, rp, rho, GdU, total;
 };
 
 __host__ __device__ inline RGlb r_glb(const MpcConst& c) {
@@ -204,6 +204,7 @@ __host__ __device__ inline RGlb r_glb(const MpcConst& c) {
         o += (cnt + 31) & ~size_t(31);  // 256-byte aligned regions
         return r;
     };
+    g.hand = take(hand_doubles(c));  // first: the condensed kernels address it at ws + b * ws_stride
     g.dta = take(c.m);
     g.dla = take(c.m);
     g.F = take((size_t)c.N * d.sF);
@@ -983,7 +984,10 @@ template <class G>
 __global__ __launch_bounds__(kWave) void mpc_riccati_kernel(const MpcConst c_arg, const MpcPtrs P) {
     extern __shared__ __attribute__((aligned(16))) double sm[];
     const int b = blockIdx.x;
-    if (c_arg.rescue && P.status[b] != CMPC_UNSOLVED) return;  // rescue pass: broken-down agents only
+    if (c_arg.rescue) {  // rescue pass: agents handed over at a breakdown, or left CMPC_UNSOLVED, only
+        const RGlb g0 = r_glb(c_arg);
+        if (P.ws[(size_t)b * g0.total + g0.hand] == 0.0 && P.status[b] != CMPC_UNSOLVED) return;
+    }
     const int l = threadIdx.x;
     const RLds L = r_layout(c_arg);
     // the weights are indexed by lane-dependent expressions: read them from an LDS copy (a
@@ -1045,6 +1049,17 @@ __global__ __launch_bounds__(kWave) void mpc_riccati_kernel(const MpcConst c_arg
 
     for (int i = l; i < L.cst; i += kWave) sm[i] = 0.0;
     wsync();
+    // rescue pass: continue from the iterate a condensed kernel handed over at its breakdown
+    // (hand_doubles, internal.h), or start cold; the flag is consumed here, so a second rescue
+    // pass over an agent this one leaves CMPC_UNSOLVED starts cold
+    double* hand = ws + gl.hand;
+    const bool warm = c_arg.rescue && hand[0] != 0.0;
+    const int it0 = warm ? (int)hand[1] : 0;
+    if (warm) {
+        for (int i = l; i < n; i += kWave) U[i] = hand[2 + i];
+        for (int i = l; i < N * ns; i += kWave) sig[i] = hand[2 + n + i];
+        wsync();
+    }
     // diagnostic per-section clock sums (MpcPtrs::stamps; tools/ric_stamps.py):
     // 0 residuals, 1 stage weights, 2 factor, 3 factor (dd), 4 rhs, 5 solve, 6 refinement,
     // 7 rows / slacks / step, 8 update, 12 dd iterations, 13 refinement steps, 14 setup + output
@@ -1075,11 +1090,17 @@ __global__ __launch_bounds__(kWave) void mpc_riccati_kernel(const MpcConst c_arg
     fwd_sim<G>(c, d, sAB, sb, x0, U, X);
 
     double mact_l = 0.0, sp_l = 1.0;
+    const size_t ht = hand_t(c);
     for (int r = l; r < m; r += kWave) {
         if (isfinite(w[r])) {
-            const double g = row_value<G>(c, C, r, X, U, sig);
-            t[r] = fmax(w[r] - g, kT0Floor);
-            lam[r] = 1.0;
+            if (warm) {
+                t[r] = hand[ht + r];
+                lam[r] = hand[ht + m + r];
+            } else {
+                const double g = row_value<G>(c, C, r, X, U, sig);
+                t[r] = fmax(w[r] - g, kT0Floor);
+                lam[r] = 1.0;
+            }
             mact_l += 1.0;
             sp_l = fmax(sp_l, fabs(w[r]));
         } else {
@@ -1090,13 +1111,14 @@ __global__ __launch_bounds__(kWave) void mpc_riccati_kernel(const MpcConst c_arg
     const double mact = fmax(wave_sum(mact_l), 1.0);
     const double scale_p = wave_max(sp_l);
     rsync();  // lam: read across lanes by the residuals
+    if (warm && l == 0) hand[0] = 0.0;  // (every lane has read the flag: `warm` steered the loop above)
 
     double best_m = INFINITY, best_kkt = INFINITY;
     int best_it = 0, stop = kStopMaxIter, it;
     double kkt = INFINITY;
     RSTAMP(14);
     double alpha_prev = 1;  // step of the previous iteration (kShortStep guard)
-    for (it = 1; it <= c.max_iter; ++it) {
+    for (it = it0 + 1; it <= c.max_iter; ++it) {
         // ================= residuals (as mpc_ipm.hip) =================
         for (int i = l; i < (N + 1) * nx; i += kWave) {
             const int k = i / nx, s = i - k * nx;
@@ -1164,6 +1186,10 @@ __global__ __launch_bounds__(kWave) void mpc_riccati_kernel(const MpcConst c_arg
             break;
         }
         if (best_m < 1e3 * c.tol && it - best_it >= kStallIters) {
+            stop = kStopStalled;
+            break;
+        }
+        if (warm && it - best_it >= kWarmStall) {  // continued solve without progress (internal.h)
             stop = kStopStalled;
             break;
         }

@@ -17,7 +17,7 @@
  * (oracle/qp_ipm.py) on QPs captured from the reference (tests/golden).
  */
 #include <math.h>
-#if defined(ORACLE_TRACE) || defined(RIC_DEBUG) || defined(LAB_THDUMP) || defined(DIRCHECK)
+#if defined(ORACLE_TRACE) || defined(RIC_DEBUG) || defined(LAB_THDUMP) || defined(DIRCHECK) || defined(LAB_STOPDUMP)
 #include <stdio.h>
 #endif
 #include <stdlib.h>
@@ -104,6 +104,9 @@ long cmpc_gz_solves = 0; /* lab: corrector solves performed */
 #define REF_TOL 1e-13 /* refinement stops once |correction| <= REF_TOL |dU| (kernel: kRefineTol) */
 #endif
 
+#ifndef WARM_STALL
+#define WARM_STALL 3 /* kWarmStall (internal.h) */
+#endif
 #ifndef LR_MAX
 #define LR_MAX 4
 #endif
@@ -917,6 +920,22 @@ typedef struct {
 /* Solve one agent.  Returns OSQP-style status: 1 solved, 2 solved inaccurate, -2 max_iter, -10 unsolved. */
 static int solve_one(const shared_t* S, const agent_t* a, double tol, int max_iter, work_t* wk,
                      double* z, double* kkt_out, int* iters_out) {
+    /* newton 4: the product's CMPC_FLAG_RESCUE policy — the condensed method; at a factorisation
+       breakdown the solve continues from that iterate with the Riccati double-double Newton solve
+       (newton 3), its best-iterate bookkeeping restarted (the kernels hand the iterate from
+       mpc_ipm3 / mpc_ipm to mpc_riccati through the rescue scratch) */
+    shared_t S_cond, S_ric;
+    const int warm_rescue = S->newton == 4;
+#ifdef LAB_STOPDUMP
+    int it_switch = 0;
+#endif
+    if (warm_rescue) {
+        S_cond = *S;
+        S_cond.newton = 0;
+        S_ric = *S;
+        S_ric.newton = 3;
+        S = &S_cond;
+    }
     const int nx = S->nx, nu = S->nu, N = S->N, ns = S->ns, mc = S->mc;
     const int n = N * nu, ms = N * mc, m = ms + 2 * nu * N;
     double* Gam = wk->Gam; /* (N+1) x nx x n */
@@ -1113,7 +1132,16 @@ static int solve_one(const shared_t* S, const agent_t* a, double tol, int max_it
 #endif
         if (merit < tol) { stop = 1; break; }
         /* near-converged but no progress for STALL_ITERS iterations: rounding floor reached */
-        if (best_m < 1e3 * tol && it - best_it >= STALL_ITERS) { stop = 3; break; }
+        if (best_m < 1e3 * tol && it - best_it >= STALL_ITERS) {
+            stop = 3;
+            break;
+        }
+        /* continued (rescue) solve: no new best iterate for WARM_STALL iterations ends it
+           (kWarmStall of the kernels) */
+        if (warm_rescue && S->newton && it - best_it >= WARM_STALL) {
+            stop = 3;
+            break;
+        }
 
         /* ---- Newton matrix ---- */
         int hp = 0; /* Riccati: this iteration factors in double-double (newton == 3) */
@@ -1237,6 +1265,19 @@ static int solve_one(const shared_t* S, const agent_t* a, double tol, int max_it
                             r < ms ? r % mc : (r - ms) % (2 * nu), wk->th[r]);
             fprintf(stderr, "\n");
 #endif
+            if (warm_rescue && !S->newton) {
+#ifdef LAB_STOPDUMP
+                it_switch = it;
+#endif
+                /* hand over: redo this iteration (its residuals are those of the same iterate) with
+                   the Riccati solve; the best iterate is tracked afresh, as the rescue kernel does */
+                S = &S_ric;
+                best_m = INFINITY;
+                best_kkt = INFINITY;
+                best_it = 0;
+                --it;
+                continue;
+            }
             stop = 2;
             break;
         }
@@ -1571,6 +1612,9 @@ static int solve_one(const shared_t* S, const agent_t* a, double tol, int max_it
     free(gz_save);
 #endif
     if (it > max_iter) it = max_iter;
+#ifdef LAB_STOPDUMP
+    if (it_switch) fprintf(stderr, "WARM switch %d after %d stop %d best_m %.2e\n", it_switch, it - it_switch, stop, best_m);
+#endif
     int status;
     if (stop == 1) {
         status = 1;
@@ -1581,6 +1625,10 @@ static int solve_one(const shared_t* S, const agent_t* a, double tol, int max_it
             kkt = best_kkt;
         }
         status = best_m < 1e3 * tol ? 2 : (stop == 0 ? -2 : -10);
+#ifdef LAB_STOPDUMP
+        fprintf(stderr, "STOP status %d stop %d newton %d it %d best_it %d best_m %.2e\n", status, stop, S->newton, it,
+                best_it, best_m);
+#endif
     }
     /* exact re-simulation for the output trajectory */
     fwd_sim(S, a, a->x0, U, X);
@@ -1626,7 +1674,8 @@ int cmpc_oracle_solve_ex(int nx, int nu, int N, int ns, int mc, int batch,
 #ifdef RIC_DEBUG
         const size_t nG = (size_t)(N + 1) * nx * n, nK = (size_t)n * n;
 #else
-        const size_t nG = newton ? 0 : (size_t)(N + 1) * nx * n, nK = newton ? 0 : (size_t)n * n;
+        const int cond = newton == 0 || newton == 4; /* the condensed Newton matrix is formed */
+        const size_t nG = cond ? (size_t)(N + 1) * nx * n : 0, nK = cond ? (size_t)n * n : 0;
 #endif
         size_t need = nF + (size_t)n + (size_t)N * ns + nG + nK + 4 * (size_t)(N + 1) * nx + 4 * (size_t)n +
                       4 * (size_t)N * ns + 12 * (size_t)m + 2 * (size_t)nx + (size_t)nx * nx + (size_t)n * 3 + (size_t)nx * n + 2 * (size_t)n + (size_t)(N + 1) * nx;

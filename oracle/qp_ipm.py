@@ -55,6 +55,32 @@ def kkt_certificate(P, q, A, l, u, x, y):
                 dual_sign=float(dfeas.max(initial=0)))
 
 
+def kkt_of_primal(P, q, A, l, u, x, act_tol=1e-7):
+    """Reference-form KKT certificate of a primal point alone (for solvers that return no
+    multipliers): the multipliers y minimising the stationarity residual ||Px + q + A'y|| subject to
+    OSQP's sign convention (y free on equality rows, y >= 0 on rows with only an upper bound,
+    y <= 0 on rows with only a lower bound) and to complementarity (y = 0 on rows farther than
+    act_tol from their bound), by bounded least squares; returns (kkt_certificate(...), y)."""
+    from scipy.optimize import lsq_linear
+
+    P, A = np.asarray(P, float), np.asarray(A, float)
+    x, l, u = np.asarray(x, float), np.asarray(l, float), np.asarray(u, float)
+    Ax = A @ x
+    nz = np.abs(A).sum(1) > 0
+    eq = nz & np.isfinite(l) & np.isfinite(u) & (l == u)
+    up = nz & ~eq & np.isfinite(u) & (np.abs(u - Ax) <= act_tol * np.maximum(1.0, np.abs(u)))
+    lo = nz & ~eq & np.isfinite(l) & (np.abs(Ax - l) <= act_tol * np.maximum(1.0, np.abs(l)))
+    use = eq | up | lo
+    idx = np.flatnonzero(use)
+    lb = np.where(up[idx] & ~lo[idx], 0.0, -np.inf)
+    ub = np.where(lo[idx] & ~up[idx], 0.0, np.inf)
+    y = np.zeros(A.shape[0])
+    if len(idx):
+        r = lsq_linear(A[idx].T, -(P @ x + q), bounds=(lb, ub), method="bvls", tol=1e-14, lsmr_tol="auto")
+        y[idx] = r.x
+    return kkt_certificate(P, q, A, l, u, x, y), y
+
+
 def solve_qp(P, q, A, l, u, tol=1e-12, max_iter=200, verbose=False):
     P = np.asarray(P, float)
     A = np.asarray(A, float)

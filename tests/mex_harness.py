@@ -8,14 +8,16 @@ import numpy as np
 from cmpc import _lib as L
 
 MOCK = os.path.join(os.path.dirname(L.LIB_PATH), "libcmpc_mex_mock.so")
-_M = None
+LPV_MOCK = os.path.join(os.path.dirname(L.LIB_PATH), "libcmpc_lpv_mex_mock.so")
+_M = {}
 
 
-def lib():
-    global _M
-    if _M is None:
+def lib(path=MOCK):
+    """The mock-MEX build of a gateway: cmpc_quadprog (default) or cmpc_lpv (LPV_MOCK).  Arrays made
+    by either build's mock_* helpers are interchangeable (same mock mxArray)."""
+    if path not in _M:
         L.load()   # torch first, then libcmpc (one HIP runtime), then the gateway
-        m = ct.CDLL(MOCK)
+        m = ct.CDLL(path)
         m.mock_array.restype = ct.c_void_p
         m.mock_array.argtypes = [ct.c_int, ct.POINTER(ct.c_long), ct.POINTER(ct.c_double)]
         m.mock_sparse.restype = ct.c_void_p
@@ -37,8 +39,26 @@ def lib():
         m.mock_field.argtypes = [ct.c_void_p, ct.c_char_p]
         m.mock_string.restype = ct.c_char_p
         m.mock_string.argtypes = [ct.c_void_p]
-        _M = m
-    return _M
+        m.mxCreateString.restype = ct.c_void_p
+        m.mxCreateString.argtypes = [ct.c_char_p]
+        _M[path] = m
+    return _M[path]
+
+
+def mx_str(s):
+    """A MATLAB char array (command strings of cmpc_lpv)."""
+    return lib().mxCreateString(s.encode())
+
+
+def call_lpv(ps, nlhs):
+    """cmpc_lpv(...) on prepared mxArray pointers -> (outputs | None, (err_id, err_msg) | None)."""
+    m = lib(LPV_MOCK)
+    prhs = (ct.c_void_p * len(ps))(*ps)
+    plhs = (ct.c_void_p * nlhs)()
+    rc = m.mock_call(nlhs, plhs, len(ps), prhs)
+    if rc:
+        return None, (m.mock_err_id().decode(), m.mock_err_msg().decode())
+    return list(plhs), None
 
 
 def mx(a):

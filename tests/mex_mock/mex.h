@@ -1,6 +1,7 @@
 /* TEST INFRASTRUCTURE: a minimal stand-in for MATLAB's mex.h / matrix.h, enough to compile
- * and exercise colaborativempc-_amd/mex/cmpc_quadprog_mex.c without MATLAB (there is none
- * in this image).  Doubles only (full or sparse CSC), column-major, struct arrays of one element. */
+ * and exercise colaborativempc-_amd/mex/cmpc_quadprog_mex.c and cmpc_lpv_mex.c without MATLAB (there is none
+ * in this image).  Doubles only (full or sparse CSC), column-major, struct arrays of one element,
+ * char arrays (command strings). */
 #ifndef CMPC_MEX_MOCK_H
 #define CMPC_MEX_MOCK_H
 #include <stddef.h>
@@ -25,6 +26,8 @@ mwIndex* mxGetJc(const mxArray* a);
 int mxGetNumberOfFields(const mxArray* a);
 int mxIsEmpty(const mxArray* a);
 int mxIsStruct(const mxArray* a);
+int mxIsChar(const mxArray* a);
+int mxGetString(const mxArray* a, char* buf, size_t buflen);
 double mxGetScalar(const mxArray* a);
 mxArray* mxGetField(const mxArray* a, size_t i, const char* name);
 void mxSetField(mxArray* a, size_t i, const char* name, mxArray* v);

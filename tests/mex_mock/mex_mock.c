@@ -49,6 +49,13 @@ mwIndex* mxGetJc(const mxArray* a) { return a->jc; }
 int mxGetNumberOfFields(const mxArray* a) { return a->nfields; }
 int mxIsEmpty(const mxArray* a) { return mxGetNumberOfElements(a) == 0; }
 int mxIsStruct(const mxArray* a) { return a->cls == mxSTRUCT_CLASS; }
+int mxIsChar(const mxArray* a) { return a->cls == mxCHAR_CLASS; }
+/* MATLAB: 0 on success, 1 if not a char array or the buffer is too small */
+int mxGetString(const mxArray* a, char* buf, size_t buflen) {
+    if (a->cls != mxCHAR_CLASS || !a->str || strlen(a->str) + 1 > buflen) return 1;
+    strcpy(buf, a->str);
+    return 0;
+}
 double mxGetScalar(const mxArray* a) { return a->pr && mxGetNumberOfElements(a) ? a->pr[0] : 0.0; }
 mxArray* mxGetField(const mxArray* a, size_t i, const char* name) {
     (void)i;
