@@ -57,10 +57,18 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    # CMPC_DIST_BACKEND: "nccl" (RCCL over xGMI, one GPU per rank: the default) or "gloo" (ranks that
+    # share a device, exchange staged through the host: tests/test_dist_gpu.py rehearses the
+    # multi-rank bench path this way on a one-GPU box); CMPC_DEVICE overrides LOCAL_RANK's device
+    backend = os.environ.get("CMPC_DIST_BACKEND", "nccl")
+    local = int(os.environ.get("CMPC_DEVICE", local))
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
 
     import cmpc
     from cmpc import scenarios as S
@@ -100,8 +108,9 @@ def main():
     inacc = (hist_st == cmpc.CMPC_SOLVED_INACCURATE).sum()
     kern_ms = sum(a.elapsed_time(b) for a, b in ev) / args.steps
 
-    stats = torch.tensor([elapsed, kern_ms, kkt_max.item()], dtype=torch.float64, device=dev)
-    tot = torch.tensor([iters_sum.item(), float(bad.item()), float(inacc.item())], dtype=torch.float64, device=dev)
+    red_dev = dev if backend == "nccl" else torch.device("cpu")   # gloo reduces host tensors
+    stats = torch.tensor([elapsed, kern_ms, kkt_max.item()], dtype=torch.float64, device=red_dev)
+    tot = torch.tensor([iters_sum.item(), float(bad.item()), float(inacc.item())], dtype=torch.float64, device=red_dev)
     if world > 1:
         dist.all_reduce(stats, op=dist.ReduceOp.MAX)
         dist.all_reduce(tot, op=dist.ReduceOp.SUM)
@@ -150,7 +159,8 @@ def main():
                             (f"cfg3: {args.agents} agents/GPU, N={N}, 2-D double integrator nx={nx} nu={nu}, "
                              f"nb={args.nb}, fp64 condensed IPM; step = build+solve+advance+all-gather"),
                 "agents_total": n_total, "horizon": N, "nx": nx, "nu": nu, "neighbours": args.nb,
-                "parallelism": f"agents sharded over {world} GPU(s), RCCL all-gather per round",
+                "parallelism": f"agents sharded over {world} GPU(s), "
+                               f"{'RCCL' if backend == 'nccl' else backend} all-gather per round",
             },
             "max_kkt": kkt_all,
             "unsolved": int(bad_all),

@@ -56,13 +56,15 @@ def _flags(fp32=False, riccati=False, generic=False, rescue=False):
         (L.CMPC_FLAG_GENERIC if generic else 0) | (L.CMPC_FLAG_RESCUE if rescue else 0)
 
 
-def solve_mpc(p, ctx=None, tol=None, max_iter=None, fp32=False, riccati=False, generic=False, rescue=False):
+def solve_mpc(p, ctx=None, tol=None, max_iter=None, fp32=False, riccati=False, generic=False, rescue=False,
+              stamps=None):
     """Solve a batch of structured agent-QPs on the GPU (host arrays in/out).
     ``fp32``: the fp32 workgroup-per-agent solver (long horizons, BASELINE cfg5);
     ``riccati``: force the stage-wise Riccati solver (the default when N*nu > 64);
     ``generic``: force the runtime-dimension condensed kernel;
     ``rescue``: CMPC_FLAG_RESCUE (a condensed solve whose factorisation breaks down continues on
-    the stage-wise Riccati kernel; PlannerLPV's default).
+    the stage-wise Riccati kernel; PlannerLPV's default);
+    ``stamps``: optional device address of a batch x 16 uint64 buffer (per-section clock counts).
 
     Returns (z (B,nz), kkt (B,), iters (B,), status (B,))."""
     ctx = ctx or L.default_context()
@@ -76,7 +78,7 @@ def solve_mpc(p, ctx=None, tol=None, max_iter=None, fp32=False, riccati=False, g
     iters = np.zeros(batch, np.int32)
     status = np.zeros(batch, np.int32)
     out = L.cmpc_mpc_out(L.dptr(z), L.dptr(kkt), L.iptr(iters), L.iptr(status))
-    o = L.opts(tol or (FP32_TOL if fp32 else None), max_iter, _flags(fp32, riccati, generic, rescue))
+    o = L.opts(tol or (FP32_TOL if fp32 else None), max_iter, _flags(fp32, riccati, generic, rescue), stamps)
     ctx.check(ctx.lib.cmpc_solve_mpc_batch(ctx.h, ct.byref(_dims(p, batch)), ct.byref(w), ct.byref(data),
                                            ct.byref(out), ct.byref(o)))
     del keep, arrs

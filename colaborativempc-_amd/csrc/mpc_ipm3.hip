@@ -44,7 +44,7 @@ struct Lds3 {
 
 template <int T, int NX, int NU, int NB>
 __host__ __device__ inline Lds3 lds3_layout(int N) {
-    constexpr int NP = 16 * T, NXP = (NX + 3) & ~3, MC = 4 + NB;
+    constexpr int NP = 16 * T, MC = 4 + NB;
     Lds3 L;
     int o = 0;
     auto take = [&](int cnt) {
@@ -60,11 +60,13 @@ __host__ __device__ inline Lds3 lds3_layout(int N) {
     L.Pq = take((N + 1) * NX);
     L.x0 = take(NX);
     L.up = take(NU);
-    // W, Gb, Yb are contiguous: the Cholesky panel scratch aliases them after the K build
-    // (Gb / Yb are only that scratch's extent now: the K build transposes in registers)
+    // the Cholesky panel scratch ((T-1) x 16 x 17) aliases W after the K build; Gb extends W only
+    // where W is smaller than that (short horizons, small NX): at NX = 9 the extra 12 KB it used to
+    // take halved the agents per CU (90 KB -> 78 KB: two agents per CU instead of one)
     L.W = take(N * NX * NX);
-    L.Gb = take(NXP * NP);
-    L.Yb = take(NXP * NP);
+    const int sp_need = (T - 1) * 16 * 17 - N * NX * NX;
+    L.Gb = take(sp_need > 0 ? sp_need : 0);
+    L.Yb = L.Gb;
     L.X = take((N + 1) * NX);
     L.dX = take((N + 1) * NX);
     L.yb = take((N + 1) * NX);
@@ -243,7 +245,7 @@ __global__ __launch_bounds__(64, 1) void mpc_ipm3_kernel(const MpcConst c, const
     double* bU = sm + L.bU;
     double* Ld = sm + L.Ld;
     double* red = sm + L.red;
-    double* SP = sW;  // Cholesky panel scratch (aliases W | Gb | Yb after the K build)
+    double* SP = sW;  // Cholesky panel scratch (aliases W | Gb after the K build)
     const bool stamp = P.stamps != nullptr;
     // diagnostic per-section clock sums live in LDS (registers stay with the solver)
     unsigned long long* tsum = reinterpret_cast<unsigned long long*>(sm + L.stamps);

@@ -46,6 +46,10 @@ constexpr int kPerSmall = 2;                               // ... when the stage
 constexpr int kDepth = 3;  // stage images in flight: a sweep step waits for a load issued 2 steps earlier
 constexpr double kDdTh = 1e10;   // max th above which an iteration runs in double-double
 constexpr int kRefineMax = 6;    // refinement steps of a double-double iteration's direction
+// ... in a continued (rescue hand-over) solve: 2 — over the 22 lpv_lab rounds the continued
+// agents end with the same statuses as with 6 (278 vs 279 at the rounding floor; oracle
+// RIC_REFINE_WARM), and a step costs ~0.3 M clocks at N = 30
+constexpr int kRefineMaxWarm = 2;
 constexpr double kRefineTol = 1e-13;  // ... until |correction| <= kRefineTol |dU|: 1e-16 -> 1e-13 cut
                                       // the steps on the captured LPV QPs by 39% (752 -> 456) with the
                                       // same iterates to 1e-13 (tools/ipm_lab.py, oracle REF_TOL)
@@ -1275,7 +1279,8 @@ __global__ __launch_bounds__(kWave) void mpc_riccati_kernel(const MpcConst c_arg
                 riccati_solve<G>(c, d, L, sm, A, B, F, rh, dU, dX);
                 RSTAMP(5);
                 // refinement: dU += M^-1 (rhs - K dU), residual in double-double (gU, cr: free here)
-                for (int ir = 0; ir < kRefineMax; ++ir) {
+                const int nref = warm ? kRefineMaxWarm : kRefineMax;
+                for (int ir = 0; ir < nref; ++ir) {
                     kres_dd<G>(c, d, L, sm, A, B, Wg, dU, rh, gU);
                     riccati_solve<G>(c, d, L, sm, A, B, F, gU, cr, nullptr);
                     double cn_l = 0.0, un_l = 0.0;

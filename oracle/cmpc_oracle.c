@@ -31,6 +31,8 @@ typedef struct {
     const double *Q, *R, *dR, *Qs, *u_ub, *u_lb;
     const int *row_slack, *row_sign;
     int newton, refine; /* refine: iterative-refinement steps of the Riccati solve */
+    int refine_dd;      /* refinement steps of a double-double iteration (RIC_REFINE_MAX; continued
+                           rescue solves RIC_REFINE_WARM, the kernels' kRefineMaxWarm) */
     /* newton: 0 condensed Cholesky; 1 Riccati (P = Qyy + A'PA + Hvy'K); 2 Riccati, Joseph form */
 } shared_t;
 
@@ -741,7 +743,12 @@ static inline dd_t dd_sqrt(dd_t x) {
 #ifndef RIC_DD_TH
 #define RIC_DD_TH 1e10
 #endif
+#ifndef RIC_REFINE_MAX
 #define RIC_REFINE_MAX 6
+#endif
+#ifndef RIC_REFINE_WARM
+#define RIC_REFINE_WARM 2
+#endif
 
 /* ric_factor in double-double (standard form); gains rounded to double */
 static int ric_factor_dd(const shared_t* S, const agent_t* a, const double* th, const double* Dsig, double* F) {
@@ -934,6 +941,7 @@ static int solve_one(const shared_t* S, const agent_t* a, double tol, int max_it
         S_cond.newton = 0;
         S_ric = *S;
         S_ric.newton = 3;
+        S_ric.refine_dd = RIC_REFINE_WARM;
         S = &S_cond;
     }
     const int nx = S->nx, nu = S->nu, N = S->N, ns = S->ns, mc = S->mc;
@@ -1362,7 +1370,7 @@ static int solve_one(const shared_t* S, const agent_t* a, double tol, int max_it
             if (S->newton) {
                 ric_solve(S, a, wk->F, wk->rhs, wk->dU, wk->dX);
                 /* iterative refinement: dU += M^-1 (rhs - K dU) */
-                const int nref = hp ? RIC_REFINE_MAX : S->refine;
+                const int nref = hp ? S->refine_dd : S->refine;
                 for (int ir = 0; ir < nref; ++ir) {
 #ifdef REF_COUNT
                     if (hp) fprintf(stderr, "REF\n");
@@ -1657,7 +1665,7 @@ int cmpc_oracle_solve_ex(int nx, int nu, int N, int ns, int mc, int batch,
                          const double* qlin, const double* Crow, const double* hrow,
                          double tol, int max_iter, int nthreads, int newton, int refine, const double* U0,
                          double* z, double* kkt, int* iters, int* status) {
-    shared_t S = {nx, nu, N, ns, mc, Q, R, dR, Qs, u_ub, u_lb, row_slack, row_sign, newton, refine};
+    shared_t S = {nx, nu, N, ns, mc, Q, R, dR, Qs, u_ub, u_lb, row_slack, row_sign, newton, refine, RIC_REFINE_MAX};
     if (newton && (nx + nu > NA_MAX || nu > NU_MAX)) return -1;
     const int n = N * nu, m = N * mc + 2 * nu * N;
     const size_t nz = (size_t)(nx + ns) * (N + 1) + 2 * (size_t)nu * N;

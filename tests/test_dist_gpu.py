@@ -118,3 +118,24 @@ def test_c_abi_rccl_allgather_single_rank(gpu_ctx):
         comm.close()
     with pytest.raises(cmpc.CmpcError):   # left the communicator: the exchange refuses to run
         gpu_ctx.check(gpu_ctx.lib.cmpc_allgather_trajectories(gpu_ctx.h, None, None, 0, None))
+
+
+def test_bench_two_ranks_on_one_device_emit_one_line():
+    """bench.py's multi-rank path launched as the driver launches it (torch.distributed.run,
+    --nproc-per-node 2, RANK / WORLD_SIZE / LOCAL_RANK from the launcher) with both ranks on
+    device 0 and the exchange over gloo (CMPC_DIST_BACKEND / CMPC_DEVICE; RCCL refuses two ranks on
+    one device): rank 0 prints one JSON line whose value covers both ranks' agents."""
+    import json
+
+    env = dict(os.environ, CMPC_DIST_BACKEND="gloo", CMPC_DEVICE="0")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.join(ROOT, "bench.py"),
+           "--gpus", "2", "--steps", "5", "--warmup", "1", "--no-cpu", "--no-ref"]
+    p = subprocess.run(cmd, env=env, cwd=ROOT, capture_output=True, text=True, timeout=240)
+    assert p.returncode == 0, (p.stdout[-2000:], p.stderr[-3000:])
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, p.stdout[-2000:]
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 2 and out["config"]["agents_total"] == 2048 and out["steps"] == 5
+    assert out["value"] > 0 and out["unsolved"] == 0 and out["max_kkt"] < 1e-6
+    assert "gloo" in out["config"]["parallelism"]

@@ -49,6 +49,9 @@ def main():
         t0 = time.perf_counter()
         z, k, it, st = cmpc.solve_mpc(P, ctx, **kw2)
         out[name] = (z, k, it, st, (time.perf_counter() - t0) * 1e3)
+    st_buf = torch.zeros((R.B, 16), dtype=torch.int64, device="cuda")
+    cmpc.solve_mpc(P, ctx, rescue=True, stamps=st_buf.data_ptr())
+    stamps = st_buf.cpu().numpy().astype(np.float64)
     zc0, _, ic0, sc0 = CO.solve_batch(P, nthreads=16)
     zc, kc, ic, sc = CO.solve_batch_rescue(P, nthreads=16)
     st0 = out["plain"][3]
@@ -59,6 +62,15 @@ def main():
         zr, kr, ir, sr, _ = out["rescue"]
         print(f" {a:5d} | {out['plain'][2][a]:3d} {st0[a]:3d} | {ic0[a]:3d} {sc0[a]:3d} | {ir[a]:3d} {sr[a]:3d} {kr[a]:.1e} | "
               f"{ic[a]:3d} {sc[a]:3d} | {np.abs(zr[a] - zc[a]).max():.1e}")
+    # Riccati stamps of the continued agents (they overwrite the condensed kernel's): tools/ric_stamps.py slots
+    names = {0: "residuals", 1: "stage weights", 2: "factor", 3: "factor dd", 4: "rhs", 5: "solve", 6: "refinement",
+             7: "rows/step", 8: "update", 14: "setup+output"}
+    sel = idx[:8]
+    print("Riccati clocks (M) of the first continued agents: " + ", ".join(f"{a}" for a in sel))
+    for k_, nm in names.items():
+        print(f"  {nm:14s} " + " ".join(f"{stamps[a, k_] / 1e6:7.3f}" for a in sel))
+    print(f"  {'dd iterations':14s} " + " ".join(f"{stamps[a, 12]:7.0f}" for a in sel))
+    print(f"  {'refine steps':14s} " + " ".join(f"{stamps[a, 13]:7.0f}" for a in sel))
 
 
 if __name__ == "__main__":
