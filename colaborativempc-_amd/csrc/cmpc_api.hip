@@ -94,7 +94,15 @@ int lpv_solver_const(cmpc_ctx* ctx, const cmpc_lpv_params* prm, const cmpc_lpv_d
     cmpc_mpc_weights w{prm->Q, prm->R, prm->dR, Qsd, ub, lb, slack, sign};
     const char* msg = nullptr;
     int rc = cmpc::mpc_prepare(&md, &w, o, mc, &msg);
-    return rc == CMPC_OK ? rc : fail(ctx, rc, msg);
+    if (rc != CMPC_OK) return fail(ctx, rc, msg);
+    // the structure lpv_build.hip writes (A_k = I + dt A_c on columns 0..2, B_k rows 0..2, rows on
+    // vx / ey / (X, Y)) lets the v3 kernel keep compact images when Q is also diagonal
+    bool qdiag = true;
+    for (int i = 0; i < 9; ++i)
+        for (int j = 0; j < 9; ++j)
+            if (i != j && prm->Q[i * 9 + j] != 0.0) qdiag = false;
+    mc->lpv = (qdiag && !(o && (o->flags & CMPC_FLAG_GENERIC))) ? 1 : 0;
+    return CMPC_OK;
 }
 
 }  // namespace

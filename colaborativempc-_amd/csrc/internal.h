@@ -25,6 +25,7 @@ struct MpcConst {
     int wg;       // 0: one-wave kernels; 2: workgroup kernel in fp32 (CMPC_FLAG_FP32)
     int riccati;  // 1: stage-wise Riccati kernel (fp64, N*nu > 64 or CMPC_FLAG_RICCATI)
     int rescue;   // 1: CMPC_FLAG_RESCUE on a condensed solve (Riccati re-solve of broken-down agents)
+    int lpv;      // 1: data made by lpv_build.hip with Q diagonal (the v3 kernel's LS layout applies)
     unsigned long long ws_stride;  // doubles of MpcPtrs::ws per agent (set by mpc_launch; 0: no scratch)
     double tol;
     double qs_max;  // max(1, 2*max(Qs)) — slack residual scale

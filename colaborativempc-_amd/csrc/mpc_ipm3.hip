@@ -42,7 +42,19 @@ struct Lds3 {
     int cst, A, B, C, H, Pq, x0, up, W, Gb, Yb, X, dX, yb, U, dU, rd, gU, vb, thin, bU, Ld, red, stamps, total;
 };
 
-template <int T, int NX, int NU, int NB>
+// LS (the reference's own agent, nx 9 / nu 2, built by lpv_build.hip): the model's structure is
+// fixed by LPV_Planner.py:493-585 and :279-380, and the images shrink to it —
+//   A_k = I + D_k with D_k nonzero only in columns 0..2 (vx, vy, wz drive every state)   N x 9 x 3
+//   B_k nonzero only in rows 0..2                                                          N x 3 x 2
+//   rows: -vx, vx, ey, -ey, then a_x X + a_y Y per plane: their coefficients only          N x (4 + 2 nb)
+//   W_k = 2Q + the rows' weights (Q diagonal): diagonal except the (X, Y) block; the entries
+//   on vx, ey and the (X, Y) block per stage                                               N x 5
+// 39 KB of LDS at N = 30 instead of 78 KB: four agents per CU, so 1024 agents run at once.
+constexpr int kLsW = 5;  // LS stage weights: w(vx,vx), w(ey,ey), w(X,X), w(X,Y), w(Y,Y)
+template <int NB>
+__host__ __device__ constexpr int ls_cw() { return 4 + 2 * NB; }
+
+template <int T, int NX, int NU, int NB, bool LS = false>
 __host__ __device__ inline Lds3 lds3_layout(int N) {
     constexpr int NP = 16 * T, MC = 4 + NB;
     Lds3 L;
@@ -53,9 +65,9 @@ __host__ __device__ inline Lds3 lds3_layout(int N) {
         return r;
     };
     L.cst = take(NX * NX + 2 * NU * NU + 3 + 2 * NU);
-    L.A = take(N * NX * NX);
-    L.B = take(N * NX * NU);
-    L.C = take(N * MC * NX);
+    L.A = take(LS ? N * NX * 3 : N * NX * NX);
+    L.B = take(LS ? N * 3 * NU : N * NX * NU);
+    L.C = take(LS ? N * ls_cw<NB>() : N * MC * NX);
     L.H = take(N * MC);
     L.Pq = take((N + 1) * NX);
     L.x0 = take(NX);
@@ -63,8 +75,9 @@ __host__ __device__ inline Lds3 lds3_layout(int N) {
     // the Cholesky panel scratch ((T-1) x 16 x 17) aliases W after the K build; Gb extends W only
     // where W is smaller than that (short horizons, small NX): at NX = 9 the extra 12 KB it used to
     // take halved the agents per CU (90 KB -> 78 KB: two agents per CU instead of one)
-    L.W = take(N * NX * NX);
-    const int sp_need = (T - 1) * 16 * 17 - N * NX * NX;
+    const int wsz = LS ? N * kLsW : N * NX * NX;
+    L.W = take(wsz);
+    const int sp_need = (T - 1) * 16 * 17 - wsz;
     L.Gb = take(sp_need > 0 ? sp_need : 0);
     L.Yb = L.Gb;
     L.X = take((N + 1) * NX);
@@ -89,10 +102,11 @@ __host__ __device__ inline Lds3 lds3_layout(int N) {
 // row by DPP row_newbcast.  A stage's A row and B u term are fetched two stages ahead into
 // rotating register sets (unrolled by three: no copies, no branches; the fetch index is clamped
 // instead of guarded).  Every lane stores: duplicates write equal values.
-template <int NX, int NU>
+template <int NX, int NU, bool LS = false>
 __device__ __forceinline__ void fwd3(int l, int N, const double* A, const double* B, const double* x0,
                                      const double* U, double* X) {
     static_assert(NX <= 16, "row broadcast");
+    constexpr int NA = LS ? 3 : NX;  // columns of the stage image (LS: D_k, A_k = I + D_k)
     const int s = (l & 15) < NX ? (l & 15) : 0;
     double xr = x0 ? x0[s] : 0.0;
     X[s] = xr;
@@ -102,29 +116,37 @@ __device__ __forceinline__ void fwd3(int l, int N, const double* A, const double
     for (int i = l; i < N * NX; i += 64) {
         const int k = i / NX, r = i - k * NX;
         double v = 0.0;
+        if constexpr (LS) {
+            const int rr = r < 3 ? r : 0;
 #pragma unroll
-        for (int j = 0; j < NU; ++j) v = fma(B[(k * NX + r) * NU + j], U[k * NU + j], v);
+            for (int j = 0; j < NU; ++j) v = fma(B[(k * 3 + rr) * NU + j], U[k * NU + j], v);
+            v = r < 3 ? v : 0.0;
+        } else {
+#pragma unroll
+            for (int j = 0; j < NU; ++j) v = fma(B[(k * NX + r) * NU + j], U[k * NU + j], v);
+        }
         X[NX + i] = v;
     }
     wsync();
     auto fetch = [&](int k, double* av, double* bv) __attribute__((always_inline)) {
 #pragma unroll
-        for (int t = 0; t < NX; ++t) av[t] = A[(k * NX + s) * NX + t];
+        for (int t = 0; t < NA; ++t) av[t] = A[(k * NX + s) * NA + t];
         bv[0] = X[(k + 1) * NX + s];
     };
     auto step = [&](int k, const double* av, const double* bv) __attribute__((always_inline)) {
         double v0 = bv[0], v1 = 0.0;
-        static_for<0, NX>([&](auto t) __attribute__((always_inline)) {
+        static_for<0, NA>([&](auto t) __attribute__((always_inline)) {
             constexpr int tt = decltype(t)::value;
             if constexpr (tt & 1) v1 = fma(av[tt], bcast16<tt>(xr), v1);
             else v0 = fma(av[tt], bcast16<tt>(xr), v0);
         });
-        xr = v0 + v1;
+        if constexpr (LS) xr = (v0 + v1) + xr;  // x_{k+1} = x_k + D_k x_k + B_k u_k
+        else xr = v0 + v1;
         X[(k + 1) * NX + s] = xr;
     };
     // three register sets, fetched two stages ahead (unrolled by three: no copies; fetch indices
     // clamped, not guarded): a stage's LDS latency hides behind two stages of the chain
-    double a0[NX], a1[NX], a2[NX], b0[1], b1[1], b2[1];
+    double a0[NA], a1[NA], a2[NA], b0[1], b1[1], b2[1];
     fetch(0, a0, b0);
     fetch(1 < N ? 1 : N - 1, a1, b1);
     int k = 0;
@@ -149,7 +171,7 @@ __device__ __forceinline__ void fwd3(int l, int N, const double* A, const double
 // psi_k overwrites it).  The products o_k = B_k' psi_{k+1} are independent of one another and
 // are formed afterwards by the lanes that own u_k (bpsi3), off the recursion's chain.  The
 // operation order is the fused recursion's (even/odd partial sums), so the bits are unchanged.
-template <int NX>
+template <int NX, bool LS = false>
 __device__ __forceinline__ void psi3(int l, int N, const double* A, double* y0, double* y1) {
     static_assert(NX <= 16, "row broadcast");
     const int h = l >> 5, s = l & 15;
@@ -157,9 +179,13 @@ __device__ __forceinline__ void psi3(int l, int N, const double* A, double* y0, 
     double* y = h ? y1 : y0;
     double pr = y[N * NX + sx];
     if (N <= 1) return;
+    // LS: (A_k' psi)[s] = psi[s] + (s < 3 ? sum_t D_k[t][s] psi[t] : 0); lanes s >= 3 read column 0
+    // of D and discard it (branch-free)
+    const int sd = sx < 3 ? sx : 0;
+    const double dmask = sx < 3 ? 1.0 : 0.0;
     auto fetch = [&](int k, double* av, double& yv) __attribute__((always_inline)) {
 #pragma unroll
-        for (int t = 0; t < NX; ++t) av[t] = A[(k * NX + t) * NX + sx];
+        for (int t = 0; t < NX; ++t) av[t] = LS ? A[(k * NX + t) * 3 + sd] : A[(k * NX + t) * NX + sx];
         yv = y[k * NX + sx];
     };
     auto step = [&](int k, const double* av, double yk) __attribute__((always_inline)) {
@@ -168,13 +194,14 @@ __device__ __forceinline__ void psi3(int l, int N, const double* A, double* y0, 
             constexpr int tt = decltype(t)::value;
             ps[tt] = bcast16<tt>(pr);
         });
-        double p0 = yk, p1 = 0.0;
+        double p0 = LS ? 0.0 : yk, p1 = 0.0;
 #pragma unroll
         for (int t = 0; t < NX; ++t) {
             if (t & 1) p1 = fma(av[t], ps[t], p1);
             else p0 = fma(av[t], ps[t], p0);
         }
-        pr = p0 + p1;
+        if constexpr (LS) pr = fma(dmask, p0 + p1, yk + pr);
+        else pr = p0 + p1;
         y[k * NX + sx] = pr;
     };
     // three register sets fetched two stages ahead; fetch indices clamped to stage 1
@@ -198,12 +225,13 @@ __device__ __forceinline__ void psi3(int l, int N, const double* A, double* y0, 
 }
 
 // o = B_k[:, i]' psi_{k+1} (psi as left in place by psi3): even/odd partial sums, as before
-template <int NX, int NU>
+template <int NX, int NU, bool LS = false>
 __device__ __forceinline__ double bpsi3(const double* B, const double* psi, int k, int i) {
+    constexpr int NB_ = LS ? 3 : NX;  // LS: B_k is nonzero only in rows 0..2
     double v0 = 0.0, v1 = 0.0;
 #pragma unroll
-    for (int t = 0; t < NX; ++t) {
-        const double bt = B[(k * NX + t) * NU + i], pt = psi[(k + 1) * NX + t];
+    for (int t = 0; t < NB_; ++t) {
+        const double bt = B[(k * NB_ + t) * NU + i], pt = psi[(k + 1) * NX + t];
         if (t & 1) v1 = fma(bt, pt, v1);
         else v0 = fma(bt, pt, v0);
     }
@@ -212,14 +240,16 @@ __device__ __forceinline__ double bpsi3(const double* B, const double* psi, int 
 
 }  // namespace
 
-template <int T, int NX, int NU, int NB>
+template <int T, int NX, int NU, int NB, bool LS = false>
 __global__ __launch_bounds__(64, 1) void mpc_ipm3_kernel(const MpcConst c, const MpcPtrs P) {
     constexpr int MC = 4 + NB, NS = 3, NT = T * (T + 1) / 2, NP = 16 * T, NXP = (NX + 3) & ~3;
     constexpr int NI = 2 * NU, RX = MC > NI ? MC : NI;
+    constexpr int CW = ls_cw<NB>();  // LS: row coefficients per stage
+    static_assert(!LS || (NX == 9 && NU == 2), "LS: the reference's agent model");
     extern __shared__ __attribute__((aligned(16))) double sm[];
     const int l0 = threadIdx.x, b = blockIdx.x, N = c.N, n = N * NU, ms = N * MC;
     const int l = l0;
-    const Lds3 L = lds3_layout<T, NX, NU, NB>(N);
+    const Lds3 L = lds3_layout<T, NX, NU, NB, LS>(N);
     double* Q2 = sm + L.cst;          // 2Q
     double* R2 = Q2 + NX * NX;        // 2R
     double* dR2 = R2 + NU * NU;       // 2dR
@@ -264,9 +294,27 @@ __global__ __launch_bounds__(64, 1) void mpc_ipm3_kernel(const MpcConst c, const
         const double* gB = P.B + (size_t)b * N * NX * NU;
         const double* gC = P.C + (size_t)b * N * MC * NX;
         const double* gP = P.p + (size_t)b * (N + 1) * NX;
-        for (int i = l; i < N * NX * NX; i += 64) sA[i] = gA[i];
-        for (int i = l; i < N * NX * NU; i += 64) sB[i] = gB[i];
-        if (P.fuse.on) {
+        if constexpr (LS) {
+            // D_k = A_k - I on columns 0..2 (the builder's A_k = I + dt A_c, LPV_Planner.py:583); B_k rows
+            // 0..2; the rows' coefficients [vx of rows 0, 1 | ey of rows 2, 3 | (X, Y) of each plane]
+            for (int i = l; i < N * 27; i += 64) {
+                const int kk = i / 27, q = i - kk * 27, r = q / 3, t = q - r * 3;
+                sA[i] = gA[kk * 81 + r * 9 + t] - (r == t ? 1.0 : 0.0);
+            }
+            for (int i = l; i < N * 6; i += 64) sB[i] = gB[(i / 6) * 18 + (i % 6)];
+            for (int i = l; i < N * CW; i += 64) {
+                const int kk = i / CW, q = i - kk * CW;
+                const int r = q < 4 ? q : 4 + ((q - 4) >> 1), col = q < 2 ? 0 : (q < 4 ? 3 : 7 + ((q - 4) & 1));
+                sC[i] = gC[(kk * MC + r) * NX + col];
+            }
+        } else {
+            for (int i = l; i < N * NX * NX; i += 64) sA[i] = gA[i];
+            for (int i = l; i < N * NX * NU; i += 64) sB[i] = gB[i];
+        }
+        if (LS) {
+            for (int i = l; i < ms; i += 64) sH[i] = P.h[(size_t)b * ms + i];
+            for (int i = l; i < (N + 1) * NX; i += 64) sP[i] = gP[i];
+        } else if (P.fuse.on) {
             // fused round: this agent's rows and linear cost built from the exchanged
             // trajectories straight into LDS (bit-identical to di_build_kernel's)
             const DiFuse& F = P.fuse;
@@ -325,18 +373,25 @@ __global__ __launch_bounds__(64, 1) void mpc_ipm3_kernel(const MpcConst c, const
             if ((lo ? r < MC : r < NI) && isfinite(wv(r))) actm |= 1u << r;
     }
 #define ACT(r) ((actm >> (r)) & 1u)
-    fwd3<NX, NU>(l, N, sA, sB, sx0, U, X);
+    fwd3<NX, NU, LS>(l, N, sA, sB, sx0, U, X);
     wsync();
 
     // value of row r at (Xv, Uv[, sig]) for this lane's rows
     auto rowval = [&](int r, const double* Xv, const double* Uv, bool with_sig) -> double {
-        const double* cr = sC + (k * MC + r) * NX;
         const double* xk = Xv + (k + 1) * NX;
         double v = 0.0;
+        if constexpr (LS) {  // the rows' nonzeros only (the dense form adds exact zeros: same bits)
+            const double* cr = sC + k * CW;
+            if (r < 2) v = cr[r] * xk[0];
+            else if (r < 4) v = cr[r] * xk[3];
+            else v = fma(cr[4 + 2 * (r - 4) + 1], xk[8], cr[4 + 2 * (r - 4)] * xk[7]);
+        } else {
+            const double* cr = sC + (k * MC + r) * NX;
 #pragma unroll
-        for (int s = 0; s < NX; ++s) {
-            const double cs = cr[s], xs = xk[s];
-            v = fma(cs, xs, v);
+            for (int s = 0; s < NX; ++s) {
+                const double cs = cr[s], xs = xk[s];
+                v = fma(cs, xs, v);
+            }
         }
         if (with_sig && slk(r) >= 0) v += sgn(r) * sg[slk(r)];
         const double u = Uv[k * NU + (r >> 1)];
@@ -392,18 +447,33 @@ __global__ __launch_bounds__(64, 1) void mpc_ipm3_kernel(const MpcConst c, const
         wsync();
         // second adjoint input (in dX) = yb + C' lambda on stages 1..N
         if (lo && own) {
+            if constexpr (LS) {
+                const double* cr = sC + k * CW;
+                static_for<0, NX>([&](auto s_c) __attribute__((always_inline)) {
+                    constexpr int s2 = decltype(s_c)::value;
+                    double v = yb[(k + 1) * NX + s2];
+                    if constexpr (s2 == 0) v = fma(lam[1], cr[1], fma(lam[0], cr[0], v));
+                    if constexpr (s2 == 3) v = fma(lam[3], cr[3], fma(lam[2], cr[2], v));
+                    if constexpr (s2 == 7 || s2 == 8) {
 #pragma unroll
-            for (int s = 0; s < NX; ++s) {
-                double v = yb[(k + 1) * NX + s];
+                        for (int q = 0; q < NB; ++q) v = fma(lam[4 + q], cr[4 + 2 * q + (s2 - 7)], v);
+                    }
+                    dX[(k + 1) * NX + s2] = v;
+                });
+            } else {
 #pragma unroll
-                for (int r = 0; r < MC; ++r) v = fma(lam[r], sC[(k * MC + r) * NX + s], v);
-                dX[(k + 1) * NX + s] = v;
+                for (int s = 0; s < NX; ++s) {
+                    double v = yb[(k + 1) * NX + s];
+#pragma unroll
+                    for (int r = 0; r < MC; ++r) v = fma(lam[r], sC[(k * MC + r) * NX + s], v);
+                    dX[(k + 1) * NX + s] = v;
+                }
             }
         }
         if (l < NX) dX[l] = yb[l];
         wsync();
         STAMP(0);
-        psi3<NX>(l, N, sA, yb, dX);  // psi over yb (-> gradient) and over dX (-> rd)
+        psi3<NX, LS>(l, N, sA, yb, dX);  // psi over yb (-> gradient) and over dX (-> rd)
         wsync();
         STAMP(1);
         double gs_l = 1.0, nrd_l = 0.0, nrs_l = 0.0, nrp_l = 0.0, mu_l = 0.0;
@@ -430,8 +500,8 @@ __global__ __launch_bounds__(64, 1) void mpc_ipm3_kernel(const MpcConst c, const
                         const double dun = (k + 1 < N) ? U[(k + 1) * NU + j] - uk : 0.0;
                         v += R2[i * NU + j] * uk + dR2[i * NU + j] * (duk - dun);
                     }
-                    const double g = bpsi3<NX, NU>(sB, yb, k, i) + v;
-                    const double rdv = bpsi3<NX, NU>(sB, dX, k, i) + v + lam[2 * i] - lam[2 * i + 1];
+                    const double g = bpsi3<NX, NU, LS>(sB, yb, k, i) + v;
+                    const double rdv = bpsi3<NX, NU, LS>(sB, dX, k, i) + v + lam[2 * i] - lam[2 * i + 1];
                     rd[ci] = rdv;
                     gs_l = nmax(gs_l, fabs(g));
                     nrd_l = nmax(nrd_l, fabs(rdv));
@@ -497,6 +567,39 @@ __global__ __launch_bounds__(64, 1) void mpc_ipm3_kernel(const MpcConst c, const
                 double thp[MC];
 #pragma unroll
                 for (int r = 0; r < MC; ++r) thp[r] = slk(r) < 0 ? th[r] : Qs2[slk(r)] * th[r] / Dsig[slk(r)];
+                if constexpr (LS) {
+                    // block diagonal (Q diagonal, rows on vx / ey / (X, Y)): the five entries that are
+                    // not 2Q's, accumulated in the dense build's order
+                    const double* cr = sC + k * CW;
+                    double wvx = fma(thp[1] * cr[1], cr[1], fma(thp[0] * cr[0], cr[0], Q2[0]));
+                    double wey = fma(thp[3] * cr[3], cr[3], fma(thp[2] * cr[2], cr[2], Q2[3 * NX + 3]));
+                    const double phi23 = th[2] * th[3] / Dsig[1], d23 = cr[2] - cr[3];
+                    wey = fma(phi23 * d23, d23, wey);
+                    double wxx = Q2[7 * NX + 7], wxy = Q2[7 * NX + 8], wyy = Q2[8 * NX + 8];
+#pragma unroll
+                    for (int q = 0; q < NB; ++q) {
+                        const double ax = cr[4 + 2 * q], ay = cr[5 + 2 * q];
+                        wxx = fma(thp[4 + q] * ax, ax, wxx);
+                        wxy = fma(thp[4 + q] * ax, ay, wxy);
+                        wyy = fma(thp[4 + q] * ay, ay, wyy);
+                    }
+#pragma unroll
+                    for (int q = 0; q < NB; ++q)
+#pragma unroll
+                        for (int q2 = q + 1; q2 < NB; ++q2) {  // plane rows share slack 2, sign -1
+                            const double phi = th[4 + q] * th[4 + q2] / Dsig[2];
+                            const double dx = cr[4 + 2 * q2] - cr[4 + 2 * q], dy = cr[5 + 2 * q2] - cr[5 + 2 * q];
+                            wxx = fma(phi * dx, dx, wxx);
+                            wxy = fma(phi * dx, dy, wxy);
+                            wyy = fma(phi * dy, dy, wyy);
+                        }
+                    double* wk = sW + k * kLsW;
+                    wk[0] = wvx;
+                    wk[1] = wey;
+                    wk[2] = wxx;
+                    wk[3] = wxy;
+                    wk[4] = wyy;
+                } else {
                 // the stage's rows and 2Q into registers in one batch of LDS reads (read inside the
                 // loops below they were issued one dependent wait at a time)
                 // (small NX only: larger ones would not fit the VGPR file and read in place)
@@ -539,6 +642,7 @@ __global__ __launch_bounds__(64, 1) void mpc_ipm3_kernel(const MpcConst c, const
                         }
                         sW[(k * NX + s) * NX + u] = v;
                     }
+                }
             } else {
 #pragma unroll
                 for (int i = 0; i < NU; ++i) thin[k * NU + i] = th[2 * i] + th[2 * i + 1];
@@ -554,7 +658,76 @@ __global__ __launch_bounds__(64, 1) void mpc_ipm3_kernel(const MpcConst c, const
 #pragma unroll
             for (int q = 0; q < NT; ++q) acc[q] = __builtin_amdgcn_mfma_f64_16x16x4f64(0.0, 0.0, z4, 0, 0, 0);
         }
-        {
+        if constexpr (LS) {
+            // the same contraction on the reference model's structure: Gamma_{k+1} = Gamma_k +
+            // D_k Gamma_k[0..2] (+ B_k's column at its stage), and W_k Gamma_k from the block-diagonal
+            // W_k (2Q's diagonal, the vx / ey entries, the (X, Y) block): 27 + 11 multiply-adds per
+            // stage and lane instead of 81 + 81, 32 LDS reads instead of 162
+            double g[NX], q2d[NX], bcol[NX];
+            const int col = l;
+            const int kc = col / NU, ic = col - kc * NU, kcl = kc < N ? kc : N - 1;
+#pragma unroll
+            for (int s2 = 0; s2 < NX; ++s2) {
+                g[s2] = 0.0;
+                q2d[s2] = Q2[s2 * NX + s2];
+                const double bv = sB[(kcl * 3 + (s2 < 3 ? s2 : 0)) * NU + ic];
+                bcol[s2] = s2 < 3 ? bv : 0.0;
+            }
+            auto stage = [&](auto tau_c, int kk) __attribute__((always_inline)) {
+                constexpr int tau = decltype(tau_c)::value;
+                const double* Dk = sA + kk * 27;
+                const double* wk = sW + kk * kLsW;
+                double dv[27], w5[kLsW];
+#pragma unroll
+                for (int i = 0; i < 27; ++i) dv[i] = Dk[i];
+#pragma unroll
+                for (int i = 0; i < kLsW; ++i) w5[i] = wk[i];
+                const bool inj = kk == kc;
+                double gn[NX];
+#pragma unroll
+                for (int s2 = 0; s2 < NX; ++s2) {
+                    double v = 0.0;
+#pragma unroll
+                    for (int t2 = 0; t2 < 3; ++t2) v = fma(dv[s2 * 3 + t2], g[t2], v);
+                    gn[s2] = inj ? bcol[s2] : v + g[s2];
+                }
+#pragma unroll
+                for (int s2 = 0; s2 < NX; ++s2) g[s2] = gn[s2];
+                double gf[NXP], yf[NXP];
+                static_for<0, NXP>([&](auto s_c) __attribute__((always_inline)) {
+                    constexpr int s2 = decltype(s_c)::value;
+                    if constexpr (s2 < NX) {
+                        gf[s2] = g[s2];
+                        if constexpr (s2 == 0) yf[s2] = w5[0] * g[0];
+                        else if constexpr (s2 == 3) yf[s2] = w5[1] * g[3];
+                        else if constexpr (s2 == 7) yf[s2] = fma(w5[3], g[8], w5[2] * g[7]);
+                        else if constexpr (s2 == 8) yf[s2] = fma(w5[4], g[8], w5[3] * g[7]);
+                        else yf[s2] = q2d[s2] * g[s2];
+                    } else {
+                        gf[s2] = 0.0;
+                        yf[s2] = 0.0;
+                    }
+                });
+#pragma unroll
+                for (int q = 0; q < NXP; q += 4) {
+                    transpose_rows4(gf[q], gf[q + 1], gf[q + 2], gf[q + 3]);
+                    transpose_rows4(yf[q], yf[q + 1], yf[q + 2], yf[q + 3]);
+#pragma unroll
+                    for (int ti = 0; ti <= tau; ++ti)
+#pragma unroll
+                        for (int tj = 0; tj <= ti; ++tj)
+                            acc[ti * (ti + 1) / 2 + tj] = __builtin_amdgcn_mfma_f64_16x16x4f64(
+                                gf[q + ti], yf[q + tj], acc[ti * (ti + 1) / 2 + tj], 0, 0, 0);
+                }
+            };
+            static_for<0, T>([&](auto tau_c) __attribute__((always_inline)) {
+                constexpr int tau = decltype(tau_c)::value;
+                const int kb = (16 * tau + NU) / NU - 1;
+                const int ke0 = (16 * (tau + 1) + NU) / NU - 1;
+                const int ke = ke0 < N ? ke0 : N;
+                for (int kk = kb; kk < ke; ++kk) stage(tau_c, kk);
+            });
+        } else {
             // lane l carries column l of Gamma_k (Gamma_0 = 0) and of W_k Gamma_k; both reach the
             // MFMA fragment layout by an in-register row transpose (no LDS round trip).
             //  * column l = kc NU + ic is zero up to stage kc, where it becomes B_kc[:, ic]: the lane
@@ -862,8 +1035,18 @@ __global__ __launch_bounds__(64, 1) void mpc_ipm3_kernel(const MpcConst c, const
                         }
                         v /= Dsig[j];
                     }
+                    if constexpr (LS) {  // the row's nonzeros (same accumulation order)
+                        const double* cr = sC + k * CW;
+                        if (r < 2) ybv[0] = fma(v, cr[r], ybv[0]);
+                        else if (r < 4) ybv[3] = fma(v, cr[r], ybv[3]);
+                        else {
+                            ybv[7] = fma(v, cr[4 + 2 * (r - 4)], ybv[7]);
+                            ybv[8] = fma(v, cr[5 + 2 * (r - 4)], ybv[8]);
+                        }
+                    } else {
 #pragma unroll
-                    for (int s = 0; s < NX; ++s) ybv[s] = fma(v, sC[(k * MC + r) * NX + s], ybv[s]);
+                        for (int s = 0; s < NX; ++s) ybv[s] = fma(v, sC[(k * MC + r) * NX + s], ybv[s]);
+                    }
                 }
 #pragma unroll
                 for (int s = 0; s < NX; ++s) yb[(k + 1) * NX + s] = ybv[s];
@@ -871,14 +1054,14 @@ __global__ __launch_bounds__(64, 1) void mpc_ipm3_kernel(const MpcConst c, const
             if (l < NX) yb[l] = 0.0;
             wsync();
             STAMP(8);
-            psi3<NX>(l, N, sA, yb, yb);
+            psi3<NX, LS>(l, N, sA, yb, yb);
             wsync();
             STAMP(9);
             if (!lo && own) {
 #pragma unroll
                 for (int i = 0; i < NU; ++i) {
                     const int ci = k * NU + i;
-                    vb[ci] = -rd[ci] - (bpsi3<NX, NU>(sB, yb, k, i) + rho[2 * i] - rho[2 * i + 1]);
+                    vb[ci] = -rd[ci] - (bpsi3<NX, NU, LS>(sB, yb, k, i) + rho[2 * i] - rho[2 * i + 1]);
                 }
             }
             wsync();
@@ -947,7 +1130,7 @@ __global__ __launch_bounds__(64, 1) void mpc_ipm3_kernel(const MpcConst c, const
             for (int i = l; i < NP; i += 64) dU[i] = (i < n) ? vb[i] : 0.0;
             wsync();
             STAMP(10);
-            fwd3<NX, NU>(l, N, sA, sB, nullptr, dU, dX);
+            fwd3<NX, NU, LS>(l, N, sA, sB, nullptr, dU, dX);
             wsync();
             STAMP(11);
 #pragma unroll
@@ -1041,7 +1224,7 @@ __global__ __launch_bounds__(64, 1) void mpc_ipm3_kernel(const MpcConst c, const
     wsync();
 
     // ---- output in the reference layout ----
-    fwd3<NX, NU>(l, N, sA, sB, sx0, U, X);
+    fwd3<NX, NU, LS>(l, N, sA, sB, sx0, U, X);
     wsync();
     constexpr int NXE = NX + NS;
     const size_t nz = (size_t)NXE * (N + 1) + 2 * (size_t)n;
@@ -1076,23 +1259,23 @@ __global__ __launch_bounds__(64, 1) void mpc_ipm3_kernel(const MpcConst c, const
 #undef ACT
 }
 
-template <int T, int NX, int NU, int NB>
+template <int T, int NX, int NU, int NB, bool LS>
 static hipError_t launch3(const MpcConst& c, const MpcPtrs& p, int batch, hipStream_t s) {
-    const size_t lds = sizeof(double) * (size_t)lds3_layout<T, NX, NU, NB>(c.N).total;
-    hipError_t e = hipFuncSetAttribute((const void*)mpc_ipm3_kernel<T, NX, NU, NB>,
+    const size_t lds = sizeof(double) * (size_t)lds3_layout<T, NX, NU, NB, LS>(c.N).total;
+    hipError_t e = hipFuncSetAttribute((const void*)mpc_ipm3_kernel<T, NX, NU, NB, LS>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL((mpc_ipm3_kernel<T, NX, NU, NB>), dim3(batch), dim3(64), lds, s, c, p);
+    hipLaunchKernelGGL((mpc_ipm3_kernel<T, NX, NU, NB, LS>), dim3(batch), dim3(64), lds, s, c, p);
     return hipGetLastError();
 }
 
-template <int NX, int NU, int NB>
+template <int NX, int NU, int NB, bool LS = false>
 static hipError_t launch3_t(const MpcConst& c, const MpcPtrs& p, int batch, hipStream_t s) {
     switch (c.npad / 16) {
-        case 1: return launch3<1, NX, NU, NB>(c, p, batch, s);
-        case 2: return launch3<2, NX, NU, NB>(c, p, batch, s);
-        case 3: return launch3<3, NX, NU, NB>(c, p, batch, s);
-        default: return launch3<4, NX, NU, NB>(c, p, batch, s);
+        case 1: return launch3<1, NX, NU, NB, LS>(c, p, batch, s);
+        case 2: return launch3<2, NX, NU, NB, LS>(c, p, batch, s);
+        case 3: return launch3<3, NX, NU, NB, LS>(c, p, batch, s);
+        default: return launch3<4, NX, NU, NB, LS>(c, p, batch, s);
     }
 }
 
@@ -1105,6 +1288,12 @@ static hipError_t launch3_t(const MpcConst& c, const MpcPtrs& p, int batch, hipS
     if (c.nx == NX_ && c.nu == NU_ && nb == NB_) {          \
         *err = launch3_t<NX_, NU_, NB_>(c, p, batch, s);    \
         return true;                                        \
+    }
+// the reference's agent as built by lpv_build.hip (MpcConst::lpv; the fused DI rows never apply)
+#define CASE_LS(NB_)                                                        \
+    if (c.lpv && c.nx == 9 && c.nu == 2 && nb == NB_ && !p.fuse.on) {       \
+        *err = launch3_t<9, 2, NB_, true>(c, p, batch, s);                  \
+        return true;                                                        \
     }
 #if CMPC_V3_SET == 1
 bool mpc3_try_set2(const MpcConst& c, const MpcPtrs& p, int batch, hipStream_t s, hipError_t* err, int nb);
@@ -1127,6 +1316,9 @@ bool mpc3_try_launch(const MpcConst& c, const MpcPtrs& p, int batch, hipStream_t
 }
 #elif CMPC_V3_SET == 2
 bool mpc3_try_set2(const MpcConst& c, const MpcPtrs& p, int batch, hipStream_t s, hipError_t* err, int nb) {
+    CASE_LS(2)
+    CASE_LS(1)
+    CASE_LS(0)
     CASE(9, 2, 2)
     CASE(9, 2, 1)
     CASE(9, 2, 0)
@@ -1139,10 +1331,12 @@ bool mpc3_try_set3(const MpcConst& c, const MpcPtrs& p, int batch, hipStream_t s
 }
 #else
 bool mpc3_try_set4(const MpcConst& c, const MpcPtrs& p, int batch, hipStream_t s, hipError_t* err, int nb) {
+    CASE_LS(3)
     CASE(9, 2, 3)
     return false;
 }
 #endif
 #undef CASE
+#undef CASE_LS
 
 }  // namespace cmpc
