@@ -136,6 +136,7 @@ def main():
     if rank == 0 and world == 1 and not args.no_ref and not cfg5:
         ref_line = reference_config(ctx)
         ref_line["lpv_rounds"] = lpv_rounds(ctx)
+        ref_line["lpv_rounds_finish"] = lpv_rounds(ctx, finish=True, check=False)
         osqp_line = osqp_dropin(ctx)
 
     if rank == 0:
@@ -278,7 +279,7 @@ def reference_config_cpu(bp, args, res, z_cert):
             "max_abs_err_vs_gpu": max(errg)}
 
 
-def lpv_population(ctx, replicas=341, rescue=True):
+def lpv_population(ctx, replicas=341, rescue=True, finish=False):
     """The population of the `lpv_rounds` line: `replicas` copies of the reference's 3-agent
     Highway scenario at its captured step 0 (tests/golden/lpv_n30_a3: x0, Last_xPredicted, uPred,
     OldSteering/OldAccelera, positions), each copy's initial v_x scaled by a seeded factor in
@@ -313,6 +314,8 @@ def lpv_population(ctx, replicas=341, rescue=True):
                               ctx=ctx)
     if not rescue:
         bp.opts = L.opts()
+    elif finish:
+        bp.opts = L.opts(flags=L.CMPC_FLAG_RESCUE | L.CMPC_FLAG_FINISH)
     return bp, (x0, x_last, u_last, nbr), dict(u_old=u_old, traj=traj)
 
 
@@ -331,11 +334,12 @@ def lpv_check_round(bp, R, sample):
              u_lb=np.array([-prm.max_ls, -prm.max_dc]), row_slack=np.array([-1, 0, 1, 1] + [2] * R.nb),
              row_sign=np.array([1, 1, 1, 1] + [-1] * R.nb), A=b["A"], B=b["B"], x0=R.x0.cpu().numpy()[sample],
              u_prev=R.u_old.cpu().numpy()[sample], qlin=b["qlin"], C=b["C"], h=b["h"])
-    zc, _, _, sc = CO.solve_batch_rescue(P, nthreads=min(16, os.cpu_count() or 1))
+    finish = bool(bp.opts.flags & 64)   # CMPC_FLAG_FINISH
+    zc, _, _, sc = CO.solve_batch_rescue(P, nthreads=min(16, os.cpu_count() or 1), finish=finish)
     return zc, sc
 
 
-def lpv_rounds(ctx, replicas=341, rounds=20, warmup=2, rescue=True, check=True, sample=128):
+def lpv_rounds(ctx, replicas=341, rounds=20, warmup=2, rescue=True, check=True, sample=128, finish=False):
     """The reference's own agent model in device-resident consensus rounds (cmpc.rounds.LPVRounds:
     gather -> LPV scheduling + planes + QP build + solve -> advance -> exchange, all in HBM), at
     N = 30 (nx 9, nu 2, 2 neighbours: the v3 kernel), on lpv_population's 1023 agents.  Timed
@@ -347,7 +351,7 @@ def lpv_rounds(ctx, replicas=341, rounds=20, warmup=2, rescue=True, check=True, 
 
     from cmpc.rounds import LPVRounds
 
-    bp, args, kw = lpv_population(ctx, replicas, rescue)
+    bp, args, kw = lpv_population(ctx, replicas, rescue, finish)
     N = bp.N
     R = LPVRounds(bp, *args, **kw)
     dev = R.dev
@@ -373,7 +377,7 @@ def lpv_rounds(ctx, replicas=341, rounds=20, warmup=2, rescue=True, check=True, 
                        f"round = gather + LPV build + solve + advance + exchange",
            "agent_qp_per_s": B * rounds / el, "ms_per_round": el / rounds * 1e3,
            "build_solve_ms": sum(a.elapsed_time(b) for a, b in ev) / rounds, "rounds": rounds, "warmup": warmup,
-           "rescue": rescue, "mean_ipm_iters": float(it.mean()), "max_ipm_iters": int(it.max()),
+           "rescue": rescue, "finish": finish, "mean_ipm_iters": float(it.mean()), "max_ipm_iters": int(it.max()),
            "max_ipm_iters_per_round": it.max(1).tolist(), "max_kkt": float(kk.max()),
            "status_counts": {int(k): int(v) for k, v in zip(*np.unique(st, return_counts=True))}}
     if check:

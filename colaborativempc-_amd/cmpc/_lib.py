@@ -40,7 +40,8 @@ _IP = ct.POINTER(ct.c_int)
 CMPC_FLAG_GENERIC = 1
 CMPC_FLAG_FP32 = 8
 CMPC_FLAG_RICCATI = 16
-CMPC_FLAG_RESCUE = 32   # Riccati re-solve of agents whose condensed factorisation broke down
+CMPC_FLAG_RESCUE = 32   # Riccati continuation of agents whose condensed factorisation broke down
+CMPC_FLAG_FINISH = 64   # ... also of breakdowns already at the rounding floor (status 2)
 
 
 class cmpc_opts(ct.Structure):

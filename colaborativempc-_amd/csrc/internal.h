@@ -26,6 +26,7 @@ struct MpcConst {
     int riccati;  // 1: stage-wise Riccati kernel (fp64, N*nu > 64 or CMPC_FLAG_RICCATI)
     int rescue;   // 1: CMPC_FLAG_RESCUE on a condensed solve (Riccati re-solve of broken-down agents)
     int lpv;      // 1: data made by lpv_build.hip with Q diagonal (the v3 kernel's LS layout applies)
+    int finish;   // 1: CMPC_FLAG_FINISH (rescue also continues breakdowns at the rounding floor)
     unsigned long long ws_stride;  // doubles of MpcPtrs::ws per agent (set by mpc_launch; 0: no scratch)
     double tol;
     double qs_max;  // max(1, 2*max(Qs)) — slack residual scale
@@ -127,6 +128,13 @@ __host__ __device__ inline size_t hand_t(const MpcConst& c) { return 2 + (size_t
 // iteration runs in double-double: 3 (the kStallIters of the condensed solve) and 8 gave the same
 // statuses in the lab, so the short one is kept.
 constexpr int kWarmStall = 3;
+// A breakdown whose best iterate is already at the rounding floor (merit < 1e3 tol, status 2) is
+// handed over only with CMPC_FLAG_FINISH (MpcConst::finish): on bench.py's lpv_rounds population
+// that finishes ~60 % of the status-2 agents (720 -> 284 of 20 460) at 112k instead of 178k
+// agent-QP/s (every dd iteration of a continued solve costs ~1 ms at N = 30).
+__host__ __device__ inline bool hand_over(int stop, double best_m, const MpcConst& c) {
+    return stop == kStopBreakdown && (c.finish || !(best_m < 1e3 * c.tol));
+}
 
 // Stage-wise Riccati kernel (mpc_riccati.hip): any horizon whose per-agent rows fit LDS.
 size_t mpc_riccati_lds_bytes(const MpcConst& c);

@@ -661,7 +661,7 @@ __global__ __launch_bounds__(kWave) void mpc_ipm_kernel(const MpcConst c, const 
         if (P.iters) P.iters[b] = it;
         if (P.status) P.status[b] = status;
         // rescue hand-over flag: set only by a breakdown (the iterate was written there)
-        if (c.rescue && P.ws) P.ws[(size_t)b * c.ws_stride] = stop == kStopBreakdown ? 1.0 : 0.0;
+        if (c.rescue && P.ws) P.ws[(size_t)b * c.ws_stride] = hand_over(stop, best_m, c) ? 1.0 : 0.0;
     }
 }
 
@@ -727,6 +727,7 @@ int mpc_prepare(const cmpc_mpc_dims* d, const cmpc_mpc_weights* wt, const cmpc_o
     // rescue pass (CMPC_FLAG_RESCUE): only for condensed fp64 solves whose rows fit the Riccati kernel
     c->rescue = (!fp32 && !c->riccati && (o && (o->flags & CMPC_FLAG_RESCUE)) && mpc_riccati_lds_bytes(*c) <= kMaxLdsBytes)
                     ? 1 : 0;
+    c->finish = (c->rescue && (o->flags & CMPC_FLAG_FINISH)) ? 1 : 0;
     for (int i = 0; i < d->nu; ++i) {
         c->u_ub[i] = wt->u_ub[i];
         c->u_lb[i] = wt->u_lb[i];

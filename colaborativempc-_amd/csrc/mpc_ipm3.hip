@@ -1248,7 +1248,7 @@ __global__ __launch_bounds__(64, 1) void mpc_ipm3_kernel(const MpcConst c, const
         if (P.iters) P.iters[b] = it;
         if (P.status) P.status[b] = status;
         // rescue hand-over flag: set only by a breakdown (the iterate was written there)
-        if (c.rescue && P.ws) P.ws[(size_t)b * c.ws_stride] = stop == kStopBreakdown ? 1.0 : 0.0;
+        if (c.rescue && P.ws) P.ws[(size_t)b * c.ws_stride] = hand_over(stop, best_m, c) ? 1.0 : 0.0;
         if (stamp) {
             unsigned long long* st = P.stamps + (size_t)b * kStampSlots;
             for (int i = 0; i < kStampSlots - 1; ++i) st[i] = tsum[i];

@@ -74,10 +74,13 @@ typedef struct cmpc_ctx cmpc_ctx;
 #define CMPC_FLAG_FP32 8     /* fp32 workgroup-per-agent solver (long horizons, BASELINE cfg5);
                                 opts.tol should then be ~1e-5 */
 #define CMPC_FLAG_RICCATI 16 /* force the stage-wise Riccati solver (fp64; the default when N*nu > 64) */
-#define CMPC_FLAG_RESCUE 32 /* condensed solves (fp64): agents whose factorisation broke down (status
-                               CMPC_UNSOLVED) are re-solved in a second launch by the stage-wise
-                               Riccati solver (double-double near the solution) on the same problem */
-#define CMPC_FLAG_ALL (CMPC_FLAG_GENERIC | CMPC_FLAG_FP32 | CMPC_FLAG_RICCATI | CMPC_FLAG_RESCUE)  /* other bits: CMPC_ERR_ARG */
+#define CMPC_FLAG_RESCUE 32 /* condensed solves (fp64): an agent whose factorisation breaks down short of
+                               1e3 tol (status CMPC_UNSOLVED) continues from its last iterate on the
+                               stage-wise Riccati solver (double-double near the solution) in a second
+                               launch; a third launch restarts cold the rare one that fails again */
+#define CMPC_FLAG_FINISH 64 /* with CMPC_FLAG_RESCUE: a breakdown whose best iterate already meets 1e3 tol
+                               (status 2) is continued too, to full tolerance (slower; fewer status 2) */
+#define CMPC_FLAG_ALL (CMPC_FLAG_GENERIC | CMPC_FLAG_FP32 | CMPC_FLAG_RICCATI | CMPC_FLAG_RESCUE | CMPC_FLAG_FINISH)  /* other bits: CMPC_ERR_ARG */
 
 typedef struct {
     double tol;    /* relative stationarity/feasibility tolerance (complementarity: 1e-4*tol); <= 0 selects 1e-9 */

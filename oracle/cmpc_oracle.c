@@ -932,7 +932,9 @@ static int solve_one(const shared_t* S, const agent_t* a, double tol, int max_it
        (newton 3), its best-iterate bookkeeping restarted (the kernels hand the iterate from
        mpc_ipm3 / mpc_ipm to mpc_riccati through the rescue scratch) */
     shared_t S_cond, S_ric;
-    const int warm_rescue = S->newton == 4;
+    /* 4: CMPC_FLAG_RESCUE | CMPC_FLAG_FINISH (every breakdown is continued); 5: CMPC_FLAG_RESCUE
+       (a breakdown already at the rounding floor, best merit < 1e3 tol, stops there: status 2) */
+    const int warm_rescue = S->newton == 4 || S->newton == 5, finish = S->newton == 4;
 #ifdef LAB_STOPDUMP
     int it_switch = 0;
 #endif
@@ -1273,7 +1275,7 @@ static int solve_one(const shared_t* S, const agent_t* a, double tol, int max_it
                             r < ms ? r % mc : (r - ms) % (2 * nu), wk->th[r]);
             fprintf(stderr, "\n");
 #endif
-            if (warm_rescue && !S->newton) {
+            if (warm_rescue && !S->newton && (finish || !(best_m < 1e3 * tol))) {
 #ifdef LAB_STOPDUMP
                 it_switch = it;
 #endif
@@ -1682,7 +1684,7 @@ int cmpc_oracle_solve_ex(int nx, int nu, int N, int ns, int mc, int batch,
 #ifdef RIC_DEBUG
         const size_t nG = (size_t)(N + 1) * nx * n, nK = (size_t)n * n;
 #else
-        const int cond = newton == 0 || newton == 4; /* the condensed Newton matrix is formed */
+        const int cond = newton == 0 || newton == 4 || newton == 5; /* the condensed Newton matrix is formed */
         const size_t nG = cond ? (size_t)(N + 1) * nx * n : 0, nK = cond ? (size_t)n * n : 0;
 #endif
         size_t need = nF + (size_t)n + (size_t)N * ns + nG + nK + 4 * (size_t)(N + 1) * nx + 4 * (size_t)n +

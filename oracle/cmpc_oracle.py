@@ -1,8 +1,8 @@
 """ORACLE (test infrastructure only) — ctypes binding of oracle/libcmpc_oracle.so,
 the plain-C condensed IPM restatement (cmpc_oracle.c).
 newton: 0 condensed Cholesky, 1 stage-wise Riccati (as csrc/mpc_riccati.hip), 2 Riccati in Joseph form,
-3 Riccati with the kernel's double-double mode, 4 condensed with the hand-over to 3 at a breakdown
-(CMPC_FLAG_RESCUE).
+3 Riccati with the kernel's double-double mode, 4 / 5 condensed with the hand-over to 3 at a breakdown
+(CMPC_FLAG_RESCUE with / without CMPC_FLAG_FINISH).
 
 Problems are plain dicts of numpy arrays (batch-major):
   nx nu N ns mc                 ints
@@ -51,13 +51,14 @@ def nz_of(p):
     return (p["nx"] + p["ns"]) * (p["N"] + 1) + 2 * p["nu"] * p["N"]
 
 
-def solve_batch_rescue(p, tol=1e-9, max_iter=60, nthreads=0):
+def solve_batch_rescue(p, tol=1e-9, max_iter=60, nthreads=0, finish=False):
     """The product's CMPC_FLAG_RESCUE policy restated: the condensed method; an agent whose
-    factorisation breaks down continues from that iterate with the Riccati method in the kernel's
-    double-double mode, its best-iterate bookkeeping restarted (newton 4, the kernels' hand-over);
-    an agent that still ends CMPC_UNSOLVED is re-solved by that Riccati method from a cold start
-    (newton 3, the second rescue pass)."""
-    z, kkt, it, st = solve_batch(p, tol, max_iter, nthreads, newton=4)
+    factorisation breaks down short of the rounding floor (best merit >= 1e3 tol; with ``finish``,
+    CMPC_FLAG_FINISH, every breakdown) continues from that iterate with the Riccati method in the
+    kernel's double-double mode, its best-iterate bookkeeping restarted (newton 5 / 4, the kernels'
+    hand-over); an agent that still ends CMPC_UNSOLVED is re-solved by that Riccati method from a
+    cold start (newton 3, the second rescue pass)."""
+    z, kkt, it, st = solve_batch(p, tol, max_iter, nthreads, newton=4 if finish else 5)
     bad = np.flatnonzero(st == -10)
     if len(bad):
         q = dict(p)

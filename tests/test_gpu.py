@@ -142,7 +142,8 @@ def test_lpv_rounds_device_resident_vs_reference_loop(gpu_ctx, name):
         assert np.array_equal(R.traj_all.cpu().numpy(), np.swapaxes(hag, 0, 1))
 
 
-def test_rescue_pass_resolves_factorisation_breakdowns(gpu_ctx):
+@pytest.mark.parametrize("finish", [False, True])
+def test_rescue_pass_resolves_factorisation_breakdowns(gpu_ctx, finish):
     """CMPC_FLAG_RESCUE: in closed-loop LPV rounds (341 jittered copies of the reference's
     3-agent N = 30 run) run without it until a round has agents whose condensed factorisation
     broke down (status CMPC_UNSOLVED); the same round re-solved with the flag: the agents that
@@ -169,7 +170,8 @@ def test_rescue_pass_resolves_factorisation_breakdowns(gpu_ctx):
     g, model = _gains()
     bp = cmpc.PlannerLPVBatch(g["Q"], g["Qs"], g["R"], g["dR"], N, dt, LR.Track.build("Highway"), g["wq"], model,
                               LR.scaled_car_limits(float(d["vx_ref"])), ctx=gpu_ctx)
-    plain, rescue = L.opts(), L.opts(flags=L.CMPC_FLAG_RESCUE)
+    plain = L.opts()
+    rescue = L.opts(flags=L.CMPC_FLAG_RESCUE | (L.CMPC_FLAG_FINISH if finish else 0))
     R = LPVRounds(bp, x0, np.tile(np.stack([d[f"x_last_{j}"] for j in sel]), (reps, 1, 1)),
                   np.tile(np.stack([d[f"u_last_{j}"] for j in sel]), (reps, 1, 1)), nbr,
                   u_old=np.tile(d["u_old"][sel], (reps, 1)), traj=np.tile(d["pose"][sel], (reps, 1, 1)))
@@ -198,13 +200,16 @@ def test_rescue_pass_resolves_factorisation_breakdowns(gpu_ctx):
                      u_ub=np.array([0.3, 5.0]), u_lb=np.array([-0.3, -10.0]), row_slack=np.array([-1, 0, 1, 1, 2, 2]),
                      row_sign=np.array([1, 1, 1, 1, -1, -1]), A=b["A"], B=b["B"], x0=R.x0.cpu().numpy(),
                      u_prev=R.u_old.cpu().numpy(), qlin=b["qlin"], C=b["C"], h=b["h"])
-            zc, kc, ic, sc = CO.solve_batch_rescue(P, nthreads=8)
+            zc, kc, ic, sc = CO.solve_batch_rescue(P, nthreads=8, finish=finish)
             both = (sc == 1) & (st1 == 1)
             err = np.abs(zc - z1).max(1)
             print(f"round {rnd}: {int(bad.sum())} broken down (status -10), {int(changed.sum())} continued; "
                   f"{int(both.sum())} of {R.B} solved by both, max |dz| {err[both].max():.1e}; GPU status 2 "
                   f"{int((st1 == 2).sum())}; C statuses {dict(zip(*[a.tolist() for a in np.unique(sc, return_counts=True)]))}")
-            assert both.mean() >= 0.95 and err[both].max() < 1e-6
+            # agents at the rounding floor (status 2, KKT <= 1e-6 asserted above) are not compared;
+            # without CMPC_FLAG_FINISH a breakdown already at the floor stays there (~8 % of this
+            # round on both sides), with it they are finished
+            assert both.mean() >= (0.95 if finish else 0.85) and err[both].max() < 1e-6
             return
         R.advance()
         R.exchange()
