@@ -1,8 +1,10 @@
 """ORACLE (test infrastructure only) — numpy restatement of the reference's OCD
 coupling-dual round (planner/scripts/NL_EU_N_main.py:119-162) in its own dense
 (n_agents, n_agents, N) layout, and the map to the neighbour-graph layout of
-cmpc_ocd_update_dev.  Parity unpinned by recorded data: the only committed lambda
-artefact (ini_lambdas.pkl of NL_3agents_def) is all zeros."""
+cmpc_ocd_update_dev.  Pinned bit-exactly by tests/golden/ocd_rounds.npz: rounds computed by the
+reference's own get_alpha / eval_constraintEU (oracle/gen_ocd_fixtures.py imports them from
+plan_lib.config.NL); the only recorded lambda artefact (ini_lambdas.pkl of NL_3agents_def) is all
+zeros."""
 import numpy as np
 
 

@@ -675,3 +675,32 @@ def test_lpv_builder_readback_matches_oracle_builder(gpu_ctx, name):
             a, b = o[k][0], s[k][0]
             ulp = np.spacing(np.maximum(np.abs(a), np.abs(b)))
             assert (np.abs(a - b) <= 16 * ulp).all(), (k, float(np.abs(a - b).max()))
+
+
+def test_ocd_round_bit_exact_against_reference_functions(gpu_ctx):
+    """cmpc_ocd_update_dev / cmpc_ocd_converged_dev against rounds computed by the reference's own
+    get_alpha / eval_constraintEU (config/NL/config.py:5-8,19-23) in the loop of
+    NL_EU_N_main.py:127-149 (tests/golden/ocd_rounds.npz, oracle/gen_ocd_fixtures.py): 3 and 5
+    agents, consecutive rounds, bit-exact (built without fma contraction, as numpy evaluates)."""
+    import torch
+
+    from cmpc import ocd
+    from oracle import ocd_ref
+
+    d = golden("ocd_rounds")
+    c = 0
+    while f"c{c}_n" in d.files:
+        n, N, dth = int(d[f"c{c}_n"]), int(d[f"c{c}_N"]), float(d[f"c{c}_dth"])
+        nbr = np.array([[j for j in range(n) if j != i] for i in range(n)], np.int32)
+        lam = torch.tensor(ocd_ref.to_neighbour_layout(d[f"c{c}_r0_lam_in"], nbr), device="cuda")
+        tnbr = torch.tensor(nbr, device="cuda")
+        for r in range(int(d[f"c{c}_rounds"])):
+            traj = torch.tensor(np.swapaxes(d[f"c{c}_r{r}_agents"], 0, 1).copy(), device="cuda")
+            ocd.dual_update(lam, traj, tnbr, self_offset=0, dth=dth, ctx=gpu_ctx)
+            want = ocd_ref.to_neighbour_layout(d[f"c{c}_r{r}_lam_out"], nbr)
+            assert np.array_equal(lam.cpu().numpy(), want), (c, r)
+            if f"c{c}_r{r}_close" in d.files:
+                close, allc = ocd.converged(torch.tensor(d[f"c{c}_r{r}_x_old"], device="cuda"),
+                                            torch.tensor(d[f"c{c}_r{r}_x_pred"], device="cuda"), ctx=gpu_ctx)
+                assert np.array_equal(close.cpu().numpy().astype(bool), d[f"c{c}_r{r}_close"])
+        c += 1

@@ -101,3 +101,29 @@ def test_settings_rewrite_is_byte_identical_to_reference_file(tmp_path):
         rows = [tuple(r) for r in csv.reader(f)]
     logio.save_settings(str(tmp_path), dict(rows))
     assert _bytes(os.path.join(tmp_path, "settings.csv")) == _bytes(src)
+
+
+def _ocd_cases():
+    from conftest import golden
+
+    d = golden("ocd_rounds")
+    c = 0
+    while f"c{c}_n" in d.files:
+        yield c, d
+        c += 1
+
+
+def test_ocd_oracle_bit_exact_against_reference_functions():
+    """oracle.ocd_ref restates the dual update and the convergence test of NL_EU_N_main.py:127-149;
+    tests/golden/ocd_rounds.npz holds rounds computed by the reference's own get_alpha and
+    eval_constraintEU (oracle/gen_ocd_fixtures.py): bit-exact."""
+    from oracle import ocd_ref
+
+    for c, d in _ocd_cases():
+        n, N, dth = int(d[f"c{c}_n"]), int(d[f"c{c}_N"]), float(d[f"c{c}_dth"])
+        for r in range(int(d[f"c{c}_rounds"])):
+            got = ocd_ref.ocd_update(d[f"c{c}_r{r}_lam_in"], d[f"c{c}_r{r}_agents"], N, dth)
+            assert np.array_equal(got, d[f"c{c}_r{r}_lam_out"]), (c, r)
+            if f"c{c}_r{r}_close" in d.files:
+                assert np.array_equal(ocd_ref.allclose_agents(d[f"c{c}_r{r}_x_old"], d[f"c{c}_r{r}_x_pred"]),
+                                      d[f"c{c}_r{r}_close"])
