@@ -11,11 +11,21 @@ Restatement of the reference's MATLAB per-agent QP path:
   beq = F(1:K.f,1), A = -F(K.f+1:end,2:end), b = F(K.f+1:end,1) :38-46, Q <- 2Q :61);
   callquadprog.m:63-69 then calls quadprog(Q, c, A, b, Aeq, beq, lb, ub, x0, ops).
 
-MATLAB, YALMIP and quadprog are absent: PARITY UNPINNED by reference outputs.
+* the planner script's scheduling of those parameters, PLAN_NL_LPV_MPC_dt_WORKS_Oval.m:127-200
+  (k = 1 from the NL_vars.mat it loads at :19, later steps from the previous solution), the
+  oval track's curvature lookup (MapMod.m "oval", Curvature.m) and the arc-length update
+  :259-260, with the script's left/right swap when it builds the inputs list (:237-238 pass
+  {..., right_limit, left_limit} to parameters_in's {..., left_limit, right_limit}).
+
+MATLAB, YALMIP and quadprog are absent: PARITY UNPINNED by quadprog outputs.
 What pins it: the transformation is restated line by line and checked on hand-built known
-answers (tests/test_matlab_ref.py), and every model's optimum is certified by the KKT
-residual of the dense IPM oracle/qp_ipm.py (tests/golden/matlab_lpv_mpc.npz, made by
-oracle/gen_matlab_fixtures.py).
+answers (tests/test_matlab_ref.py); the first control step's parameters come from the
+reference's own data file NL_vars.mat (read by scipy.io.loadmat, data only) through the
+restated :127-167; every model's optimum is certified by the KKT residual of the dense IPM
+oracle/qp_ipm.py (tests/golden/matlab_lpv_mpc.npz, made by oracle/gen_matlab_fixtures.py).
+Steps k >= 2 are scheduled from the certified optimum of step k-1; the reference's optimum has
+flat directions (tests/test_mex_gpu.py::_flat_directions), so quadprog could pick another point
+of the same face and schedule slightly different parameters from it.
 
 Variable order (YALMIP orders by sdpvar creation; the ones that survive parameter
 substitution here are the decision variables, in this restatement's order):
@@ -171,6 +181,106 @@ def lpv_mpc_interface(Hp, dt, p, max_vel=3.5):
         rows.append(r)
     F = np.vstack(eqs + rows)
     return F, len(eqs), c, Q, lb, ub
+
+
+# ---- the planner script's scheduling (PLAN_NL_LPV_MPC_dt_WORKS_Oval.m) ----
+# vehicle constants of :46-53 (this script's, not the Python planners' scaled car)
+PLAN_LF, PLAN_LR, PLAN_M, PLAN_I, PLAN_CF, PLAN_CR = 0.125, 0.125, 1.98, 0.03, 70.0, 70.0
+PLAN_HP, PLAN_TSS = 15, 0.1                      # :44, Tss of NL_vars.mat
+PLAN_X0 = np.array([0.97, 0.0, 0.0, 0.0, 0.0])   # :162 [vx, vy, w, ey, etheta]
+
+
+def oval_segments(side=1):
+    """MapMod.m "oval" (spec of lane `side`, scale 2 on lane 1): the Curvature.m-relevant columns
+    of PointAndTangent — cumulative s at the segment start (column 4), segment length (5) and
+    signed curvature (6) — for the spec rows (Curvature.m loops over all rows but the closing
+    one).  Straights have curvature 0, arcs 1/r (MapMod.m: NewLine(6) = 1 / r)."""
+    if side == 1:
+        spec = 2.0 * np.array([[1.0, 0.0], [4.5, 4.5 / np.pi], [2.0, 0.0], [4.5, 4.5 / np.pi], [1.0, 0.0]])
+    else:
+        spec = np.array([[2.0, 0.0], [5.85, 5.85 / np.pi], [4.0, 0.0], [5.85, 5.85 / np.pi], [2.0, 0.0]])
+    length = spec[:, 0]
+    s0 = np.concatenate([[0.0], np.cumsum(length)[:-1]])
+    curv = np.where(spec[:, 1] == 0.0, 0.0, 1.0 / np.where(spec[:, 1] == 0.0, 1.0, spec[:, 1]))
+    return s0, length, curv
+
+
+def curvature(s, seg):
+    """Curvature.m: wrap s by the track length (end-1 row's s + length), then the LAST segment
+    with s0 <= s <= s0 + len wins (both ends inclusive)."""
+    s0, length, curv = seg
+    track = s0[-1] + length[-1]
+    while s > track:
+        s = s - track
+    idx = None
+    for i in range(len(s0)):
+        if s >= s0[i] and s <= s0[i] + length[i]:
+            idx = i
+    if idx is None:
+        raise ValueError("s before the start of the track")   # MATLAB: undefined indx
+    return curv[idx]
+
+
+def _lpv_entries(vx, vy, psi_e, ey, delta, curv):
+    """:141-160 / :181-197 — A_1..A_10, B_1..B_4 from a scheduling trajectory."""
+    lf, lr, m, I, Cf, Cr = PLAN_LF, PLAN_LR, PLAN_M, PLAN_I, PLAN_CF, PLAN_CR
+    sd, cd = np.sin(delta), np.cos(delta)
+    return dict(A1=1.0 / (1.0 - ey * curv), A2=np.sin(psi_e), A3=np.array(vy, float), A4=np.array(vx, float),
+                A5=(sd * Cf) / (m * vx), A6=(sd * Cf * lf) / (m * vx) + vy,
+                A7=-(Cr + Cf * cd) / (m * vx), A8=-(lf * Cf * cd - lr * Cr) / (m * vx) - vx,
+                A9=-(lf * Cf * cd - lr * Cr) / (I * vx), A10=-(lf * lf * Cf * cd + lr * lr * Cr) / (I * vx),
+                B1=-(sd * Cf) / m, B2=np.ones_like(vx), B3=(Cf * cd) / m, B4=(lf * Cf * cd) / I)
+
+
+def _limits(Hp, counter=0):
+    """:227-232 and the swap of :237-238: returns the (left, right) PARAMETERS of the controller."""
+    left_limit = (0.5 + counter * 0.1) * np.ones(Hp + 1)
+    right_limit = (-0.5 - counter * 0.1) * np.ones(Hp + 1)
+    return right_limit, left_limit
+
+
+def plan_first_step(nl, Hp=PLAN_HP, side=1):
+    """Optimizer inputs of control step k = 1 (:127-167) from NL_vars.mat's arrays `nl`
+    (ss_NL, ey_NL, etheta_NL, Vy_NL, Vx_NL, delta; each 1 x 26)."""
+    g = lambda k: np.asarray(nl[k], float).ravel()   # noqa: E731
+    seg = oval_segments(side)
+    ss = g("ss_NL")
+    curv = np.zeros(Hp + 1)
+    for j in range(Hp):                                   # :131-133
+        curv[j] = curvature(ss[j], seg)
+    s_variation = ss[Hp - 1] - ss[Hp - 2]                 # :136-137
+    curv[Hp] = curvature(ss[Hp - 1] + s_variation, seg)
+    p = _lpv_entries(g("Vx_NL")[:Hp], g("Vy_NL")[:Hp], g("etheta_NL")[:Hp], g("ey_NL")[:Hp], g("delta")[:Hp],
+                     curv[:Hp])
+    left, right = _limits(Hp)
+    p.update(x1=PLAN_X0.copy(), curv=curv, left=left, right=right)
+    return p
+
+
+def plan_next_step(z, s_hist, k, curv_prev, Hp=PLAN_HP, side=1):
+    """After the step-(k-1) solve with decision vector z (this module's variable order): the
+    arc-length update :259-260 extends s_hist (0-based list, s_hist[i] = MATLAB s(i+1)), then the
+    step-k inputs of :171-199 (x0 = XX_dt(:,1), scheduling on XX_dt / UU_dt).  Returns p."""
+    XX = z[: NX * Hp].reshape(Hp, NX).T                   # XX_dt = x(:, 2:end), 5 x Hp
+    UU = z[NX * Hp: (NX + NU) * Hp].reshape(Hp, NU).T     # UU_dt = u, 2 x Hp
+    kk = k - 1                                            # the step just solved
+    for j in range(1, Hp + 1):                            # :259-260, s(kk+j)
+        vx, vy, ey, pe = XX[0, j - 1], XX[1, j - 1], XX[3, j - 1], XX[4, j - 1]
+        val = s_hist[kk + j - 2] + ((vx * np.cos(pe) - vy * np.sin(pe)) / (1.0 - ey * curv_prev[j - 1])) * PLAN_TSS
+        if len(s_hist) < kk + j:
+            s_hist.append(val)
+        else:
+            s_hist[kk + j - 1] = val
+    seg = oval_segments(side)
+    curv = np.zeros(Hp + 1)
+    for j in range(1, Hp + 1):                            # :171-173, s(k+j-1)
+        curv[j - 1] = curvature(s_hist[k + j - 2], seg)
+    s_variation = s_hist[k + Hp - 2] - s_hist[k + Hp - 3]
+    curv[Hp] = curvature(s_hist[k + Hp - 2] + s_variation, seg)
+    p = _lpv_entries(XX[0], XX[1], XX[4], XX[3], UU[0], curv[:Hp])
+    left, right = _limits(Hp)
+    p.update(x1=XX[:, 0].copy(), curv=curv, left=left, right=right)
+    return p
 
 
 def sample_parameters(Hp, seed, vx=1.5, curv_amp=0.4):

@@ -1,8 +1,10 @@
 """The MATLAB per-agent QP path restated (oracle/matlab_ref.py): YALMIP's quadprog model
 transformation (yalmip2quadprog.m) on hand-built known answers, and the 5-state LPV-MPC models
 of LPV_MPC_fnc_dt_Vnew.m regenerated bit for bit against the committed, KKT-certified
-fixtures (tests/golden/matlab_lpv_mpc.npz, oracle/gen_matlab_fixtures.py).  MATLAB is absent:
-parity with MATLAB's own output is unpinned (oracle/matlab_ref.py header)."""
+fixtures (tests/golden/matlab_lpv_mpc.npz, oracle/gen_matlab_fixtures.py), including the planner
+script's first control steps scheduled from the reference's NL_vars.mat
+(PLAN_NL_LPV_MPC_dt_WORKS_Oval.m:127-200).  MATLAB is absent: parity with quadprog's own output
+is unpinned (oracle/matlab_ref.py header)."""
 import os
 
 import numpy as np
@@ -50,3 +52,33 @@ def test_lpv_mpc_models_regenerate_and_are_certified():
         assert np.abs(mod["Aeq"] @ z - mod["beq"]).max() < 1e-9
         assert (mod["A"] @ z - mod["b"]).max() < 1e-9
         assert (z - mod["lb"]).min() > -1e-9 and (mod["ub"] - z).min() > -1e-9
+
+
+def test_oval_curvature_lookup():
+    seg = M.oval_segments(1)
+    # MapMod.m "oval" lane 1: straight 2, arc 9 of radius 9/pi, straight 4, arc, straight 2
+    np.testing.assert_allclose(seg[0], [0.0, 2.0, 11.0, 15.0, 24.0])
+    assert M.curvature(1.0, seg) == 0.0 and M.curvature(2.0, seg) == np.pi / 9   # both ends inclusive, last wins
+    assert M.curvature(26.0 + 3.0, seg) == np.pi / 9                             # wraps by the track length 26
+    assert M.curvature(24.5, seg) == 0.0
+
+
+def test_planner_steps_from_nl_vars_regenerate():
+    """Step 1 re-derived from the stored NL_vars.mat arrays (:127-167, limits swapped at :237-238),
+    steps 2..4 from the stored optimum of the step before (:171-199, :259-260)."""
+    d = np.load(GOLD, allow_pickle=False)
+    Hp, steps = int(d["Hp"]), int(d["plan_steps"])
+    nl = {k[3:]: d[k] for k in d.files if k.startswith("nl_")}
+    p = M.plan_first_step(nl, Hp)
+    # the swap: the controller's left parameter is the script's right_limit (-0.5)
+    np.testing.assert_array_equal(p["left"], -0.5)
+    np.testing.assert_array_equal(p["right"], 0.5)
+    np.testing.assert_array_equal(p["x1"], [0.97, 0, 0, 0, 0])
+    s_hist = [0.0]
+    for j in range(steps):
+        for k in p:
+            np.testing.assert_array_equal(p[k], d[f"p{j}_{k}"], err_msg=f"step {j + 1} {k}")
+        if j + 1 < steps:
+            p = M.plan_next_step(d[f"z{j}"], s_hist, j + 2, p["curv"], Hp)
+            np.testing.assert_array_equal(p["x1"], d[f"z{j}"][:5])        # x0 = XX_dt(:,1)
+    assert len(s_hist) == steps - 1 + Hp and all(np.diff(s_hist) > 0)

@@ -3,7 +3,8 @@ on the GPU, checked against oracles — not against cmpc.quadprog itself:
 
 * sparse arguments as YALMIP passes them (yalmip2quadprog.m:38-70 slices sparse Q / A / Aeq
   out of F_struc) on the MATLAB variant's 5-state LPV-MPC models (LPV_MPC_fnc_dt_Vnew.m,
-  oracle/matlab_ref.py) against their KKT-certified optima (tests/golden/matlab_lpv_mpc.npz);
+  oracle/matlab_ref.py) against their KKT-certified optima (tests/golden/matlab_lpv_mpc.npz):
+  the planner script's first four control steps scheduled from NL_vars.mat and four hand-built;
 * the struct form (cmpc_solve_mpc_batch through MATLAB plumbing) on BASELINE cfg2 — 64 agents,
   N = 20, nb = 2 — against the C restatement oracle/cmpc_oracle.c."""
 import os
@@ -32,7 +33,7 @@ def _flat_directions(mod, curv=1e-5):
     return Z @ V[:, ev < curv]
 
 
-@pytest.mark.parametrize("case", range(4))
+@pytest.mark.parametrize("case", range(8))
 def test_mex_sparse_yalmip_model_matches_certified_optimum(gpu_ctx, case):
     d = np.load(GOLD, allow_pickle=False)
     mod = {k: d[f"m{case}_{k}"] for k in ("H", "f", "A", "b", "Aeq", "beq", "lb", "ub")}
