@@ -42,6 +42,7 @@ CMPC_FLAG_FP32 = 8
 CMPC_FLAG_RICCATI = 16
 CMPC_FLAG_RESCUE = 32   # Riccati continuation of agents whose condensed factorisation broke down
 CMPC_FLAG_FINISH = 64   # ... also of breakdowns already at the rounding floor (status 2)
+CMPC_FLAG_LANE = 128    # lane-per-agent stage-wise kernel, fp64
 
 
 class cmpc_opts(ct.Structure):

@@ -48,18 +48,21 @@ def check_shapes(p, batch):
             raise ValueError(f"{k}: shape {np.shape(p[k])} != {shp}")
 
 
-FP32_TOL = 1e-5   # default tolerance of the fp32 workgroup solver (BASELINE cfg5)
+FP32_TOL = 1e-6   # default tolerance of the fp32 path (BASELINE cfg5; lane kernel, mixed precision)
 
 
-def _flags(fp32=False, riccati=False, generic=False, rescue=False):
+def _flags(fp32=False, riccati=False, generic=False, rescue=False, lane=False):
     return (L.CMPC_FLAG_FP32 if fp32 else 0) | (L.CMPC_FLAG_RICCATI if riccati else 0) | \
-        (L.CMPC_FLAG_GENERIC if generic else 0) | (L.CMPC_FLAG_RESCUE if rescue else 0)
+        (L.CMPC_FLAG_GENERIC if generic else 0) | (L.CMPC_FLAG_RESCUE if rescue else 0) | \
+        (L.CMPC_FLAG_LANE if lane else 0)
 
 
 def solve_mpc(p, ctx=None, tol=None, max_iter=None, fp32=False, riccati=False, generic=False, rescue=False,
-              stamps=None):
+              stamps=None, lane=False):
     """Solve a batch of structured agent-QPs on the GPU (host arrays in/out).
-    ``fp32``: the fp32 workgroup-per-agent solver (long horizons, BASELINE cfg5);
+    ``fp32``: the fp32 path (BASELINE cfg5): the lane-per-agent kernel with an fp32 Riccati
+    factorisation where it is instantiated, else the fp32 workgroup-per-agent solver;
+    ``lane``: the lane-per-agent stage-wise kernel in fp64;
     ``riccati``: force the stage-wise Riccati solver (the default when N*nu > 64);
     ``generic``: force the runtime-dimension condensed kernel;
     ``rescue``: CMPC_FLAG_RESCUE (a condensed solve whose factorisation breaks down continues on
@@ -78,7 +81,7 @@ def solve_mpc(p, ctx=None, tol=None, max_iter=None, fp32=False, riccati=False, g
     iters = np.zeros(batch, np.int32)
     status = np.zeros(batch, np.int32)
     out = L.cmpc_mpc_out(L.dptr(z), L.dptr(kkt), L.iptr(iters), L.iptr(status))
-    o = L.opts(tol or (FP32_TOL if fp32 else None), max_iter, _flags(fp32, riccati, generic, rescue), stamps)
+    o = L.opts(tol or (FP32_TOL if fp32 else None), max_iter, _flags(fp32, riccati, generic, rescue, lane), stamps)
     ctx.check(ctx.lib.cmpc_solve_mpc_batch(ctx.h, ct.byref(_dims(p, batch)), ct.byref(w), ct.byref(data),
                                            ct.byref(out), ct.byref(o)))
     del keep, arrs
@@ -99,7 +102,8 @@ def _tptr(t):
     raise TypeError(f"unsupported dtype {t.dtype}")
 
 
-def solve_mpc_dev(shared, dev, out, ctx=None, tol=None, max_iter=None, stream=None, fp32=False, riccati=False):
+def solve_mpc_dev(shared, dev, out, ctx=None, tol=None, max_iter=None, stream=None, fp32=False, riccati=False,
+                  lane=False):
     """Device-resident batch solve.  ``shared``: dict with dims + shared weights (host);
     ``dev``: dict of CUDA float64 tensors (PER_AGENT keys); ``out``: dict with
     'z' (float64) and optional 'kkt' (float64), 'iters', 'status' (int32) tensors.
@@ -112,7 +116,7 @@ def solve_mpc_dev(shared, dev, out, ctx=None, tol=None, max_iter=None, stream=No
     data = L.cmpc_mpc_data(*[_tptr(dev[k]) for k in PER_AGENT])
     o_ = L.cmpc_mpc_out(_tptr(out["z"]), _tptr(out.get("kkt")), _tptr(out.get("iters")), _tptr(out.get("status")))
     s = stream if stream is not None else torch.cuda.current_stream(dev["A"].device)
-    o = L.opts(tol or (FP32_TOL if fp32 else None), max_iter, _flags(fp32, riccati))
+    o = L.opts(tol or (FP32_TOL if fp32 else None), max_iter, _flags(fp32, riccati, lane=lane))
     ctx.check(ctx.lib.cmpc_solve_mpc_batch_dev(ctx.h, ct.byref(_dims(shared, batch)), ct.byref(w),
                                                ct.byref(data), ct.byref(o_), ct.byref(o),
                                                ct.c_void_p(s.cuda_stream)))

@@ -27,6 +27,7 @@ struct MpcConst {
     int rescue;   // 1: CMPC_FLAG_RESCUE on a condensed solve (Riccati re-solve of broken-down agents)
     int lpv;      // 1: data made by lpv_build.hip with Q diagonal (the v3 kernel's LS layout applies)
     int finish;   // 1: CMPC_FLAG_FINISH (rescue also continues breakdowns at the rounding floor)
+    int lane;     // lane-per-agent kernel (mpc_lane.hip): 1 fp64 (CMPC_FLAG_LANE), 2 mixed fp32 (CMPC_FLAG_FP32)
     unsigned long long ws_stride;  // doubles of MpcPtrs::ws per agent (set by mpc_launch; 0: no scratch)
     double tol;
     double qs_max;  // max(1, 2*max(Qs)) — slack residual scale
@@ -140,8 +141,15 @@ __host__ __device__ inline bool hand_over(int stop, double best_m, const MpcCons
 size_t mpc_riccati_lds_bytes(const MpcConst& c);
 size_t mpc_riccati_ws_doubles(const MpcConst& c);
 hipError_t mpc_riccati_launch(const MpcConst& c, const MpcPtrs& p, int batch, hipStream_t s);
+// Lane-per-agent stage-wise kernel (mpc_lane.hip): the dimension sets it is instantiated for.
+bool mpc_lane_supported(const MpcConst& c);
+size_t mpc_lane_ws_doubles(const MpcConst& c);
+hipError_t mpc_lane_launch(const MpcConst& c, const MpcPtrs& p, int batch, hipStream_t s);
 // Device scratch (doubles per agent) the solver chosen for c needs in MpcPtrs::ws (0: none).
-inline size_t mpc_ws_doubles(const MpcConst& c) { return (c.riccati || c.rescue) ? mpc_riccati_ws_doubles(c) : 0; }
+inline size_t mpc_ws_doubles(const MpcConst& c) {
+    if (c.lane) return mpc_lane_ws_doubles(c);
+    return (c.riccati || c.rescue) ? mpc_riccati_ws_doubles(c) : 0;
+}
 
 // Fills the derived fields of MpcConst; returns CMPC_OK or an error code with msg.
 int mpc_prepare(const cmpc_mpc_dims* d, const cmpc_mpc_weights* w, const cmpc_opts* o,

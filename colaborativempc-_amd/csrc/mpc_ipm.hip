@@ -681,11 +681,22 @@ int mpc_prepare(const cmpc_mpc_dims* d, const cmpc_mpc_weights* wt, const cmpc_o
         return CMPC_ERR_ARG;
     }
     const bool fp32 = o && (o->flags & CMPC_FLAG_FP32);
-    if (fp32 && d->N * d->nu > CMPC_MAX_NCOND_WG) {
+    const bool lane_req = o && (o->flags & CMPC_FLAG_LANE);
+    *c = MpcConst{};
+    c->nx = d->nx;
+    c->nu = d->nu;
+    c->mc = d->mc;
+    c->ns = d->ns;
+    // the lane-per-agent kernel: CMPC_FLAG_LANE (fp64), or CMPC_FLAG_FP32 where it is instantiated
+    const bool lane_ok = mpc_lane_supported(*c);
+    if (lane_req && !lane_ok) {
+        *msg = "CMPC_FLAG_LANE: no lane-per-agent kernel for these dimensions (nx,nu,mc,ns = 6,3,6,3 or 4,2,6,3)";
+        return CMPC_ERR_UNSUPPORTED;
+    }
+    if (fp32 && !lane_ok && d->N * d->nu > CMPC_MAX_NCOND_WG) {
         *msg = "N*nu > 256: exceeds the fp32 workgroup-per-agent solver";
         return CMPC_ERR_UNSUPPORTED;
     }
-    *c = MpcConst{};
     c->nx = d->nx;
     c->nu = d->nu;
     c->N = d->N;
@@ -699,8 +710,9 @@ int mpc_prepare(const cmpc_mpc_dims* d, const cmpc_mpc_weights* wt, const cmpc_o
     c->ldk = (c->n & 1) ? c->n : c->n + 1;
     c->tol = (o && o->tol > 0) ? o->tol : 1e-9;
     c->max_iter = (o && o->max_iter > 0) ? o->max_iter : 60;
-    c->wg = fp32 ? 2 : 0;
-    c->riccati = (!fp32 && (c->n > CMPC_MAX_NCOND || (o && (o->flags & CMPC_FLAG_RICCATI)))) ? 1 : 0;
+    c->lane = (fp32 && lane_ok) ? 2 : (lane_req ? 1 : 0);
+    c->wg = (fp32 && !c->lane) ? 2 : 0;
+    c->riccati = (!fp32 && !c->lane && (c->n > CMPC_MAX_NCOND || (o && (o->flags & CMPC_FLAG_RICCATI)))) ? 1 : 0;
     double qs = 1.0;
     for (int i = 0; i < d->nx * d->nx; ++i) c->Q[i] = wt->Q[i];
     for (int i = 0; i < d->nu * d->nu; ++i) {
@@ -725,7 +737,8 @@ int mpc_prepare(const cmpc_mpc_dims* d, const cmpc_mpc_weights* wt, const cmpc_o
         return CMPC_ERR_UNSUPPORTED;
     }
     // rescue pass (CMPC_FLAG_RESCUE): only for condensed fp64 solves whose rows fit the Riccati kernel
-    c->rescue = (!fp32 && !c->riccati && (o && (o->flags & CMPC_FLAG_RESCUE)) && mpc_riccati_lds_bytes(*c) <= kMaxLdsBytes)
+    c->rescue = (!fp32 && !c->lane && !c->riccati && (o && (o->flags & CMPC_FLAG_RESCUE)) &&
+                 mpc_riccati_lds_bytes(*c) <= kMaxLdsBytes)
                     ? 1 : 0;
     c->finish = (c->rescue && (o->flags & CMPC_FLAG_FINISH)) ? 1 : 0;
     for (int i = 0; i < d->nu; ++i) {
@@ -757,6 +770,7 @@ hipError_t mpc_launch(const MpcConst& c_in, const MpcPtrs& p, int batch, hipStre
     if (batch == 0) return hipSuccess;
     MpcConst c = c_in;
     c.ws_stride = p.ws ? mpc_ws_doubles(c) : 0;
+    if (c.lane) return mpc_lane_launch(c, p, batch, s);
     if (c.wg) return mpc_wg_launch(c, p, batch, s, c.wg == 2);
     if (c.riccati) return mpc_riccati_launch(c, p, batch, s);
     hipError_t e;

@@ -1,0 +1,102 @@
+// Lane-per-agent stage-wise interior-point solver: one LANE of a wavefront owns one agent, so a
+// wavefront advances 64 agents at once with no cross-lane traffic at all — the layout for large
+// batches of long-horizon agents (BASELINE cfg5: 8192 agents per GPU, N = 50, nx = 6, nu = 3),
+// where the one-wave-per-agent Riccati kernel (mpc_riccati.hip) leaves most lanes idle in every
+// serial step of the stage recursion.
+//
+// Method: the SAME Mehrotra predictor-corrector as every other solver of libcmpc (internal.h:
+// residuals, scaling, merit, safeguards, termination; oracle/cmpc_oracle.c restates it), with the
+// Newton system solved stage-wise by the Riccati recursion of mpc_riccati.hip on the augmented
+// state y_k = [dX_k; dU_{k-1}] (oracle ric_factor / ric_solve, standard form).  The QP is the one
+// PlannerLPV assembles (planner/lib/plan_lib/distributedPlanner/LPV_Planner.py:279-475).
+//
+// Sweeps.  Everything an iteration needs is produced by four passes over the horizon, each stage
+// read once per pass straight from the caller's agent-major inputs:
+//   S1 backward: the step of the previous iteration applied (lazily), residual adjoints (gradient
+//      scale, dual residual), primal / slack residuals, complementarity, the Riccati factorisation
+//      and the predictor's backward solve;
+//   S2 forward:  predictor feedback solve, predictor row steps (stored), the affine step and
+//      mu_aff (as a quadratic in the step length);
+//   S3 backward: corrector right-hand side and backward solve (same gains);
+//   S4 forward:  corrector feedback solve, the direction (stored), the step bound;
+// then one pass over the rows for the neighbourhood backtracking.  Per-agent scratch is lane-
+// interleaved (element i of agent b at ws[i * batch + b]) so every access of a wavefront is one
+// coalesced 512-byte (fp64) line set.
+//
+// Precision (template MIXED).  MIXED = false: everything fp64.  MIXED = true (CMPC_FLAG_FP32,
+// BASELINE cfg5's "fp32 path with tolerance check vs fp64 reference"): the Riccati factorisation,
+// its gains and both Newton solves' recursions run in fp32; iterates, residuals, the row algebra
+// and the state recursion of the direction stay fp64, so the iterate never drifts from the
+// simulation of its inputs.  An agent whose fp32 factorisation breaks down, or that makes no
+// progress for kF32Stall iterations, continues in fp64 (per lane: the wave runs both paths only
+// while its lanes disagree).  tools/f32_lab.py measured the scheme on the C restatement
+// (oracle RIC_F32): 99.3 % CMPC_SOLVED at tol 1e-6 on 2048 cfg5 agents, z within 2e-4 of the
+// fp64 double-double solve, ~12 % of agents finishing in fp64 (two iterations on average).
+#include "lane_body.h"
+
+namespace cmpc {
+
+template <int NX, int NU, int MC, int NS, bool MIXED>
+__global__ __launch_bounds__(kWave) void mpc_lane_kernel(const MpcConst c, const MpcPtrs P, int batch) {
+    const int b = blockIdx.x * kWave + threadIdx.x;
+    if (b < batch) lane_agent<NX, NU, MC, NS, MIXED>(c, P, batch, b);
+}
+
+size_t mpc_lane_ws_doubles(const MpcConst& c) { return lane_layout(c).total; }
+
+// dst[e * batch + b] = src[b * T + e]: agent-major inputs -> lane-interleaved copy, through a
+// 64 x 64 LDS tile so both the reads (along e) and the writes (along b) are coalesced
+__global__ __launch_bounds__(256) void lane_pack_kernel(const double* __restrict__ src, double* __restrict__ dst,
+                                                        int batch, int T) {
+    __shared__ double tile[64][65];
+    const int e0 = blockIdx.x * 64, b0 = blockIdx.y * 64, tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+    for (int r = ty; r < 64; r += 4) {
+        const int b = b0 + r, e = e0 + tx;
+        if (b < batch && e < T) tile[r][tx] = src[(size_t)b * T + e];
+    }
+    __syncthreads();
+    for (int r = ty; r < 64; r += 4) {
+        const int e = e0 + r, b = b0 + tx;
+        if (b < batch && e < T) dst[(size_t)e * batch + b] = tile[tx][r];
+    }
+}
+
+static hipError_t lane_pack(const double* src, double* dst, int batch, int T, hipStream_t s) {
+    if (T <= 0) return hipSuccess;
+    hipLaunchKernelGGL(lane_pack_kernel, dim3((T + 63) / 64, (batch + 63) / 64), dim3(256), 0, s, src, dst, batch, T);
+    return hipGetLastError();
+}
+
+template <int NX, int NU, int MC, int NS>
+static bool lane_try(const MpcConst& c, const MpcPtrs& p, int batch, hipStream_t s, hipError_t* e) {
+    if (c.nx != NX || c.nu != NU || c.mc != MC || c.ns != NS) return false;
+    const dim3 grid((batch + kWave - 1) / kWave);
+    if (c.lane == 2) hipLaunchKernelGGL((mpc_lane_kernel<NX, NU, MC, NS, true>), grid, dim3(kWave), 0, s, c, p, batch);
+    else hipLaunchKernelGGL((mpc_lane_kernel<NX, NU, MC, NS, false>), grid, dim3(kWave), 0, s, c, p, batch);
+    *e = hipGetLastError();
+    return true;
+}
+
+bool mpc_lane_supported(const MpcConst& c) {
+    return (c.nx == 6 && c.nu == 3 && c.mc == 6 && c.ns == 3) || (c.nx == 4 && c.nu == 2 && c.mc == 6 && c.ns == 3);
+}
+
+hipError_t mpc_lane_launch(const MpcConst& c, const MpcPtrs& p, int batch, hipStream_t s) {
+    if (batch == 0) return hipSuccess;
+    if (!p.ws) return hipErrorInvalidValue;
+    const LaneLayout L = lane_layout(c);
+    const size_t S = (size_t)batch;
+    const int N = c.N, nx = c.nx, nu = c.nu, mc = c.mc;
+    hipError_t e;
+    if ((e = lane_pack(p.A, p.ws + L.iA * S, batch, N * nx * nx, s)) != hipSuccess) return e;
+    if ((e = lane_pack(p.B, p.ws + L.iB * S, batch, N * nx * nu, s)) != hipSuccess) return e;
+    if ((e = lane_pack(p.C, p.ws + L.iC * S, batch, N * mc * nx, s)) != hipSuccess) return e;
+    if ((e = lane_pack(p.h, p.ws + L.ih * S, batch, N * mc, s)) != hipSuccess) return e;
+    if ((e = lane_pack(p.p, p.ws + L.ip * S, batch, (N + 1) * nx, s)) != hipSuccess) return e;
+    e = hipErrorInvalidValue;
+    if (lane_try<6, 3, 6, 3>(c, p, batch, s, &e)) return e;  // BASELINE cfg5 (3-D double integrator, nb = 2)
+    if (lane_try<4, 2, 6, 3>(c, p, batch, s, &e)) return e;  // cfg1-4 shape (2-D double integrator, nb = 2)
+    return hipErrorInvalidValue;
+}
+
+}  // namespace cmpc

@@ -71,8 +71,11 @@ extern "C" {
 typedef struct cmpc_ctx cmpc_ctx;
 
 #define CMPC_FLAG_GENERIC 1  /* force the generic (runtime-dimension) kernel */
-#define CMPC_FLAG_FP32 8     /* fp32 workgroup-per-agent solver (long horizons, BASELINE cfg5);
-                                opts.tol should then be ~1e-5 */
+#define CMPC_FLAG_FP32 8     /* fp32 path (BASELINE cfg5): where the lane-per-agent kernel is instantiated
+                                (nx,nu,mc,ns = 6,3,6,3 or 4,2,6,3) its Riccati factorisation and Newton
+                                recursions run in fp32 with fp64 iterates / residuals and a per-agent fp64
+                                finish (opts.tol ~1e-6); elsewhere the fp32 workgroup-per-agent condensed
+                                solver (N*nu <= 256, opts.tol ~1e-5) */
 #define CMPC_FLAG_RICCATI 16 /* force the stage-wise Riccati solver (fp64; the default when N*nu > 64) */
 #define CMPC_FLAG_RESCUE 32 /* condensed solves (fp64): an agent whose factorisation breaks down short of
                                1e3 tol (status CMPC_UNSOLVED) continues from its last iterate on the
@@ -80,7 +83,11 @@ typedef struct cmpc_ctx cmpc_ctx;
                                launch; a third launch restarts cold the rare one that fails again */
 #define CMPC_FLAG_FINISH 64 /* with CMPC_FLAG_RESCUE: a breakdown whose best iterate already meets 1e3 tol
                                (status 2) is continued too, to full tolerance (slower; fewer status 2) */
-#define CMPC_FLAG_ALL (CMPC_FLAG_GENERIC | CMPC_FLAG_FP32 | CMPC_FLAG_RICCATI | CMPC_FLAG_RESCUE | CMPC_FLAG_FINISH)  /* other bits: CMPC_ERR_ARG */
+#define CMPC_FLAG_LANE 128  /* lane-per-agent stage-wise solver in fp64 (one lane per agent, 64 agents per
+                               wavefront: large batches of long horizons); CMPC_ERR_UNSUPPORTED for
+                               dimensions it is not instantiated for (see CMPC_FLAG_FP32) */
+#define CMPC_FLAG_ALL (CMPC_FLAG_GENERIC | CMPC_FLAG_FP32 | CMPC_FLAG_RICCATI | CMPC_FLAG_RESCUE | CMPC_FLAG_FINISH | \
+                       CMPC_FLAG_LANE)  /* other bits: CMPC_ERR_ARG */
 
 typedef struct {
     double tol;    /* relative stationarity/feasibility tolerance (complementarity: 1e-4*tol); <= 0 selects 1e-9 */

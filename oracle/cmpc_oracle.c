@@ -115,6 +115,9 @@ long cmpc_gz_solves = 0; /* lab: corrector solves performed */
 #ifndef CREF_TH
 #define CREF_TH 1e10
 #endif
+#ifndef MU_FACTOR
+#define MU_FACTOR 1e4   /* merit max(res, MU_FACTOR mu); lab: the fp32 kernels use 10 */
+#endif
 #ifndef T0_FLOOR
 #define T0_FLOOR 0.5    /* starting slacks t_r = max(w_r - g_r, T0_FLOOR) (internal.h kT0Floor) */
 #endif
@@ -530,6 +533,213 @@ static void ric_solve(const shared_t* S, const agent_t* a, const double* F, cons
     }
 }
 
+
+#ifdef RIC_F32
+/* lab: the Riccati factorisation and Newton solves in single precision (gains, cost-to-go and every
+   operation of ric_factor / ric_solve in float), iterates and residuals in double — the mixed
+   scheme of an fp32 stage-wise kernel (tools/f32_lab.py) */
+static int ric_factor_f32(const shared_t* S, const agent_t* a, const double* th, const double* Dsig, double* F) {
+    const int nx = S->nx, nu = S->nu, N = S->N, na = nx + nu, ms = N * S->mc, sF = nu * na + nu * nu;
+    float P[NA_MAX * NA_MAX], Pn[NA_MAX * NA_MAX], H[NU_MAX * NU_MAX], Hy[NU_MAX * NA_MAX];
+    float Lf[NU_MAX * NU_MAX], Hi[NU_MAX * NU_MAX], Ak[NA_MAX * NA_MAX], Bk[NA_MAX * NU_MAX], PB[NA_MAX * NU_MAX];
+    double W[NA_MAX * NA_MAX];
+    memset(P, 0, sizeof P);
+    stage_w(S, a, th, Dsig, N - 1, W);
+    for (int i = 0; i < nx; ++i) for (int j = 0; j < nx; ++j) P[i * na + j] = (float)W[i * nx + j];
+    for (int k = N - 1; k >= 0; --k) {
+        for (int i = 0; i < nx * nx; ++i) Ak[i] = (float)a->A[(size_t)k * nx * nx + i];
+        for (int i = 0; i < nx * nu; ++i) Bk[i] = (float)a->B[(size_t)k * nx * nu + i];
+        for (int i = 0; i < na; ++i)
+            for (int c = 0; c < nu; ++c) {
+                float v = P[i * na + nx + c];
+                for (int s2 = 0; s2 < nx; ++s2) v += P[i * na + s2] * Bk[s2 * nu + c];
+                PB[i * nu + c] = v;
+            }
+        for (int c = 0; c < nu; ++c)
+            for (int e = 0; e < nu; ++e) {
+                float v = (float)(2.0 * S->R[c * nu + e] + 2.0 * S->dR[c * nu + e]) + PB[(nx + c) * nu + e];
+                for (int s2 = 0; s2 < nx; ++s2) v += Bk[s2 * nu + c] * PB[s2 * nu + e];
+                if (c == e) { int r = ms + 2 * (k * nu + c); v += (float)(th[r] + th[r + 1]); }
+                H[c * nu + e] = v;
+            }
+        for (int c = 0; c < nu; ++c)
+            for (int j = 0; j < na; ++j) {
+                float v = 0.0f;
+                if (j < nx)
+                    for (int s2 = 0; s2 < nx; ++s2) v += PB[s2 * nu + c] * Ak[s2 * nx + j];
+                else
+                    v = (float)(-2.0 * S->dR[c * nu + (j - nx)]);
+                Hy[c * na + j] = v;
+            }
+        for (int j = 0; j < nu; ++j) {
+            float d = H[j * nu + j];
+            for (int q = 0; q < j; ++q) d -= Lf[j * nu + q] * Lf[j * nu + q];
+            if (!(d > 0.0f)) return -1;
+            d = sqrtf(d);
+            Lf[j * nu + j] = d;
+            for (int i = j + 1; i < nu; ++i) {
+                float v = H[i * nu + j];
+                for (int q = 0; q < j; ++q) v -= Lf[i * nu + q] * Lf[j * nu + q];
+                Lf[i * nu + j] = v / d;
+            }
+        }
+        for (int c = 0; c < nu; ++c) {
+            float e[NU_MAX];
+            for (int i = 0; i < nu; ++i) e[i] = (i == c) ? 1.0f : 0.0f;
+            for (int i = 0; i < nu; ++i) {
+                float v = e[i];
+                for (int q = 0; q < i; ++q) v -= Lf[i * nu + q] * e[q];
+                e[i] = v / Lf[i * nu + i];
+            }
+            for (int i = nu - 1; i >= 0; --i) {
+                float v = e[i];
+                for (int q = i + 1; q < nu; ++q) v -= Lf[q * nu + i] * e[q];
+                e[i] = v / Lf[i * nu + i];
+            }
+            for (int i = 0; i < nu; ++i) Hi[i * nu + c] = e[i];
+        }
+        double* Fk = F + (size_t)k * sF;
+        float Kk[NU_MAX * NA_MAX];
+        for (int c = 0; c < nu; ++c)
+            for (int j = 0; j < na; ++j) {
+                float v = 0.0f;
+                for (int e = 0; e < nu; ++e) v -= Hi[c * nu + e] * Hy[e * na + j];
+                Kk[c * na + j] = v;
+                Fk[c * na + j] = v;
+            }
+        for (int c = 0; c < nu * nu; ++c) Fk[nu * na + c] = Hi[c];
+        if (k == 0) break;
+        stage_w(S, a, th, Dsig, k - 1, W);
+#ifdef RIC_F32_JOSEPH
+        {   /* Joseph form in float: P_k = blkdiag(W_k, 0) + K'(2R + th)K + (K - E)'2dR(K - E) + Acl'P Acl */
+            float Acl[NA_MAX * NA_MAX], T[NA_MAX * NA_MAX];
+            for (int i = 0; i < na; ++i)
+                for (int j = 0; j < na; ++j) {
+                    float v;
+                    if (i < nx) {
+                        v = (j < nx) ? Ak[i * nx + j] : 0.0f;
+                        for (int c = 0; c < nu; ++c) v += Bk[i * nu + c] * Kk[c * na + j];
+                    } else {
+                        v = Kk[(i - nx) * na + j];
+                    }
+                    Acl[i * na + j] = v;
+                }
+            for (int i = 0; i < na; ++i)
+                for (int j = 0; j < na; ++j) {
+                    float v = 0.0f;
+                    for (int s2 = 0; s2 < na; ++s2) v += P[i * na + s2] * Acl[s2 * na + j];
+                    T[i * na + j] = v;
+                }
+            for (int i = 0; i < na; ++i)
+                for (int j = 0; j <= i; ++j) {
+                    float v = (i < nx && j < nx) ? (float)W[i * nx + j] : 0.0f;
+                    for (int s2 = 0; s2 < na; ++s2) v += Acl[s2 * na + i] * T[s2 * na + j];
+                    for (int c = 0; c < nu; ++c) {
+                        const float kc_i = Kk[c * na + i], kc_j = Kk[c * na + j];
+                        float ru = 0.0f;
+                        for (int e = 0; e < nu; ++e) {
+                            const float ke_j = Kk[e * na + j];
+                            ru += (float)(2.0 * S->R[c * nu + e]) * ke_j;
+                            const float d_i = kc_i - ((i >= nx && i - nx == c) ? 1.0f : 0.0f);
+                            const float d_j = ke_j - ((j >= nx && j - nx == e) ? 1.0f : 0.0f);
+                            v += d_i * (float)(2.0 * S->dR[c * nu + e]) * d_j;
+                        }
+                        const int r = ms + 2 * (k * nu + c);
+                        v += kc_i * (ru + (float)(th[r] + th[r + 1]) * kc_j);
+                    }
+                    Pn[i * na + j] = v;
+                    Pn[j * na + i] = v;
+                }
+            memcpy(P, Pn, sizeof(float) * na * na);
+            continue;
+        }
+#endif
+        for (int i = 0; i < na; ++i)
+            for (int j = 0; j <= i; ++j) {
+                float v;
+                if (i < nx) {
+                    v = (float)W[i * nx + j];
+                    for (int s2 = 0; s2 < nx; ++s2) {
+                        float pa = 0.0f;
+                        for (int t2 = 0; t2 < nx; ++t2) pa += P[s2 * na + t2] * Ak[t2 * nx + j];
+                        v += Ak[s2 * nx + i] * pa;
+                    }
+                } else {
+                    v = (j >= nx) ? (float)(2.0 * S->dR[(i - nx) * nu + (j - nx)]) : 0.0f;
+                }
+                for (int c = 0; c < nu; ++c) v += Hy[c * na + i] * Kk[c * na + j];
+                Pn[i * na + j] = v;
+                Pn[j * na + i] = v;
+            }
+        memcpy(P, Pn, sizeof(float) * na * na);
+    }
+    return 0;
+}
+
+static void ric_solve_f32(const shared_t* S, const agent_t* a, const double* F, const double* rhs, double* dU, double* dX) {
+    const int nx = S->nx, nu = S->nu, N = S->N, na = nx + nu, sF = nu * na + nu * nu;
+    float p[NA_MAX], pn[NA_MAX], g[NA_MAX];
+    float* dUf = (float*)malloc(sizeof(float) * (size_t)N * nu);
+    float* dXf = (float*)malloc(sizeof(float) * (size_t)(N + 1) * nx);
+    memset(p, 0, sizeof p);
+    for (int k = N - 1; k >= 0; --k) {
+        const double* Ak = a->A + (size_t)k * nx * nx;
+        const double* Bk = a->B + (size_t)k * nx * nu;
+        const double* Kg = F + (size_t)k * sF;
+        const double* Hg = Kg + nu * na;
+        for (int c = 0; c < nu; ++c) {
+            float v = p[nx + c] - (float)rhs[k * nu + c];
+            for (int s2 = 0; s2 < nx; ++s2) v += (float)Bk[s2 * nu + c] * p[s2];
+            g[c] = v;
+        }
+        for (int c = 0; c < nu; ++c) {
+            float v = 0.0f;
+            for (int e = 0; e < nu; ++e) v -= (float)Hg[c * nu + e] * g[e];
+            dUf[k * nu + c] = v;
+        }
+        for (int j = 0; j < na; ++j) {
+            float v = 0.0f;
+            if (j < nx)
+                for (int s2 = 0; s2 < nx; ++s2) v += (float)Ak[s2 * nx + j] * p[s2];
+            for (int c = 0; c < nu; ++c) v += (float)Kg[c * na + j] * g[c];
+            pn[j] = v;
+        }
+        memcpy(p, pn, sizeof(float) * na);
+    }
+    /* forward: the feedback in float, the state recursion dX_{k+1} = A dX_k + B dU_k in double (the
+       iterate's X stays the simulation of its U) */
+    for (int s2 = 0; s2 < nx; ++s2) dX[s2] = 0.0;
+    for (int k = 0; k < N; ++k) {
+        const double* Ak = a->A + (size_t)k * nx * nx;
+        const double* Bk = a->B + (size_t)k * nx * nu;
+        const double* Kg = F + (size_t)k * sF;
+        for (int c = 0; c < nu; ++c) {
+            float v = dUf[k * nu + c];
+            for (int j = 0; j < nx; ++j) v += (float)Kg[c * na + j] * (float)dX[k * nx + j];
+            if (k > 0)
+                for (int e = 0; e < nu; ++e) v += (float)Kg[c * na + nx + e] * dUf[(k - 1) * nu + e];
+            dUf[k * nu + c] = v;
+            dU[k * nu + c] = v;
+        }
+        for (int s2 = 0; s2 < nx; ++s2) {
+            double v = 0.0;
+            for (int t2 = 0; t2 < nx; ++t2) v += Ak[s2 * nx + t2] * dX[k * nx + t2];
+            for (int c = 0; c < nu; ++c) v += Bk[s2 * nu + c] * dU[k * nu + c];
+            dX[(k + 1) * nx + s2] = v;
+        }
+    }
+    (void)dXf;
+    free(dUf);
+    free(dXf);
+}
+long cmpc_f32_iters = 0, cmpc_f64_iters = 0, cmpc_f64_agents = 0; /* lab counters */
+#ifndef F32_STALL
+#define F32_STALL 2      /* lab: fp32 iterations without a new best before the agent switches to fp64 */
+#endif
+#ifndef F32_SWITCH_M
+#define F32_SWITCH_M 0.0 /* lab: best merit below which the agent switches to fp64 (0: off) */
+#endif
+#endif
 
 /* y = K v for the condensed Newton matrix K = sum_k Gamma_k'W_k Gamma_k + 2R + 2D'dR D + diag(th_u),
    matrix-free through the stage recursions (dX = Gamma v, then the adjoint) */
@@ -1053,6 +1263,9 @@ static int solve_one(const shared_t* S, const agent_t* a, double tol, int max_it
     int it;
     double kkt = INFINITY;
     double alpha_prev = 1.0; /* step of the previous iteration (kShortStep rule) */
+#ifdef RIC_F32
+    int f32_on = 1;          /* lab: this agent still factors in fp32 */
+#endif
 #ifdef GONDZIO
     /* lab: Gondzio centrality correctors (up to GONDZIO per iteration) on the Mehrotra direction */
     long gz_used = 0;
@@ -1127,7 +1340,7 @@ static int solve_one(const shared_t* S, const agent_t* a, double tol, int max_it
            (degenerate rows sit at t, lambda ~ sqrt(mu): primal accuracy needs tiny mu) */
         double res = nmax(nmax(nrd / gscale, nrs / qs_max), nrp / scale_p);
         kkt = nmax(res, mu);
-        const double merit = nmax(res, 1e4 * mu);
+        const double merit = nmax(res, MU_FACTOR * mu);
         if (!isfinite(merit)) { stop = 4; break; }
         if (merit < best_m) {
             best_m = merit;
@@ -1183,6 +1396,29 @@ static int solve_one(const shared_t* S, const agent_t* a, double tol, int max_it
 #ifdef RIC_QUAD
             if (ric_factor_q(S, a, wk->th, wk->Dsig, wk->F)) { stop = 2; break; }
 #else
+#ifdef RIC_F32
+            if (f32_on && (it - best_it >= F32_STALL || best_m < F32_SWITCH_M)) {
+                f32_on = 0;
+#pragma omp atomic
+                cmpc_f64_agents += 1;
+            }
+            if (f32_on) {
+                if (ric_factor_f32(S, a, wk->th, wk->Dsig, wk->F)) {
+                    f32_on = 0;
+#pragma omp atomic
+                    cmpc_f64_agents += 1;
+                }
+            }
+            {
+                const int was = f32_on;
+#pragma omp atomic
+                cmpc_f32_iters += f32_on;
+#pragma omp atomic
+                cmpc_f64_iters += !f32_on;
+                (void)was;
+            }
+            if (!f32_on)
+#endif
             if (hp ? ric_factor_dd(S, a, wk->th, wk->Dsig, wk->F) : ric_factor(S, a, wk->th, wk->Dsig, wk->F)) { stop = 2; break; }
 #endif
         }
@@ -1370,6 +1606,9 @@ static int solve_one(const shared_t* S, const agent_t* a, double tol, int max_it
                 wk->rhs[c] = -wk->rd[c] - (wk->rhs[c] + wk->rt[r] - wk->rt[r + 1]);
             }
             if (S->newton) {
+#ifdef RIC_F32
+                if (f32_on) ric_solve_f32(S, a, wk->F, wk->rhs, wk->dU, wk->dX); else
+#endif
                 ric_solve(S, a, wk->F, wk->rhs, wk->dU, wk->dX);
                 /* iterative refinement: dU += M^-1 (rhs - K dU) */
                 const int nref = hp ? S->refine_dd : S->refine;
@@ -1387,6 +1626,9 @@ static int solve_one(const shared_t* S, const agent_t* a, double tol, int max_it
                         kmul(S, a, wk->th, wk->Dsig, wk->dU, kv, cx, ybar, wk->psi, wk->tmp);
                         for (int c = 0; c < n; ++c) kv[c] = wk->rhs[c] - kv[c];
                     }
+#endif
+#ifdef RIC_F32
+                    if (f32_on) ric_solve_f32(S, a, wk->F, kv, cr, cx); else
 #endif
                     ric_solve(S, a, wk->F, kv, cr, cx);
                     double cn = 0.0, un = 0.0;
@@ -1478,6 +1720,12 @@ static int solve_one(const shared_t* S, const agent_t* a, double tol, int max_it
 #endif
                 fwd_sim(S, a, NULL, wk->dU, wk->dX);
             }
+#ifdef ORACLE_TRACE
+            for (int k = 0; k < N; ++k)
+                if (k < 2 || k == N - 1)
+                    fprintf(stderr, "  pass %d k %d du %.10e %.10e %.10e\n", pass, k, wk->dU[k * nu], wk->dU[k * nu + 1 % nu],
+                            wk->dU[k * nu + 2 % nu]);
+#endif
             for (int r = 0; r < m; ++r) {
                 double g; ROWVAL(wk->dX, wk->dU, (const double*)NULL, r, g);
                 wk->GdU[r] = g;
