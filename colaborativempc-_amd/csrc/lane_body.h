@@ -14,12 +14,51 @@ namespace {
 
 constexpr int kF32Stall = 2;  // fp32 iterations without a new best iterate before an agent goes fp64
 
-// lane-interleaved view: element i of this lane's agent at p[i * s]
+// Lane-interleaved view: element i of this lane's agent at byte (region + i) * batch * sizeof(T) +
+// b * sizeof(T) of the scratch.  On the device every access is a raw buffer load / store whose
+// element offset is a wave-uniform SGPR and whose lane offset is one VGPR for all arrays (plain
+// 64-bit addresses per element made the compiler precompute and spill hundreds of them); on the
+// host (tools/lane_cpu.cpp) a pointer.  Accesses go through a small proxy (read / assign).
 template <class T>
 struct LV {
+#if defined(__HIP_DEVICE_COMPILE__)
+    __amdgpu_buffer_rsrc_t r;
+    unsigned base, s, vo;  // region start (elements of T), batch stride, lane byte offset
+    __device__ __forceinline__ T ld(int i) const {
+        const int so = (int)((base + (unsigned)i) * s * (unsigned)sizeof(T));
+        if constexpr (sizeof(T) == 8)
+            return __builtin_bit_cast(T, __builtin_amdgcn_raw_buffer_load_b64(r, (int)vo, so, 0));
+        else
+            return __builtin_bit_cast(T, __builtin_amdgcn_raw_buffer_load_b32(r, (int)vo, so, 0));
+    }
+    __device__ __forceinline__ void st(int i, T v) const {
+        const int so = (int)((base + (unsigned)i) * s * (unsigned)sizeof(T));
+        if constexpr (sizeof(T) == 8)
+            __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(__attribute__((ext_vector_type(2))) unsigned, v), r,
+                                                  (int)vo, so, 0);
+        else
+            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), r, (int)vo, so, 0);
+    }
+#else
     T* p;
     size_t s;
-    __host__ __device__ __forceinline__ T& operator[](int i) const { return p[(size_t)i * s]; }
+    T ld(int i) const { return p[(size_t)i * s]; }
+    void st(int i, T v) const { p[(size_t)i * s] = v; }
+#endif
+    struct Ref {
+        const LV* v;
+        int i;
+        __host__ __device__ __forceinline__ operator T() const { return v->ld(i); }
+        __host__ __device__ __forceinline__ const Ref& operator=(T x) const {
+            v->st(i, x);
+            return *this;
+        }
+        __host__ __device__ __forceinline__ const Ref& operator=(const Ref& o) const {
+            v->st(i, (T)o);
+            return *this;
+        }
+    };
+    __host__ __device__ __forceinline__ Ref operator[](int i) const { return Ref{this, i}; }
 };
 
 struct LaneLayout {
@@ -68,8 +107,39 @@ __host__ __device__ inline LaneLayout lane_layout(const MpcConst& c) {
 // NaN-propagating max (a NaN residual must never look converged)
 __host__ __device__ inline double lane_nmax(double a, double b) { return (a > b || a != a) ? a : b; }
 
+// scheduling fence between the phases of a stage (keeps the compiler from hoisting one phase's loads
+// into the previous phase, which multiplies the live registers); nothing on the host
+#if defined(__HIP_DEVICE_COMPILE__)
+#define LANE_PHASE() __builtin_amdgcn_sched_barrier(0)
+#else
+#define LANE_PHASE() ((void)0)
+#endif
+
 // packed lower-triangle index (i >= j) and its symmetric accessor
 __host__ __device__ constexpr int sy(int i, int j) { return i >= j ? i * (i + 1) / 2 + j : j * (j + 1) / 2 + i; }
+
+// Stage images.  Every sweep step reads its stage's data (inputs, iterate, direction, gains) from an
+// LDS image that the step before filled with buffer_load ... lds (no VGPRs, the load latency hidden
+// behind a whole step of arithmetic): two images, ping-pong.  A wavefront serves kLaneAP agents
+// (the other 32 lanes exit at once): an image row is one element for those agents, 256 bytes, and
+// one dwordx4 LDS load of 32 lanes fills two rows.  The map below (rows; runs start on even rows,
+// float runs on multiples of 4 float rows) is the union of what the sweeps fetch.
+constexpr int kLaneAP = 32;
+
+template <int NX, int NU, int MC, int NS>
+struct IMap {
+    static constexpr int SF = NU * (NX + NU) + NU * NU;
+    static constexpr int ev(int x) { return (x + 1) & ~1; }
+    static constexpr int A = 0, B = A + ev(NX * NX), C = B + ev(NX * NU), h = C + ev(MC * NX), p = h + ev(MC);
+    static constexpr int X = p + ev(NX), U = X + ev(NX), sig = U + ev(NU), tB = sig + ev(NS), lB = tB + ev(MC);
+    static constexpr int tI = lB + ev(MC), lI = tI + ev(2 * NU), dX = lI + ev(2 * NU), dsig = dX + ev(NX);
+    static constexpr int dtB = dsig + ev(NS), dlB = dtB + ev(MC), dU = dlB + ev(MC), dtI = dU + ev(NU);
+    static constexpr int dlI = dtI + ev(2 * NU), rd = dlI + ev(2 * NU), dUp = rd + ev(NU), aB = dUp + ev(NU);
+    static constexpr int alB = aB + ev(MC), aI = alB + ev(MC), alI = aI + ev(2 * NU), Fd = alI + ev(2 * NU);
+    static constexpr int rows = Fd + ev(SF);
+    static constexpr int frows = (SF + 3) & ~3;                     // fp32 gains
+    static constexpr int bytes = rows * kLaneAP * 8 + frows * kLaneAP * 4;  // one image
+};
 
 // Residual and factorisation accumulators of one S1 sweep.
 struct S1Out {
@@ -79,46 +149,77 @@ struct S1Out {
 
 }  // namespace
 
-// One agent's solve (lane b of the batch).  __host__ __device__: the kernel below runs it per lane,
-// and tools/lane_cpu.cpp runs the same code on the host to check it against the C restatement.
+// One agent's solve (lane j = b % kLaneAP of its wavefront).  __host__ __device__: the kernel runs it
+// per lane; tools/lane_cpu.cpp runs the same code on the host (images emulated per agent) to check it
+// against the C restatement.  `smem`: the two stage images of this wavefront (device).
 template <int NX, int NU, int MC, int NS, bool MIXED>
-__host__ __device__ inline void lane_agent(const MpcConst& c, const MpcPtrs& P, int batch, int b) {
-    constexpr int NA = NX + NU, SF = NU * NA + NU * NU;
+__host__ __device__ inline void lane_agent(const MpcConst& c, const MpcPtrs& P, int batch, int b, char* smem) {
+    using M = IMap<NX, NU, MC, NS>;
+    constexpr int NA = NX + NU, SF = M::SF;
     const int N = c.N, ms = c.ms, m = c.m;
     const LaneLayout L = lane_layout(c);
     const size_t S = (size_t)batch;
     double* ws = P.ws;
-    const LV<double> X{ws + L.X * S + b, S}, U{ws + L.U * S + b, S}, sig{ws + L.sig * S + b, S};
-    const LV<double> t{ws + L.t * S + b, S}, lam{ws + L.lam * S + b, S}, bU{ws + L.bU * S + b, S};
-    const LV<double> bsig{ws + L.bsig * S + b, S}, rd{ws + L.rd * S + b, S}, dUp{ws + L.dUp * S + b, S};
-    const LV<double> Fd{ws + L.Fd * S + b, S}, dta{ws + L.dta * S + b, S}, dla{ws + L.dla * S + b, S};
-    const LV<double> dU{ws + L.dU * S + b, S}, dX{ws + L.dX * S + b, S}, dsig{ws + L.dsig * S + b, S};
-    const LV<double> dt{ws + L.dt * S + b, S}, dl{ws + L.dl * S + b, S};
+    const int j = b % kLaneAP;  // lane within the wavefront's agents
+#if defined(__HIP_DEVICE_COMPILE__)
+    // one buffer resource over the launch's scratch (mpc_lane_launch keeps it below 2 GiB)
+    const __amdgpu_buffer_rsrc_t rs =
+        __builtin_amdgcn_make_buffer_rsrc(ws, 0, (int)(L.total * S * 8 < 0x7fffffffull ? L.total * S * 8 : 0x7fffffffull),
+                                          0x00020000);
+    const unsigned Su = (unsigned)S;
+    auto mk = [&](size_t region) { return LV<double>{rs, (unsigned)region, Su, (unsigned)b * 8u}; };
+    const LV<float> Ff{rs, (unsigned)(2 * L.Ff), Su, (unsigned)b * 4u};  // float elements from byte 8 * Ff * S
+    const unsigned b0 = (unsigned)(b - j);
+    // lane offsets of the image fills: 2 double rows (16 lanes x 16 B each) / 4 float rows per instruction
+    const int vo_d = (int)((((unsigned)j >> 4) * Su + b0 + 2u * ((unsigned)j & 15u)) * 8u);
+    const int vo_f = (int)((((unsigned)j >> 3) * Su + b0 + 4u * ((unsigned)j & 7u)) * 4u);
+    // image rows (double run of cnt rows from global element ge, float run from float element gf)
+    auto fd = [&](int buf, int row, size_t ge, int cnt) {
+        char* dst = smem + buf * M::bytes + row * (kLaneAP * 8);
+        for (int q = 0; q < cnt; q += 2)
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)(dst + q * (kLaneAP * 8)),
+                                                     16, vo_d, (int)((ge + q) * Su * 8u), 0, 0);
+    };
+    auto ff = [&](int buf, size_t gf, int cnt) {
+        char* dst = smem + buf * M::bytes + M::rows * (kLaneAP * 8);
+        for (int q = 0; q < cnt; q += 4)
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)(dst + q * (kLaneAP * 4)),
+                                                     16, vo_f, (int)((gf + q) * Su * 4u), 0, 0);
+    };
+    const double* imd0 = reinterpret_cast<const double*>(smem);
+    auto im = [&](int buf, int row) -> double { return imd0[buf * (M::bytes / 8) + row * kLaneAP + j]; };
+    auto imf = [&](int buf, int row) -> float {
+        return reinterpret_cast<const float*>(smem + buf * M::bytes + M::rows * (kLaneAP * 8))[row * kLaneAP + j];
+    };
+    // every image fill (and store) of this wavefront retired
+    auto img_wait = [&]() { __builtin_amdgcn_s_waitcnt(0x0F70); };
+#else
+    (void)smem;
+    auto mk = [&](size_t region) { return LV<double>{ws + region * S + b, S}; };
     const LV<float> Ff{reinterpret_cast<float*>(ws + L.Ff * S) + b, S};
-
-    // inputs in the lane-interleaved copy lane_pack made (coalesced across the wavefront)
-    const LV<double> gA{ws + L.iA * S + b, S}, gB{ws + L.iB * S + b, S}, gC{ws + L.iC * S + b, S};
-    const LV<double> gh{ws + L.ih * S + b, S}, gp{ws + L.ip * S + b, S};
+    double hd[2][M::rows];
+    float hf[2][M::frows];
+    auto fd = [&](int buf, int row, size_t ge, int cnt) {
+        for (int q = 0; q < cnt; ++q) hd[buf][row + q] = ws[(ge + q) * S + b];
+    };
+    auto ff = [&](int buf, size_t gf, int cnt) {
+        const float* f = reinterpret_cast<const float*>(ws);
+        for (int q = 0; q < cnt; ++q) hf[buf][q] = f[(gf + q) * S + b];
+    };
+    auto im = [&](int buf, int row) -> double { return hd[buf][row]; };
+    auto imf = [&](int buf, int row) -> float { return hf[buf][row]; };
+    auto img_wait = [&]() {};
+#endif
+    (void)j;
+    const LV<double> X = mk(L.X), U = mk(L.U), sig = mk(L.sig), t = mk(L.t), lam = mk(L.lam), bU = mk(L.bU);
+    const LV<double> bsig = mk(L.bsig), rd = mk(L.rd), dUp = mk(L.dUp), Fd = mk(L.Fd), dta = mk(L.dta);
+    const LV<double> dla = mk(L.dla), dU = mk(L.dU), dX = mk(L.dX), dsig = mk(L.dsig), dt = mk(L.dt), dl = mk(L.dl);
+    const LV<double> gA = mk(L.iA), gB = mk(L.iB), gC = mk(L.iC), gh = mk(L.ih);
     double x0[NX], up[NU];
 #pragma unroll
     for (int s = 0; s < NX; ++s) x0[s] = P.x0[(size_t)b * NX + s];
 #pragma unroll
     for (int i = 0; i < NU; ++i) up[i] = P.up[(size_t)b * NU + i];
-
-    auto loadA = [&](int k, double* A) {
-#pragma unroll
-        for (int i = 0; i < NX * NX; ++i) A[i] = gA[k * NX * NX + i];
-    };
-    auto loadB = [&](int k, double* Bm) {
-#pragma unroll
-        for (int i = 0; i < NX * NU; ++i) Bm[i] = gB[k * NX * NU + i];
-    };
-    auto loadC = [&](int k, double* C, double* h) {
-#pragma unroll
-        for (int i = 0; i < MC * NX; ++i) C[i] = gC[k * MC * NX + i];
-#pragma unroll
-        for (int r = 0; r < MC; ++r) h[r] = gh[k * MC + r];
-    };
     // input-row bound of row q (0: u <= ub, 1: -u <= -lb) of input i
     auto w_in = [&](int i, int q) -> double { return q ? -c.u_lb[i] : c.u_ub[i]; };
 
@@ -133,15 +234,12 @@ __host__ __device__ inline void lane_agent(const MpcConst& c, const MpcPtrs& P, 
             X[s] = x[s];
         }
         for (int k = 0; k < N; ++k) {
-            double A[NX * NX], C[MC * NX], h[MC];
-            loadA(k, A);
-            loadC(k, C, h);
             double xn[NX];
 #pragma unroll
             for (int s = 0; s < NX; ++s) {
                 double v = 0.0;
 #pragma unroll
-                for (int q = 0; q < NX; ++q) v = fma(A[s * NX + q], x[q], v);
+                for (int q = 0; q < NX; ++q) v = fma((double)gA[k * NX * NX + s * NX + q], x[q], v);
                 xn[s] = v;
             }
 #pragma unroll
@@ -152,19 +250,20 @@ __host__ __device__ inline void lane_agent(const MpcConst& c, const MpcPtrs& P, 
 #pragma unroll
             for (int i = 0; i < NU; ++i) U[k * NU + i] = 0.0;
 #pragma unroll
-            for (int j = 0; j < NS; ++j) sig[k * NS + j] = 0.0;
+            for (int q = 0; q < NS; ++q) sig[k * NS + q] = 0.0;
 #pragma unroll
             for (int r = 0; r < MC; ++r) {
                 const int R = k * MC + r;
-                if (__builtin_isfinite(h[r])) {
+                const double hr = gh[R];
+                if (__builtin_isfinite(hr)) {
                     double g = 0.0;
 #pragma unroll
-                    for (int s = 0; s < NX; ++s) g = fma(C[r * NX + s], x[s], g);
-                    const double s0 = h[r] - g;
+                    for (int s = 0; s < NX; ++s) g = fma((double)gC[k * MC * NX + r * NX + s], x[s], g);
+                    const double s0 = hr - g;
                     t[R] = s0 > kT0Floor ? s0 : kT0Floor;
                     lam[R] = 1.0;
                     ++mact;
-                    scale_p = fmax(scale_p, fabs(h[r]));
+                    scale_p = fmax(scale_p, fabs(hr));
                 } else {
                     t[R] = 1.0;
                     lam[R] = 0.0;
@@ -192,38 +291,38 @@ __host__ __device__ inline void lane_agent(const MpcConst& c, const MpcPtrs& P, 
     const double mactd = mact ? (double)mact : 1.0;
 
     // ---- row algebra of one block (the MC rows of stage kb, acting on X_{kb+1}) ----
-    // th, the slack-group Schur terms Dsig, the slack residual rsig, and for rc (the complementarity
-    // right-hand side per row) rho and its stable-form rt (oracle solve_one).
+    // th, the slack-group Schur terms Dsig, the slack residual rsig (oracle solve_one); the block's
+    // data come from a stage image (C rows at M::C, h at M::h) and the caller's t / lam / x / sigma
     struct Blk {
         double th[MC], rp[MC], tt[MC], ll[MC], Dsig[NS], rsig[NS];
         bool act[MC];
     };
-    auto blk_rows = [&](int kb, const double* xn, const double* sg, const double* C, const double* h, Blk& q) {
+    auto blk_rows = [&](int buf, const double* xn, const double* sg, const double* tt, const double* ll, Blk& q) {
 #pragma unroll
         for (int r = 0; r < MC; ++r) {
-            const int R = kb * MC + r;
-            q.act[r] = __builtin_isfinite(h[r]);
-            q.tt[r] = t[R];
-            q.ll[r] = lam[R];
+            const double hr = im(buf, M::h + r);
+            q.act[r] = __builtin_isfinite(hr);
+            q.tt[r] = tt[r];
+            q.ll[r] = ll[r];
             double g = 0.0;
 #pragma unroll
-            for (int s = 0; s < NX; ++s) g = fma(C[r * NX + s], xn[s], g);
-            const int j = c.row_slack[r];
-            if (j >= 0) g += (double)c.row_sign[r] * sg[j];
-            q.rp[r] = q.act[r] ? g + q.tt[r] - h[r] : 0.0;
+            for (int s = 0; s < NX; ++s) g = fma(im(buf, M::C + r * NX + s), xn[s], g);
+            const int jj = c.row_slack[r];
+            if (jj >= 0) g += (double)c.row_sign[r] * sg[jj];
+            q.rp[r] = q.act[r] ? g + q.tt[r] - hr : 0.0;
             q.th[r] = q.act[r] ? q.ll[r] / q.tt[r] : 0.0;
         }
 #pragma unroll
-        for (int j = 0; j < NS; ++j) {
-            double v = 2.0 * c.Qs[j], rs = 2.0 * c.Qs[j] * sg[j];
+        for (int jj = 0; jj < NS; ++jj) {
+            double v = 2.0 * c.Qs[jj], rsv = 2.0 * c.Qs[jj] * sg[jj];
 #pragma unroll
             for (int r = 0; r < MC; ++r)
-                if (c.row_slack[r] == j) {
+                if (c.row_slack[r] == jj) {
                     v += q.th[r];
-                    rs += (double)c.row_sign[r] * q.ll[r];
+                    rsv += (double)c.row_sign[r] * q.ll[r];
                 }
-            q.Dsig[j] = v;
-            q.rsig[j] = rs;
+            q.Dsig[jj] = v;
+            q.rsig[jj] = rsv;
         }
     };
     // rho (rows of the block) from the complementarity rhs rc, and rt (stable group form)
@@ -232,47 +331,51 @@ __host__ __device__ inline void lane_agent(const MpcConst& c, const MpcPtrs& P, 
         for (int r = 0; r < MC; ++r) rho[r] = q.act[r] ? (rc[r] + q.ll[r] * q.rp[r]) / q.tt[r] : 0.0;
 #pragma unroll
         for (int r = 0; r < MC; ++r) {
-            const int j = c.row_slack[r];
-            if (j < 0) {
+            const int jj = c.row_slack[r];
+            if (jj < 0) {
                 rt[r] = rho[r];
                 continue;
             }
-            double v = 2.0 * c.Qs[j] * rho[r] - q.th[r] * (double)c.row_sign[r] * q.rsig[j];
+            double v = 2.0 * c.Qs[jj] * rho[r] - q.th[r] * (double)c.row_sign[r] * q.rsig[jj];
 #pragma unroll
             for (int r2 = 0; r2 < MC; ++r2) {
-                if (r2 == r || c.row_slack[r2] != j) continue;
+                if (r2 == r || c.row_slack[r2] != jj) continue;
                 v += q.th[r2] * rho[r] - q.th[r] * (double)(c.row_sign[r] * c.row_sign[r2]) * rho[r2];
             }
-            rt[r] = v / q.Dsig[j];
+            rt[r] = v / q.Dsig[jj];
         }
     };
     // W = 2Q + M (stable group Schur form) of the block (oracle stage_w); lower triangle, packed
-    auto blk_w = [&](const Blk& q, const double* C, double* W) {
+    auto blk_w = [&](int buf, const Blk& q, double* W) {
 #pragma unroll
         for (int s = 0; s < NX; ++s)
 #pragma unroll
             for (int u = 0; u <= s; ++u) W[sy(s, u)] = 2.0 * c.Q[s * NX + u];
 #pragma unroll
         for (int r = 0; r < MC; ++r) {
-            const double* c1 = C + r * NX;
+            double c1[NX];
+#pragma unroll
+            for (int s = 0; s < NX; ++s) c1[s] = im(buf, M::C + r * NX + s);
             const double th1 = q.th[r];
-            const int j = c.row_slack[r];
-            if (j < 0) {
+            const int jj = c.row_slack[r];
+            if (jj < 0) {
 #pragma unroll
                 for (int s = 0; s < NX; ++s)
 #pragma unroll
                     for (int u = 0; u <= s; ++u) W[sy(s, u)] += th1 * c1[s] * c1[u];
                 continue;
             }
-            const double inv = 1.0 / q.Dsig[j], qq = 2.0 * c.Qs[j];
+            const double inv = 1.0 / q.Dsig[jj], qq = 2.0 * c.Qs[jj];
 #pragma unroll
             for (int s = 0; s < NX; ++s)
 #pragma unroll
                 for (int u = 0; u <= s; ++u) W[sy(s, u)] += qq * th1 * c1[s] * c1[u] * inv;
 #pragma unroll
             for (int r2 = r + 1; r2 < MC; ++r2) {
-                if (c.row_slack[r2] != j) continue;
-                const double* c2 = C + r2 * NX;
+                if (c.row_slack[r2] != jj) continue;
+                double c2[NX];
+#pragma unroll
+                for (int s = 0; s < NX; ++s) c2[s] = im(buf, M::C + r2 * NX + s);
                 const double th2 = q.th[r2], s1 = c.row_sign[r], s2 = c.row_sign[r2];
 #pragma unroll
                 for (int s = 0; s < NX; ++s)
@@ -282,19 +385,18 @@ __host__ __device__ inline void lane_agent(const MpcConst& c, const MpcPtrs& P, 
             }
         }
     };
-    // 2R u_k + 2dR (du_k - du_{k+1}) (the input part of the gradient), entry i
-    auto rdr = [&](int k, int i) -> double {
+    // 2R u_k + 2dR (du_k - du_{k+1}) (the input part of the gradient), entry i, from u_{k-1}, u_k, u_{k+1}
+    auto rdr = [&](int k, int i, const double* um, const double* uk, const double* un) -> double {
         double v = 0.0;
 #pragma unroll
-        for (int j = 0; j < NU; ++j) {
-            const double uk = U[k * NU + j];
-            const double duk = uk - (k ? U[(k - 1) * NU + j] : up[j]);
-            const double dun = (k + 1 < N) ? U[(k + 1) * NU + j] - uk : 0.0;
-            v += 2.0 * c.R[i * NU + j] * uk + 2.0 * c.dR[i * NU + j] * (duk - dun);
+        for (int q = 0; q < NU; ++q) {
+            const double duk = uk[q] - um[q];
+            const double dun = (k + 1 < N) ? un[q] - uk[q] : 0.0;
+            v += 2.0 * c.R[i * NU + q] * uk[q] + 2.0 * c.dR[i * NU + q] * (duk - dun);
         }
         return v;
     };
-    // gains store / load (RF precision; fp32 in Ff, fp64 in Fd)
+    // gains store (RF precision; fp32 in Ff, fp64 in Fd) and image fetch / read
     auto storeF = [&](int k, const auto* K, const auto* Hi) {
         using RF = std::remove_cv_t<std::remove_reference_t<decltype(K[0])>>;
 #pragma unroll
@@ -308,331 +410,448 @@ __host__ __device__ inline void lane_agent(const MpcConst& c, const MpcPtrs& P, 
             else Fd[k * SF + NU * NA + e] = Hi[e];
         }
     };
-    auto loadF = [&](int k, auto* K, auto* Hi) {
-        using RF = std::remove_reference_t<decltype(K[0])>;
-#pragma unroll
-        for (int e = 0; e < NU * NA; ++e) {
-            if constexpr (std::is_same_v<RF, float>) K[e] = Ff[k * SF + e];
-            else K[e] = Fd[k * SF + e];
-        }
-#pragma unroll
-        for (int e = 0; e < NU * NU; ++e) {
-            if constexpr (std::is_same_v<RF, float>) Hi[e] = Ff[k * SF + NU * NA + e];
-            else Hi[e] = Fd[k * SF + NU * NA + e];
-        }
+    auto fetchF = [&](auto rf_tag, int buf, int k) {
+        using RF = decltype(rf_tag);
+        if constexpr (std::is_same_v<RF, float>) ff(buf, 2 * L.Ff + (size_t)k * SF, SF);
+        else fd(buf, M::Fd, L.Fd + (size_t)k * SF, SF);
+    };
+    auto imF = [&](auto rf_tag, int buf, int e) {
+        using RF = decltype(rf_tag);
+        if constexpr (std::is_same_v<RF, float>) return imf(buf, e);
+        else return im(buf, M::Fd + e);
     };
     // backward solve step at stage k (oracle ric_solve): g = p_u - rhs + B'p_x, dUp = -Hi g,
-    // p <- [A'p_x; 0] + K'g
-    auto bsolve = [&](const auto* K, const auto* Hi, const double* A, const double* Bm, const double* rhs, auto* pv,
-                      double* dup) {
-        using RF = std::remove_cv_t<std::remove_reference_t<decltype(K[0])>>;
+    // p <- [A'p_x; 0] + K'g; A, B, K, Hi from the image
+    auto bsolve_img = [&](auto rf_tag, int buf, const double* rhs, auto* pv, double* dup) {
+        using RF = decltype(rf_tag);
         RF g[NU], pn[NA];
 #pragma unroll
         for (int cc = 0; cc < NU; ++cc) {
             RF v = pv[NX + cc] - (RF)rhs[cc];
 #pragma unroll
-            for (int s = 0; s < NX; ++s) v += (RF)Bm[s * NU + cc] * pv[s];
+            for (int s = 0; s < NX; ++s) v += (RF)im(buf, M::B + s * NU + cc) * pv[s];
             g[cc] = v;
         }
 #pragma unroll
         for (int cc = 0; cc < NU; ++cc) {
             RF v = 0;
 #pragma unroll
-            for (int e = 0; e < NU; ++e) v -= Hi[cc * NU + e] * g[e];
+            for (int e = 0; e < NU; ++e) v -= imF(rf_tag, buf, NU * NA + cc * NU + e) * g[e];
             dup[cc] = (double)v;
         }
 #pragma unroll
-        for (int j = 0; j < NA; ++j) {
+        for (int jj = 0; jj < NA; ++jj) {
             RF v = 0;
-            if (j < NX)
+            if (jj < NX)
 #pragma unroll
-                for (int s = 0; s < NX; ++s) v += (RF)A[s * NX + j] * pv[s];
+                for (int s = 0; s < NX; ++s) v += (RF)im(buf, M::A + s * NX + jj) * pv[s];
 #pragma unroll
-            for (int cc = 0; cc < NU; ++cc) v += K[cc * NA + j] * g[cc];
-            pn[j] = v;
+            for (int cc = 0; cc < NU; ++cc) v += imF(rf_tag, buf, cc * NA + jj) * g[cc];
+            pn[jj] = v;
         }
 #pragma unroll
-        for (int j = 0; j < NA; ++j) pv[j] = pn[j];
+        for (int jj = 0; jj < NA; ++jj) pv[jj] = pn[jj];
     };
 
     // ============ S1: lazy update, residuals, factorisation, predictor backward solve ============
-    auto sweep1 = [&](auto rf_tag, bool apply, double al) -> S1Out {
+    // Step jb = N .. 0: the block part of block kb = jb - 1 (jb >= 1; the previous step's update of
+    // its rows, X_jb, sigma_kb, u_kb, then its residual terms, W_jb and y_jb) and the stage part of
+    // stage k = jb (jb <= N-1: rows of u_k, dual residual, predictor rhs, factorisation, backward
+    // solve).  u_{k+1}, u_k and the rows of u_k come from the two previous steps (registers): the
+    // image of a step is fetched before the step before it stores its update.
+    auto s1_fetch = [&](int buf, int jb, bool apply) {
+        if (jb <= N - 1) {
+            fd(buf, M::A, L.iA + (size_t)jb * NX * NX, NX * NX);
+            fd(buf, M::B, L.iB + (size_t)jb * NX * NU, NX * NU);
+        }
+        if (jb >= 1) {
+            const int kb = jb - 1;
+            fd(buf, M::C, L.iC + (size_t)kb * MC * NX, MC * NX);
+            fd(buf, M::h, L.ih + (size_t)kb * MC, MC);
+            fd(buf, M::p, L.ip + (size_t)jb * NX, NX);
+            fd(buf, M::X, L.X + (size_t)jb * NX, NX);
+            fd(buf, M::sig, L.sig + (size_t)kb * NS, NS);
+            fd(buf, M::tB, L.t + (size_t)kb * MC, MC);
+            fd(buf, M::lB, L.lam + (size_t)kb * MC, MC);
+            fd(buf, M::U, L.U + (size_t)kb * NU, NU);
+            fd(buf, M::tI, L.t + ms + (size_t)kb * 2 * NU, 2 * NU);
+            fd(buf, M::lI, L.lam + ms + (size_t)kb * 2 * NU, 2 * NU);
+            if (apply) {
+                fd(buf, M::dX, L.dX + (size_t)jb * NX, NX);
+                fd(buf, M::dsig, L.dsig + (size_t)kb * NS, NS);
+                fd(buf, M::dtB, L.dt + (size_t)kb * MC, MC);
+                fd(buf, M::dlB, L.dl + (size_t)kb * MC, MC);
+                fd(buf, M::dU, L.dU + (size_t)kb * NU, NU);
+                fd(buf, M::dtI, L.dt + ms + (size_t)kb * 2 * NU, 2 * NU);
+                fd(buf, M::dlI, L.dl + ms + (size_t)kb * 2 * NU, 2 * NU);
+            }
+        }
+    };
+    auto sweep1 = [&](auto rf_tag, bool apply, double al) __attribute__((always_inline)) -> S1Out {
         using RF = decltype(rf_tag);
         S1Out o{1.0, 0.0, 0.0, 0.0, 0.0, false};
         RF Pm[NA * (NA + 1) / 2], pv[NA];  // cost-to-go P_{k+1}, lower triangle packed
         double psf[NX], ps[NX], ps3[NX];
-        // lazy update of block kb: X_{kb+1}, sig_kb, its rows, U_kb and the rows of u_kb
-        auto update_blk = [&](int kb) {
-            if (!apply) return;
+        double un[NU], uk[NU], tIk[2 * NU], lIk[2 * NU];  // u_{k+1}, u_k, rows of u_k
 #pragma unroll
-            for (int s = 0; s < NX; ++s) X[(kb + 1) * NX + s] = fma(al, dX[(kb + 1) * NX + s], X[(kb + 1) * NX + s]);
+        for (int i = 0; i < NU; ++i) un[i] = uk[i] = 0.0;
 #pragma unroll
-            for (int j = 0; j < NS; ++j) sig[kb * NS + j] = fma(al, dsig[kb * NS + j], sig[kb * NS + j]);
+        for (int i = 0; i < 2 * NU; ++i) tIk[i] = lIk[i] = 0.0;
+        s1_fetch(N & 1, N, apply);
+        img_wait();
+        for (int jb = N; jb >= 0; --jb) {
+            const int buf = jb & 1, k = jb, kb = jb - 1;
+            if (jb >= 1) s1_fetch(buf ^ 1, jb - 1, apply);
+            // ---- block part, phase 0: the lazy update of block kb ----
+            double xn[NX], sg[NS], tB[MC], lB[MC], um[NU], tIm[2 * NU], lIm[2 * NU];
+            if (jb >= 1) {
 #pragma unroll
-            for (int i = 0; i < NU; ++i) U[kb * NU + i] = fma(al, dU[kb * NU + i], U[kb * NU + i]);
+                for (int s = 0; s < NX; ++s) xn[s] = im(buf, M::X + s);
 #pragma unroll
-            for (int r = 0; r < MC; ++r) {
-                const int R = kb * MC + r;
-                if (__builtin_isfinite(gh[R])) {
-                    t[R] = fma(al, dt[R], t[R]);
-                    lam[R] = fma(al, dl[R], lam[R]);
-                }
-            }
-#pragma unroll
-            for (int i = 0; i < NU; ++i)
-#pragma unroll
-                for (int q = 0; q < 2; ++q) {
-                    const int R = ms + 2 * (kb * NU + i) + q;
-                    if (__builtin_isfinite(w_in(i, q))) {
-                        t[R] = fma(al, dt[R], t[R]);
-                        lam[R] = fma(al, dl[R], lam[R]);
-                    }
-                }
-        };
-        // rows of block kb at X_{kb+1}: residual terms, W, and the three adjoint loads y
-        auto block = [&](int kb, const double* C, const double* h, double* W, double* yf, double* y, double* y3) {
-            double xn[NX], sg[NS];
-#pragma unroll
-            for (int s = 0; s < NX; ++s) xn[s] = X[(kb + 1) * NX + s];
-#pragma unroll
-            for (int j = 0; j < NS; ++j) sg[j] = sig[kb * NS + j];
-            Blk q;
-            blk_rows(kb, xn, sg, C, h, q);
-            double rc[MC], rho[MC], rt[MC];
-#pragma unroll
-            for (int r = 0; r < MC; ++r) {
-                rc[r] = -q.tt[r] * q.ll[r];
-                if (q.act[r]) {
-                    o.nrp = lane_nmax(o.nrp, fabs(q.rp[r]));
-                    o.mu += q.tt[r] * q.ll[r];
-                }
-            }
-#pragma unroll
-            for (int j = 0; j < NS; ++j) o.nrs = lane_nmax(o.nrs, fabs(q.rsig[j]));
-            blk_rho(q, rc, rho, rt);
-            blk_w(q, C, W);
-#pragma unroll
-            for (int s = 0; s < NX; ++s) {
-                double v = 2.0 * gp[(kb + 1) * NX + s];
-#pragma unroll
-                for (int u = 0; u < NX; ++u) v = fma(2.0 * c.Q[s * NX + u], xn[u], v);
-                yf[s] = v;
-                double vl = v, v3 = 0.0;
+                for (int q = 0; q < NS; ++q) sg[q] = im(buf, M::sig + q);
 #pragma unroll
                 for (int r = 0; r < MC; ++r) {
-                    vl = fma(q.ll[r], C[r * NX + s], vl);
-                    v3 = fma(rt[r], C[r * NX + s], v3);
+                    tB[r] = im(buf, M::tB + r);
+                    lB[r] = im(buf, M::lB + r);
                 }
-                y[s] = vl;
-                y3[s] = v3;
-            }
-        };
-        {   // prologue: block N-1 (X_N): psi_N = y_N, P_N = blkdiag(W_N, 0), p = 0
-            update_blk(N - 1);
-            double C[MC * NX], h[MC], W[NX * (NX + 1) / 2];
-            loadC(N - 1, C, h);
-            block(N - 1, C, h, W, psf, ps, ps3);
 #pragma unroll
-            for (int i = 0; i < NA; ++i)
+                for (int i = 0; i < NU; ++i) um[i] = im(buf, M::U + i);
 #pragma unroll
-                for (int j = 0; j <= i; ++j) Pm[sy(i, j)] = (i < NX) ? (RF)W[sy(i, j)] : (RF)0;
-#pragma unroll
-            for (int j = 0; j < NA; ++j) pv[j] = 0;
-        }
-        for (int k = N - 1; k >= 0; --k) {
-            if (k >= 1) update_blk(k - 1);
-            double A[NX * NX], Bm[NX * NU];
-            loadA(k, A);
-            loadB(k, Bm);
-            // ---- input rows of u_k ----
-            double thu[NU], rtu[NU];  // th_ub + th_lb, rt_ub - rt_lb
-            double lamu[NU];          // lam_ub - lam_lb
-#pragma unroll
-            for (int i = 0; i < NU; ++i) {
-                thu[i] = 0.0;
-                rtu[i] = 0.0;
-                lamu[i] = 0.0;
-                const double uk = U[k * NU + i];
-#pragma unroll
-                for (int q = 0; q < 2; ++q) {
-                    const int R = ms + 2 * (k * NU + i) + q;
-                    const double wv = w_in(i, q);
-                    const double tt = t[R], ll = lam[R];
-                    lamu[i] += q ? -ll : ll;
-                    if (!__builtin_isfinite(wv)) continue;
-                    const double rp = (q ? -uk : uk) + tt - wv;
-                    o.nrp = lane_nmax(o.nrp, fabs(rp));
-                    o.mu += tt * ll;
-                    const double th = ll / tt;
-                    thu[i] += th;
-                    const double rho = (-tt * ll + ll * rp) / tt;
-                    rtu[i] += q ? -rho : rho;
+                for (int i = 0; i < 2 * NU; ++i) {
+                    tIm[i] = im(buf, M::tI + i);
+                    lIm[i] = im(buf, M::lI + i);
                 }
-            }
-            // ---- gradient / dual residual / predictor rhs of u_k ----
-            double rhs[NU];
+                if (apply) {
 #pragma unroll
-            for (int i = 0; i < NU; ++i) {
-                double gf = 0.0, gd = 0.0, g3 = 0.0;
-#pragma unroll
-                for (int s = 0; s < NX; ++s) {
-                    gf = fma(Bm[s * NU + i], psf[s], gf);
-                    gd = fma(Bm[s * NU + i], ps[s], gd);
-                    g3 = fma(Bm[s * NU + i], ps3[s], g3);
-                }
-                const double rr = rdr(k, i);
-                o.gsc = lane_nmax(o.gsc, fabs(gf + rr));
-                const double rdv = gd + rr + lamu[i];
-                o.nrd = lane_nmax(o.nrd, fabs(rdv));
-                rd[k * NU + i] = rdv;
-                rhs[i] = -rdv - (g3 + rtu[i]);
-            }
-            // ---- Riccati factorisation at stage k (oracle ric_factor, standard form) ----
-            RF K[NU * NA], Hi[NU * NU], Hy[NU * NA];
-            if (!o.broke) {
-                RF PB[NA * NU], H[NU * NU], Lf[NU * NU];
-#pragma unroll
-                for (int i = 0; i < NA; ++i)
-#pragma unroll
-                    for (int cc = 0; cc < NU; ++cc) {
-                        RF v = Pm[sy(i, NX + cc)];
-#pragma unroll
-                        for (int s = 0; s < NX; ++s) v += Pm[sy(i, s)] * (RF)Bm[s * NU + cc];
-                        PB[i * NU + cc] = v;
+                    for (int s = 0; s < NX; ++s) {
+                        xn[s] = fma(al, im(buf, M::dX + s), xn[s]);
+                        X[jb * NX + s] = xn[s];
                     }
 #pragma unroll
-                for (int cc = 0; cc < NU; ++cc)
-#pragma unroll
-                    for (int e = 0; e < NU; ++e) {
-                        RF v = (RF)(2.0 * c.R[cc * NU + e] + 2.0 * c.dR[cc * NU + e]) + PB[(NX + cc) * NU + e];
-#pragma unroll
-                        for (int s = 0; s < NX; ++s) v += (RF)Bm[s * NU + cc] * PB[s * NU + e];
-                        if (cc == e) v += (RF)thu[cc];
-                        H[cc * NU + e] = v;
+                    for (int q = 0; q < NS; ++q) {
+                        sg[q] = fma(al, im(buf, M::dsig + q), sg[q]);
+                        sig[kb * NS + q] = sg[q];
                     }
 #pragma unroll
-                for (int cc = 0; cc < NU; ++cc)
-#pragma unroll
-                    for (int j = 0; j < NA; ++j) {
-                        RF v = 0;
-                        if (j < NX) {
-#pragma unroll
-                            for (int s = 0; s < NX; ++s) v += PB[s * NU + cc] * (RF)A[s * NX + j];
-                        } else {
-                            v = (RF)(-2.0 * c.dR[cc * NU + (j - NX)]);
+                    for (int r = 0; r < MC; ++r)
+                        if (__builtin_isfinite(im(buf, M::h + r))) {
+                            tB[r] = fma(al, im(buf, M::dtB + r), tB[r]);
+                            lB[r] = fma(al, im(buf, M::dlB + r), lB[r]);
+                            t[kb * MC + r] = tB[r];
+                            lam[kb * MC + r] = lB[r];
                         }
-                        Hy[cc * NA + j] = v;
-                    }
-#pragma unroll
-                for (int j = 0; j < NU; ++j) {
-                    RF d = H[j * NU + j];
-#pragma unroll
-                    for (int q = 0; q < j; ++q) d -= Lf[j * NU + q] * Lf[j * NU + q];
-                    if (!(d > (RF)0)) {
-                        o.broke = true;
-                        d = (RF)1;
-                    }
-                    d = sqrt(d);
-                    Lf[j * NU + j] = d;
-#pragma unroll
-                    for (int i = j + 1; i < NU; ++i) {
-                        RF v = H[i * NU + j];
-#pragma unroll
-                        for (int q = 0; q < j; ++q) v -= Lf[i * NU + q] * Lf[j * NU + q];
-                        Lf[i * NU + j] = v / d;
-                    }
-                }
-#pragma unroll
-                for (int cc = 0; cc < NU; ++cc) {
-                    RF e[NU];
-#pragma unroll
-                    for (int i = 0; i < NU; ++i) e[i] = (i == cc) ? (RF)1 : (RF)0;
 #pragma unroll
                     for (int i = 0; i < NU; ++i) {
-                        RF v = e[i];
-#pragma unroll
-                        for (int q = 0; q < i; ++q) v -= Lf[i * NU + q] * e[q];
-                        e[i] = v / Lf[i * NU + i];
+                        um[i] = fma(al, im(buf, M::dU + i), um[i]);
+                        U[kb * NU + i] = um[i];
                     }
 #pragma unroll
-                    for (int i = NU - 1; i >= 0; --i) {
-                        RF v = e[i];
+                    for (int i = 0; i < 2 * NU; ++i)
+                        if (__builtin_isfinite(w_in(i >> 1, i & 1))) {
+                            tIm[i] = fma(al, im(buf, M::dtI + i), tIm[i]);
+                            lIm[i] = fma(al, im(buf, M::dlI + i), lIm[i]);
+                            t[ms + kb * 2 * NU + i] = tIm[i];
+                            lam[ms + kb * 2 * NU + i] = lIm[i];
+                        }
+                }
+            } else {
 #pragma unroll
-                        for (int q = i + 1; q < NU; ++q) v -= Lf[q * NU + i] * e[q];
-                        e[i] = v / Lf[i * NU + i];
+                for (int i = 0; i < NU; ++i) um[i] = up[i];
+            }
+            LANE_PHASE();
+            // ---- stage part, phase 1: rows of u_k, gradient, dual residual and predictor rhs ----
+            double thu[NU], rhs[NU];  // th_ub + th_lb; -rd - (B'psi3 + rt_ub - rt_lb)
+            if (jb <= N - 1) {
+                double rtu[NU], lamu[NU];
+#pragma unroll
+                for (int i = 0; i < NU; ++i) {
+                    thu[i] = 0.0;
+                    rtu[i] = 0.0;
+                    lamu[i] = 0.0;
+#pragma unroll
+                    for (int q = 0; q < 2; ++q) {
+                        const double wv = w_in(i, q);
+                        const double tt = tIk[2 * i + q], ll = lIk[2 * i + q];
+                        lamu[i] += q ? -ll : ll;
+                        if (!__builtin_isfinite(wv)) continue;
+                        const double rp = (q ? -uk[i] : uk[i]) + tt - wv;
+                        o.nrp = lane_nmax(o.nrp, fabs(rp));
+                        o.mu += tt * ll;
+                        thu[i] += ll / tt;
+                        const double rho = (-tt * ll + ll * rp) / tt;
+                        rtu[i] += q ? -rho : rho;
                     }
-#pragma unroll
-                    for (int i = 0; i < NU; ++i) Hi[i * NU + cc] = e[i];
                 }
 #pragma unroll
-                for (int cc = 0; cc < NU; ++cc)
+                for (int i = 0; i < NU; ++i) {
+                    double gf = 0.0, gd = 0.0, g3 = 0.0;
 #pragma unroll
-                    for (int j = 0; j < NA; ++j) {
-                        RF v = 0;
-#pragma unroll
-                        for (int e = 0; e < NU; ++e) v -= Hi[cc * NU + e] * Hy[e * NA + j];
-                        K[cc * NA + j] = v;
+                    for (int s = 0; s < NX; ++s) {
+                        const double bs = im(buf, M::B + s * NU + i);
+                        gf = fma(bs, psf[s], gf);
+                        gd = fma(bs, ps[s], gd);
+                        g3 = fma(bs, ps3[s], g3);
                     }
-                storeF(k, K, Hi);
-                double dup[NU];
-                bsolve(K, Hi, A, Bm, rhs, pv, dup);
-#pragma unroll
-                for (int i = 0; i < NU; ++i) dUp[k * NU + i] = dup[i];
+                    const double rr = rdr(k, i, um, uk, un);
+                    o.gsc = lane_nmax(o.gsc, fabs(gf + rr));
+                    const double rdv = gd + rr + lamu[i];
+                    o.nrd = lane_nmax(o.nrd, fabs(rdv));
+                    rd[k * NU + i] = rdv;
+                    rhs[i] = -rdv - (g3 + rtu[i]);
+                }
             }
-            if (k == 0) break;
-            // ---- block k-1 (X_k): residual terms, W_k, adjoints psi_k = y_k + A_k' psi_{k+1}, P_k ----
-            double C[MC * NX], h[MC], W[NX * (NX + 1) / 2], yf[NX], y[NX], y3[NX];
-            loadC(k - 1, C, h);
-            block(k - 1, C, h, W, yf, y, y3);
-            double nf[NX], nd[NX], n3[NX];
+            LANE_PHASE();
+            // ---- block part, phase 2: residual terms, W, y and the adjoints psi_jb = y_jb + A_jb' psi ----
+            double W[NX * (NX + 1) / 2];
+            if (jb >= 1) {
+                Blk q;
+                blk_rows(buf, xn, sg, tB, lB, q);
+                double rc[MC], rho[MC], rt[MC];
 #pragma unroll
-            for (int j = 0; j < NX; ++j) {
-                double a1 = yf[j], a2 = y[j], a3 = y3[j];
+                for (int r = 0; r < MC; ++r) {
+                    rc[r] = -q.tt[r] * q.ll[r];
+                    if (q.act[r]) {
+                        o.nrp = lane_nmax(o.nrp, fabs(q.rp[r]));
+                        o.mu += q.tt[r] * q.ll[r];
+                    }
+                }
+#pragma unroll
+                for (int qq = 0; qq < NS; ++qq) o.nrs = lane_nmax(o.nrs, fabs(q.rsig[qq]));
+                blk_rho(q, rc, rho, rt);
+                blk_w(buf, q, W);
+                double yf[NX], y[NX], y3[NX];
 #pragma unroll
                 for (int s = 0; s < NX; ++s) {
-                    a1 = fma(A[s * NX + j], psf[s], a1);
-                    a2 = fma(A[s * NX + j], ps[s], a2);
-                    a3 = fma(A[s * NX + j], ps3[s], a3);
-                }
-                nf[j] = a1;
-                nd[j] = a2;
-                n3[j] = a3;
-            }
+                    double v = 2.0 * im(buf, M::p + s);
 #pragma unroll
-            for (int j = 0; j < NX; ++j) {
-                psf[j] = nf[j];
-                ps[j] = nd[j];
-                ps3[j] = n3[j];
-            }
-            if (!o.broke) {
-                // P_k = blkdiag(W_k + A'P_xx A, 2dR) + Hy'K, written over P_{k+1} once P_xx A is formed
-                RF PA[NX * NX];
+                    for (int u = 0; u < NX; ++u) v = fma(2.0 * c.Q[s * NX + u], xn[u], v);
+                    yf[s] = v;
+                    double vl = v, v3 = 0.0;
 #pragma unroll
-                for (int s = 0; s < NX; ++s)
-#pragma unroll
-                    for (int j = 0; j < NX; ++j) {
-                        RF v = 0;
-#pragma unroll
-                        for (int q = 0; q < NX; ++q) v += Pm[sy(s, q)] * (RF)A[q * NX + j];
-                        PA[s * NX + j] = v;
+                    for (int r = 0; r < MC; ++r) {
+                        const double cr = im(buf, M::C + r * NX + s);
+                        vl = fma(q.ll[r], cr, vl);
+                        v3 = fma(rt[r], cr, v3);
                     }
+                    y[s] = vl;
+                    y3[s] = v3;
+                }
+                if (jb == N) {
+#pragma unroll
+                    for (int s = 0; s < NX; ++s) {
+                        psf[s] = yf[s];
+                        ps[s] = y[s];
+                        ps3[s] = y3[s];
+                    }
+                } else {
+                    double nf[NX], nd[NX], n3[NX];
+#pragma unroll
+                    for (int jj = 0; jj < NX; ++jj) {
+                        double a1 = yf[jj], a2 = y[jj], a3 = y3[jj];
+#pragma unroll
+                        for (int s = 0; s < NX; ++s) {
+                            const double as = im(buf, M::A + s * NX + jj);
+                            a1 = fma(as, psf[s], a1);
+                            a2 = fma(as, ps[s], a2);
+                            a3 = fma(as, ps3[s], a3);
+                        }
+                        nf[jj] = a1;
+                        nd[jj] = a2;
+                        n3[jj] = a3;
+                    }
+#pragma unroll
+                    for (int jj = 0; jj < NX; ++jj) {
+                        psf[jj] = nf[jj];
+                        ps[jj] = nd[jj];
+                        ps3[jj] = n3[jj];
+                    }
+                }
+            }
+            LANE_PHASE();
+            if (jb == N) {  // P_N = blkdiag(W_N, 0), p = 0
 #pragma unroll
                 for (int i = 0; i < NA; ++i)
 #pragma unroll
-                    for (int j = 0; j <= i; ++j) {
-                        RF v;
-                        if (i < NX) {
-                            v = (RF)W[sy(i, j)];
+                    for (int jj = 0; jj <= i; ++jj) Pm[sy(i, jj)] = (i < NX) ? (RF)W[sy(i, jj)] : (RF)0;
 #pragma unroll
-                            for (int s = 0; s < NX; ++s) v += (RF)A[s * NX + i] * PA[s * NX + j];
-                        } else {
-                            v = (j >= NX) ? (RF)(2.0 * c.dR[(i - NX) * NU + (j - NX)]) : (RF)0;
+                for (int jj = 0; jj < NA; ++jj) pv[jj] = 0;
+            } else if (!o.broke) {
+                // ---- stage part, phase 3: factorisation at stage k (oracle ric_factor), gains stored,
+                // predictor backward solve step, T = Hy'K ----
+                RF T[NA * (NA + 1) / 2];
+                {
+                    RF K[NU * NA], Hi[NU * NU], Hy[NU * NA];
+                    {
+                        RF PB[NA * NU], H[NU * NU], Lf[NU * NU];
+#pragma unroll
+                        for (int i = 0; i < NA; ++i)
+#pragma unroll
+                            for (int cc = 0; cc < NU; ++cc) {
+                                RF v = Pm[sy(i, NX + cc)];
+#pragma unroll
+                                for (int s = 0; s < NX; ++s) v += Pm[sy(i, s)] * (RF)im(buf, M::B + s * NU + cc);
+                                PB[i * NU + cc] = v;
+                            }
+#pragma unroll
+                        for (int cc = 0; cc < NU; ++cc)
+#pragma unroll
+                            for (int e = 0; e < NU; ++e) {
+                                RF v = (RF)(2.0 * c.R[cc * NU + e] + 2.0 * c.dR[cc * NU + e]) + PB[(NX + cc) * NU + e];
+#pragma unroll
+                                for (int s = 0; s < NX; ++s) v += (RF)im(buf, M::B + s * NU + cc) * PB[s * NU + e];
+                                if (cc == e) v += (RF)thu[cc];
+                                H[cc * NU + e] = v;
+                            }
+#pragma unroll
+                        for (int cc = 0; cc < NU; ++cc)
+#pragma unroll
+                            for (int jj = 0; jj < NA; ++jj) {
+                                RF v = 0;
+                                if (jj < NX) {
+#pragma unroll
+                                    for (int s = 0; s < NX; ++s) v += PB[s * NU + cc] * (RF)im(buf, M::A + s * NX + jj);
+                                } else {
+                                    v = (RF)(-2.0 * c.dR[cc * NU + (jj - NX)]);
+                                }
+                                Hy[cc * NA + jj] = v;
+                            }
+#pragma unroll
+                        for (int jj = 0; jj < NU; ++jj) {
+                            RF d = H[jj * NU + jj];
+#pragma unroll
+                            for (int qq = 0; qq < jj; ++qq) d -= Lf[jj * NU + qq] * Lf[jj * NU + qq];
+                            if (!(d > (RF)0)) {
+                                o.broke = true;
+                                d = (RF)1;
+                            }
+                            d = sqrt(d);
+                            Lf[jj * NU + jj] = d;
+#pragma unroll
+                            for (int i = jj + 1; i < NU; ++i) {
+                                RF v = H[i * NU + jj];
+#pragma unroll
+                                for (int qq = 0; qq < jj; ++qq) v -= Lf[i * NU + qq] * Lf[jj * NU + qq];
+                                Lf[i * NU + jj] = v / d;
+                            }
                         }
 #pragma unroll
-                        for (int cc = 0; cc < NU; ++cc) v += Hy[cc * NA + i] * K[cc * NA + j];
-                        Pm[sy(i, j)] = v;
+                        for (int cc = 0; cc < NU; ++cc) {
+                            RF e[NU];
+#pragma unroll
+                            for (int i = 0; i < NU; ++i) e[i] = (i == cc) ? (RF)1 : (RF)0;
+#pragma unroll
+                            for (int i = 0; i < NU; ++i) {
+                                RF v = e[i];
+#pragma unroll
+                                for (int qq = 0; qq < i; ++qq) v -= Lf[i * NU + qq] * e[qq];
+                                e[i] = v / Lf[i * NU + i];
+                            }
+#pragma unroll
+                            for (int i = NU - 1; i >= 0; --i) {
+                                RF v = e[i];
+#pragma unroll
+                                for (int qq = i + 1; qq < NU; ++qq) v -= Lf[qq * NU + i] * e[qq];
+                                e[i] = v / Lf[i * NU + i];
+                            }
+#pragma unroll
+                            for (int i = 0; i < NU; ++i) Hi[i * NU + cc] = e[i];
+                        }
                     }
+#pragma unroll
+                    for (int cc = 0; cc < NU; ++cc)
+#pragma unroll
+                        for (int jj = 0; jj < NA; ++jj) {
+                            RF v = 0;
+#pragma unroll
+                            for (int e = 0; e < NU; ++e) v -= Hi[cc * NU + e] * Hy[e * NA + jj];
+                            K[cc * NA + jj] = v;
+                        }
+                    storeF(k, K, Hi);
+                    {   // backward solve step: g = p_u - rhs + B'p_x, dUp = -Hi g, p <- [A'p_x; 0] + K'g
+                        RF g[NU], pn[NA];
+#pragma unroll
+                        for (int cc = 0; cc < NU; ++cc) {
+                            RF v = pv[NX + cc] - (RF)rhs[cc];
+#pragma unroll
+                            for (int s = 0; s < NX; ++s) v += (RF)im(buf, M::B + s * NU + cc) * pv[s];
+                            g[cc] = v;
+                        }
+#pragma unroll
+                        for (int cc = 0; cc < NU; ++cc) {
+                            RF v = 0;
+#pragma unroll
+                            for (int e = 0; e < NU; ++e) v -= Hi[cc * NU + e] * g[e];
+                            dUp[k * NU + cc] = (double)v;
+                        }
+#pragma unroll
+                        for (int jj = 0; jj < NA; ++jj) {
+                            RF v = 0;
+                            if (jj < NX)
+#pragma unroll
+                                for (int s = 0; s < NX; ++s) v += (RF)im(buf, M::A + s * NX + jj) * pv[s];
+#pragma unroll
+                            for (int cc = 0; cc < NU; ++cc) v += K[cc * NA + jj] * g[cc];
+                            pn[jj] = v;
+                        }
+#pragma unroll
+                        for (int jj = 0; jj < NA; ++jj) pv[jj] = pn[jj];
+                    }
+                    if (jb >= 1) {
+#pragma unroll
+                        for (int i = 0; i < NA; ++i)
+#pragma unroll
+                            for (int jj = 0; jj <= i; ++jj) {
+                                RF v = 0;
+#pragma unroll
+                                for (int cc = 0; cc < NU; ++cc) v += Hy[cc * NA + i] * K[cc * NA + jj];
+                                T[sy(i, jj)] = v;
+                            }
+                    }
+                }
+                LANE_PHASE();
+                // ---- phase 4: P_k = blkdiag(W_k + A'P_xx A, 2dR) + Hy'K over P_{k+1} ----
+                if (jb >= 1) {
+                    RF PA[NX * NX];
+#pragma unroll
+                    for (int s = 0; s < NX; ++s)
+#pragma unroll
+                        for (int jj = 0; jj < NX; ++jj) {
+                            RF v = 0;
+#pragma unroll
+                            for (int qq = 0; qq < NX; ++qq) v += Pm[sy(s, qq)] * (RF)im(buf, M::A + qq * NX + jj);
+                            PA[s * NX + jj] = v;
+                        }
+#pragma unroll
+                    for (int i = 0; i < NA; ++i)
+#pragma unroll
+                        for (int jj = 0; jj <= i; ++jj) {
+                            RF v;
+                            if (i < NX) {
+                                v = (RF)W[sy(i, jj)];
+#pragma unroll
+                                for (int s = 0; s < NX; ++s) v += (RF)im(buf, M::A + s * NX + i) * PA[s * NX + jj];
+                            } else {
+                                v = (jj >= NX) ? (RF)(2.0 * c.dR[(i - NX) * NU + (jj - NX)]) : (RF)0;
+                            }
+                            Pm[sy(i, jj)] = v + T[sy(i, jj)];
+                        }
+                }
             }
+            // registers for the next step: u_{k+1} <- u_k, u_k <- u_kb, rows of u_k <- rows of u_kb
+            if (jb >= 1) {
+#pragma unroll
+                for (int i = 0; i < NU; ++i) {
+                    un[i] = uk[i];
+                    uk[i] = um[i];
+                }
+#pragma unroll
+                for (int i = 0; i < 2 * NU; ++i) {
+                    tIk[i] = tIm[i];
+                    lIk[i] = lIm[i];
+                }
+            }
+            img_wait();
+            LANE_PHASE();
         }
         return o;
     };
@@ -643,7 +862,28 @@ __host__ __device__ inline void lane_agent(const MpcConst& c, const MpcPtrs& P, 
     struct FwdOut {
         double amax, s0, s1, s2;
     };
-    auto sweep_fwd = [&](auto rf_tag, int pass, double sm) -> FwdOut {
+    auto fwd_fetch = [&](auto rf_tag, int buf, int k, int pass) {
+        fd(buf, M::A, L.iA + (size_t)k * NX * NX, NX * NX);
+        fd(buf, M::B, L.iB + (size_t)k * NX * NU, NX * NU);
+        fd(buf, M::C, L.iC + (size_t)k * MC * NX, MC * NX);
+        fd(buf, M::h, L.ih + (size_t)k * MC, MC);
+        fd(buf, M::X, L.X + (size_t)(k + 1) * NX, NX);
+        fd(buf, M::U, L.U + (size_t)k * NU, NU);
+        fd(buf, M::sig, L.sig + (size_t)k * NS, NS);
+        fd(buf, M::tB, L.t + (size_t)k * MC, MC);
+        fd(buf, M::lB, L.lam + (size_t)k * MC, MC);
+        fd(buf, M::tI, L.t + ms + (size_t)k * 2 * NU, 2 * NU);
+        fd(buf, M::lI, L.lam + ms + (size_t)k * 2 * NU, 2 * NU);
+        fd(buf, M::dUp, L.dUp + (size_t)k * NU, NU);
+        fetchF(rf_tag, buf, k);
+        if (pass) {
+            fd(buf, M::aB, L.dta + (size_t)k * MC, MC);
+            fd(buf, M::alB, L.dla + (size_t)k * MC, MC);
+            fd(buf, M::aI, L.dta + ms + (size_t)k * 2 * NU, 2 * NU);
+            fd(buf, M::alI, L.dla + ms + (size_t)k * 2 * NU, 2 * NU);
+        }
+    };
+    auto sweep_fwd = [&](auto rf_tag, int pass, double sm) __attribute__((always_inline)) -> FwdOut {
         using RF = decltype(rf_tag);
         FwdOut o{INFINITY, 0.0, 0.0, 0.0};
         double dx[NX];
@@ -670,23 +910,21 @@ __host__ __device__ inline void lane_agent(const MpcConst& c, const MpcPtrs& P, 
                 dla[R] = dlv;
             }
         };
+        fwd_fetch(rf_tag, 0, 0, pass);
+        img_wait();
         for (int k = 0; k < N; ++k) {
-            double A[NX * NX], Bm[NX * NU], C[MC * NX], h[MC];
-            loadA(k, A);
-            loadB(k, Bm);
-            loadC(k, C, h);
-            RF K[NU * NA], Hi[NU * NU];
-            loadF(k, K, Hi);
+            const int buf = k & 1;
+            if (k + 1 < N) fwd_fetch(rf_tag, buf ^ 1, k + 1, pass);
             double du[NU];
             RF dcur[NU];
 #pragma unroll
             for (int cc = 0; cc < NU; ++cc) {
-                RF v = (RF)dUp[k * NU + cc];
+                RF v = (RF)im(buf, M::dUp + cc);
 #pragma unroll
-                for (int j = 0; j < NX; ++j) v += K[cc * NA + j] * (RF)dx[j];
+                for (int jj = 0; jj < NX; ++jj) v += imF(rf_tag, buf, cc * NA + jj) * (RF)dx[jj];
                 if (k > 0)
 #pragma unroll
-                    for (int e = 0; e < NU; ++e) v += K[cc * NA + NX + e] * dup_prev[e];
+                    for (int e = 0; e < NU; ++e) v += imF(rf_tag, buf, cc * NA + NX + e) * dup_prev[e];
                 dcur[cc] = v;
                 du[cc] = (double)v;
             }
@@ -697,16 +935,13 @@ __host__ __device__ inline void lane_agent(const MpcConst& c, const MpcPtrs& P, 
             for (int s = 0; s < NX; ++s) {
                 double v = 0.0;
 #pragma unroll
-                for (int q = 0; q < NX; ++q) v = fma(A[s * NX + q], dx[q], v);
+                for (int qq = 0; qq < NX; ++qq) v = fma(im(buf, M::A + s * NX + qq), dx[qq], v);
 #pragma unroll
-                for (int cc = 0; cc < NU; ++cc) v = fma(Bm[s * NU + cc], du[cc], v);
+                for (int cc = 0; cc < NU; ++cc) v = fma(im(buf, M::B + s * NU + cc), du[cc], v);
                 dxn[s] = v;
             }
 #pragma unroll
             for (int s = 0; s < NX; ++s) dx[s] = dxn[s];
-#ifdef LANE_TRACE
-            if (k < 2 || k == N - 1) printf("  pass %d k %d du %.10e %.10e %.10e\n", pass, k, du[0], du[1 % NU], du[2 % NU]);
-#endif
             if (pass) {
 #pragma unroll
                 for (int cc = 0; cc < NU; ++cc) dU[k * NU + cc] = du[cc];
@@ -716,7 +951,7 @@ __host__ __device__ inline void lane_agent(const MpcConst& c, const MpcPtrs& P, 
             // input rows of u_k: GdU = +-du
 #pragma unroll
             for (int i = 0; i < NU; ++i) {
-                const double uk = U[k * NU + i];
+                const double ukv = im(buf, M::U + i);
 #pragma unroll
                 for (int q = 0; q < 2; ++q) {
                     const int R = ms + 2 * (k * NU + i) + q;
@@ -728,44 +963,48 @@ __host__ __device__ inline void lane_agent(const MpcConst& c, const MpcPtrs& P, 
                         }
                         continue;
                     }
-                    const double tt = t[R], ll = lam[R];
-                    const double rp = (q ? -uk : uk) + tt - wv;
+                    const double tt = im(buf, M::tI + 2 * i + q), ll = im(buf, M::lI + 2 * i + q);
+                    const double rp = (q ? -ukv : ukv) + tt - wv;
                     double rc = -tt * ll;
-                    if (pass) rc += sm - dta[R] * dla[R];
+                    if (pass) rc += sm - im(buf, M::aI + 2 * i + q) * im(buf, M::alI + 2 * i + q);
                     const double rho = (rc + ll * rp) / tt;
                     const double gdu = q ? -du[i] : du[i];
                     step_row(R, tt, ll, -rp - gdu, rho + (ll / tt) * gdu);
                 }
             }
             // block k rows at X_{k+1}
-            double xn[NX], sg[NS];
+            double xn[NX], sg[NS], tB[MC], lB[MC];
 #pragma unroll
-            for (int s = 0; s < NX; ++s) xn[s] = X[(k + 1) * NX + s];
+            for (int s = 0; s < NX; ++s) xn[s] = im(buf, M::X + s);
 #pragma unroll
-            for (int j = 0; j < NS; ++j) sg[j] = sig[k * NS + j];
-            Blk q;
-            blk_rows(k, xn, sg, C, h, q);
-            double rc[MC], rho[MC], gdu[MC];
+            for (int qq = 0; qq < NS; ++qq) sg[qq] = im(buf, M::sig + qq);
 #pragma unroll
             for (int r = 0; r < MC; ++r) {
-                const int R = k * MC + r;
-                rc[r] = -q.tt[r] * q.ll[r];
-                if (pass && q.act[r]) rc[r] += sm - dta[R] * dla[R];
-                rho[r] = q.act[r] ? (rc[r] + q.ll[r] * q.rp[r]) / q.tt[r] : 0.0;
+                tB[r] = im(buf, M::tB + r);
+                lB[r] = im(buf, M::lB + r);
+            }
+            Blk q;
+            blk_rows(buf, xn, sg, tB, lB, q);
+            double rho[MC], gdu[MC];
+#pragma unroll
+            for (int r = 0; r < MC; ++r) {
+                double rc = -q.tt[r] * q.ll[r];
+                if (pass && q.act[r]) rc += sm - im(buf, M::aB + r) * im(buf, M::alB + r);
+                rho[r] = q.act[r] ? (rc + q.ll[r] * q.rp[r]) / q.tt[r] : 0.0;
                 double g = 0.0;
 #pragma unroll
-                for (int s = 0; s < NX; ++s) g = fma(C[r * NX + s], dx[s], g);
+                for (int s = 0; s < NX; ++s) g = fma(im(buf, M::C + r * NX + s), dx[s], g);
                 gdu[r] = g;
             }
             double ds[NS];
 #pragma unroll
-            for (int j = 0; j < NS; ++j) {
-                double v = q.rsig[j];
+            for (int qq = 0; qq < NS; ++qq) {
+                double v = q.rsig[qq];
 #pragma unroll
                 for (int r = 0; r < MC; ++r)
-                    if (c.row_slack[r] == j) v += (double)c.row_sign[r] * (rho[r] + q.th[r] * gdu[r]);
-                ds[j] = -v / q.Dsig[j];
-                if (pass) dsig[k * NS + j] = ds[j];
+                    if (c.row_slack[r] == qq) v += (double)c.row_sign[r] * (rho[r] + q.th[r] * gdu[r]);
+                ds[qq] = -v / q.Dsig[qq];
+                if (pass) dsig[k * NS + qq] = ds[qq];
             }
 #pragma unroll
             for (int r = 0; r < MC; ++r) {
@@ -777,98 +1016,128 @@ __host__ __device__ inline void lane_agent(const MpcConst& c, const MpcPtrs& P, 
                     }
                     continue;
                 }
-                const int j = c.row_slack[r];
-                const double sd = j >= 0 ? (double)c.row_sign[r] * ds[j] : 0.0;
+                const int jj = c.row_slack[r];
+                const double sd = jj >= 0 ? (double)c.row_sign[r] * ds[jj] : 0.0;
                 step_row(R, q.tt[r], q.ll[r], -q.rp[r] - gdu[r] - sd, rho[r] + q.th[r] * (gdu[r] + sd));
             }
+            img_wait();
+            LANE_PHASE();
         }
         return o;
     };
 
     // ============ S3: corrector right-hand side and backward solve ============
-    auto sweep3 = [&](auto rf_tag, double sm) {
+    // step jb = N .. 0: block part kb = jb - 1 (rt of its rows -> psi3_jb) after the stage part k = jb
+    // (rows of u_k, rhs, backward solve step with the stored gains)
+    auto s3_fetch = [&](auto rf_tag, int buf, int jb) {
+        if (jb <= N - 1) {
+            fd(buf, M::A, L.iA + (size_t)jb * NX * NX, NX * NX);
+            fd(buf, M::B, L.iB + (size_t)jb * NX * NU, NX * NU);
+            fd(buf, M::rd, L.rd + (size_t)jb * NU, NU);
+            fd(buf, M::U, L.U + (size_t)jb * NU, NU);
+            fd(buf, M::tI, L.t + ms + (size_t)jb * 2 * NU, 2 * NU);
+            fd(buf, M::lI, L.lam + ms + (size_t)jb * 2 * NU, 2 * NU);
+            fd(buf, M::aI, L.dta + ms + (size_t)jb * 2 * NU, 2 * NU);
+            fd(buf, M::alI, L.dla + ms + (size_t)jb * 2 * NU, 2 * NU);
+            fetchF(rf_tag, buf, jb);
+        }
+        if (jb >= 1) {
+            const int kb = jb - 1;
+            fd(buf, M::C, L.iC + (size_t)kb * MC * NX, MC * NX);
+            fd(buf, M::h, L.ih + (size_t)kb * MC, MC);
+            fd(buf, M::X, L.X + (size_t)jb * NX, NX);
+            fd(buf, M::sig, L.sig + (size_t)kb * NS, NS);
+            fd(buf, M::tB, L.t + (size_t)kb * MC, MC);
+            fd(buf, M::lB, L.lam + (size_t)kb * MC, MC);
+            fd(buf, M::aB, L.dta + (size_t)kb * MC, MC);
+            fd(buf, M::alB, L.dla + (size_t)kb * MC, MC);
+        }
+    };
+    auto sweep3 = [&](auto rf_tag, double sm) __attribute__((always_inline)) {
         using RF = decltype(rf_tag);
         RF pv[NA];
         double ps3[NX];
-        auto y3_of = [&](int kb, const double* C, const double* h, double* y3) {
-            double xn[NX], sg[NS];
 #pragma unroll
-            for (int s = 0; s < NX; ++s) xn[s] = X[(kb + 1) * NX + s];
+        for (int jj = 0; jj < NA; ++jj) pv[jj] = 0;
+        s3_fetch(rf_tag, N & 1, N);
+        img_wait();
+        for (int jb = N; jb >= 0; --jb) {
+            const int buf = jb & 1, k = jb;
+            if (jb >= 1) s3_fetch(rf_tag, buf ^ 1, jb - 1);
+            if (jb <= N - 1) {
+                double rtu[NU];
 #pragma unroll
-            for (int j = 0; j < NS; ++j) sg[j] = sig[kb * NS + j];
-            Blk q;
-            blk_rows(kb, xn, sg, C, h, q);
-            double rc[MC], rho[MC], rt[MC];
+                for (int i = 0; i < NU; ++i) {
+                    rtu[i] = 0.0;
+                    const double ukv = im(buf, M::U + i);
 #pragma unroll
-            for (int r = 0; r < MC; ++r) {
-                const int R = kb * MC + r;
-                rc[r] = q.act[r] ? -q.tt[r] * q.ll[r] + sm - dta[R] * dla[R] : 0.0;
+                    for (int q = 0; q < 2; ++q) {
+                        const double wv = w_in(i, q);
+                        if (!__builtin_isfinite(wv)) continue;
+                        const double tt = im(buf, M::tI + 2 * i + q), ll = im(buf, M::lI + 2 * i + q);
+                        const double rp = (q ? -ukv : ukv) + tt - wv;
+                        const double rc = -tt * ll + sm - im(buf, M::aI + 2 * i + q) * im(buf, M::alI + 2 * i + q);
+                        const double rho = (rc + ll * rp) / tt;
+                        rtu[i] += q ? -rho : rho;
+                    }
+                }
+                double rhs[NU];
+#pragma unroll
+                for (int i = 0; i < NU; ++i) {
+                    double g3 = 0.0;
+#pragma unroll
+                    for (int s = 0; s < NX; ++s) g3 = fma(im(buf, M::B + s * NU + i), ps3[s], g3);
+                    rhs[i] = -im(buf, M::rd + i) - (g3 + rtu[i]);
+                }
+                double dup[NU];
+                bsolve_img(rf_tag, buf, rhs, pv, dup);
+#pragma unroll
+                for (int i = 0; i < NU; ++i) dUp[k * NU + i] = dup[i];
             }
-            blk_rho(q, rc, rho, rt);
+            if (jb >= 1) {
+                double xn[NX], sg[NS], tB[MC], lB[MC];
 #pragma unroll
-            for (int s = 0; s < NX; ++s) {
-                double v3 = 0.0;
+                for (int s = 0; s < NX; ++s) xn[s] = im(buf, M::X + s);
 #pragma unroll
-                for (int r = 0; r < MC; ++r) v3 = fma(rt[r], C[r * NX + s], v3);
-                y3[s] = v3;
-            }
-        };
-        {
-            double C[MC * NX], h[MC];
-            loadC(N - 1, C, h);
-            y3_of(N - 1, C, h, ps3);
+                for (int qq = 0; qq < NS; ++qq) sg[qq] = im(buf, M::sig + qq);
 #pragma unroll
-            for (int j = 0; j < NA; ++j) pv[j] = 0;
-        }
-        for (int k = N - 1; k >= 0; --k) {
-            double A[NX * NX], Bm[NX * NU];
-            loadA(k, A);
-            loadB(k, Bm);
-            double rtu[NU];
+                for (int r = 0; r < MC; ++r) {
+                    tB[r] = im(buf, M::tB + r);
+                    lB[r] = im(buf, M::lB + r);
+                }
+                Blk q;
+                blk_rows(buf, xn, sg, tB, lB, q);
+                double rc[MC], rho[MC], rt[MC];
 #pragma unroll
-            for (int i = 0; i < NU; ++i) {
-                rtu[i] = 0.0;
-                const double uk = U[k * NU + i];
+                for (int r = 0; r < MC; ++r)
+                    rc[r] = q.act[r] ? -q.tt[r] * q.ll[r] + sm - im(buf, M::aB + r) * im(buf, M::alB + r) : 0.0;
+                blk_rho(q, rc, rho, rt);
+                double y3[NX];
 #pragma unroll
-                for (int q = 0; q < 2; ++q) {
-                    const int R = ms + 2 * (k * NU + i) + q;
-                    const double wv = w_in(i, q);
-                    if (!__builtin_isfinite(wv)) continue;
-                    const double tt = t[R], ll = lam[R];
-                    const double rp = (q ? -uk : uk) + tt - wv;
-                    const double rc = -tt * ll + sm - dta[R] * dla[R];
-                    const double rho = (rc + ll * rp) / tt;
-                    rtu[i] += q ? -rho : rho;
+                for (int s = 0; s < NX; ++s) {
+                    double v3 = 0.0;
+#pragma unroll
+                    for (int r = 0; r < MC; ++r) v3 = fma(rt[r], im(buf, M::C + r * NX + s), v3);
+                    y3[s] = v3;
+                }
+                if (jb == N) {
+#pragma unroll
+                    for (int s = 0; s < NX; ++s) ps3[s] = y3[s];
+                } else {
+                    double n3[NX];
+#pragma unroll
+                    for (int jj = 0; jj < NX; ++jj) {
+                        double a3 = y3[jj];
+#pragma unroll
+                        for (int s = 0; s < NX; ++s) a3 = fma(im(buf, M::A + s * NX + jj), ps3[s], a3);
+                        n3[jj] = a3;
+                    }
+#pragma unroll
+                    for (int jj = 0; jj < NX; ++jj) ps3[jj] = n3[jj];
                 }
             }
-            double rhs[NU];
-#pragma unroll
-            for (int i = 0; i < NU; ++i) {
-                double g3 = 0.0;
-#pragma unroll
-                for (int s = 0; s < NX; ++s) g3 = fma(Bm[s * NU + i], ps3[s], g3);
-                rhs[i] = -rd[k * NU + i] - (g3 + rtu[i]);
-            }
-            RF K[NU * NA], Hi[NU * NU];
-            loadF(k, K, Hi);
-            double dup[NU];
-            bsolve(K, Hi, A, Bm, rhs, pv, dup);
-#pragma unroll
-            for (int i = 0; i < NU; ++i) dUp[k * NU + i] = dup[i];
-            if (k == 0) break;
-            double C[MC * NX], h[MC], y3[NX];
-            loadC(k - 1, C, h);
-            y3_of(k - 1, C, h, y3);
-            double n3[NX];
-#pragma unroll
-            for (int j = 0; j < NX; ++j) {
-                double a3 = y3[j];
-#pragma unroll
-                for (int s = 0; s < NX; ++s) a3 = fma(A[s * NX + j], ps3[s], a3);
-                n3[j] = a3;
-            }
-#pragma unroll
-            for (int j = 0; j < NX; ++j) ps3[j] = n3[j];
+            img_wait();
+            LANE_PHASE();
         }
     };
 
@@ -879,19 +1148,19 @@ __host__ __device__ inline void lane_agent(const MpcConst& c, const MpcPtrs& P, 
     double alpha_prev = 1.0, alpha = 0.0;
     bool pending = false;  // a step (alpha, dU, dX, dsig, dt, dl) waits to be applied by S1
     // the sweeps in this agent's current precision (the fp32 instantiations exist only when MIXED)
-    auto run1 = [&](bool apply, double al) -> S1Out {
+    auto run1 = [&](bool apply, double al) __attribute__((always_inline)) -> S1Out {
         if constexpr (MIXED) {
             if (f32) return sweep1(0.0f, apply, al);
         }
         return sweep1(0.0, apply, al);
     };
-    auto run_fwd = [&](int pass, double sm) -> FwdOut {
+    auto run_fwd = [&](int pass, double sm) __attribute__((always_inline)) -> FwdOut {
         if constexpr (MIXED) {
             if (f32) return sweep_fwd(0.0f, pass, sm);
         }
         return sweep_fwd(0.0, pass, sm);
     };
-    auto run3 = [&](double sm) {
+    auto run3 = [&](double sm) __attribute__((always_inline)) {
         if constexpr (MIXED) {
             if (f32) {
                 sweep3(0.0f, sm);
@@ -954,7 +1223,7 @@ __host__ __device__ inline void lane_agent(const MpcConst& c, const MpcPtrs& P, 
         for (int bt = 0; bt < kMaxBacktrack && mact; ++bt) {
             double mn = 0.0, pmin = INFINITY;
             for (int R = 0; R < m; ++R) {
-                const bool act = R < ms ? __builtin_isfinite(gh[R]) : __builtin_isfinite(w_in(((R - ms) >> 1) % NU, (R - ms) & 1));
+                const bool act = R < ms ? __builtin_isfinite((double)gh[R]) : __builtin_isfinite(w_in(((R - ms) >> 1) % NU, (R - ms) & 1));
                 if (!act) continue;
                 const double pr = (t[R] + al * dt[R]) * (lam[R] + al * dl[R]);
                 mn += pr;
@@ -990,9 +1259,7 @@ __host__ __device__ inline void lane_agent(const MpcConst& c, const MpcPtrs& P, 
 #pragma unroll
     for (int j = 0; j < NS; ++j) z[NX + j] = 0.0;
     for (int k = 0; k < N; ++k) {
-        double A[NX * NX], Bm[NX * NU], u[NU];
-        loadA(k, A);
-        loadB(k, Bm);
+        double u[NU];
 #pragma unroll
         for (int i = 0; i < NU; ++i) u[i] = U[k * NU + i];
         double xn[NX];
@@ -1000,9 +1267,9 @@ __host__ __device__ inline void lane_agent(const MpcConst& c, const MpcPtrs& P, 
         for (int s = 0; s < NX; ++s) {
             double v = 0.0;
 #pragma unroll
-            for (int q = 0; q < NX; ++q) v += A[s * NX + q] * x[q];
+            for (int q = 0; q < NX; ++q) v += (double)gA[k * NX * NX + s * NX + q] * x[q];
 #pragma unroll
-            for (int i = 0; i < NU; ++i) v += Bm[s * NU + i] * u[i];
+            for (int i = 0; i < NU; ++i) v += (double)gB[k * NX * NU + s * NU + i] * u[i];
             xn[s] = v;
         }
 #pragma unroll

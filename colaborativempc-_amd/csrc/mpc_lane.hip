@@ -36,10 +36,13 @@
 
 namespace cmpc {
 
+// One wavefront per kLaneAP agents (lanes kLaneAP..63 leave at once); dynamic LDS: its two stage images.
 template <int NX, int NU, int MC, int NS, bool MIXED>
 __global__ __launch_bounds__(kWave) void mpc_lane_kernel(const MpcConst c, const MpcPtrs P, int batch) {
-    const int b = blockIdx.x * kWave + threadIdx.x;
-    if (b < batch) lane_agent<NX, NU, MC, NS, MIXED>(c, P, batch, b);
+    extern __shared__ __attribute__((aligned(16))) char lane_smem[];
+    if (threadIdx.x >= kLaneAP) return;
+    const int b = blockIdx.x * kLaneAP + threadIdx.x;
+    if (b < batch) lane_agent<NX, NU, MC, NS, MIXED>(c, P, batch, b, lane_smem);
 }
 
 size_t mpc_lane_ws_doubles(const MpcConst& c) { return lane_layout(c).total; }
@@ -70,9 +73,13 @@ static hipError_t lane_pack(const double* src, double* dst, int batch, int T, hi
 template <int NX, int NU, int MC, int NS>
 static bool lane_try(const MpcConst& c, const MpcPtrs& p, int batch, hipStream_t s, hipError_t* e) {
     if (c.nx != NX || c.nu != NU || c.mc != MC || c.ns != NS) return false;
-    const dim3 grid((batch + kWave - 1) / kWave);
-    if (c.lane == 2) hipLaunchKernelGGL((mpc_lane_kernel<NX, NU, MC, NS, true>), grid, dim3(kWave), 0, s, c, p, batch);
-    else hipLaunchKernelGGL((mpc_lane_kernel<NX, NU, MC, NS, false>), grid, dim3(kWave), 0, s, c, p, batch);
+    const dim3 grid((batch + kLaneAP - 1) / kLaneAP);
+    const size_t lds = 2 * (size_t)IMap<NX, NU, MC, NS>::bytes;
+    const void* fn = c.lane == 2 ? (const void*)mpc_lane_kernel<NX, NU, MC, NS, true>
+                                 : (const void*)mpc_lane_kernel<NX, NU, MC, NS, false>;
+    if ((*e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds)) != hipSuccess) return true;
+    if (c.lane == 2) hipLaunchKernelGGL((mpc_lane_kernel<NX, NU, MC, NS, true>), grid, dim3(kWave), lds, s, c, p, batch);
+    else hipLaunchKernelGGL((mpc_lane_kernel<NX, NU, MC, NS, false>), grid, dim3(kWave), lds, s, c, p, batch);
     *e = hipGetLastError();
     return true;
 }

@@ -24,6 +24,7 @@ def main():
     ap.add_argument("--sample", type=int, default=128)
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--no-oracle", action="store_true")
+    ap.add_argument("--only", default=None, help="run one solver only: riccati_f64 | lane_f64 | lane_fp32")
     a = ap.parse_args()
     import torch
 
@@ -62,6 +63,10 @@ def main():
                          iters_mean=float(it.mean()), iters_max=int(it.max()))
         return z, st, it
 
+    if a.only:
+        flags = dict(riccati_f64=L.CMPC_FLAG_RICCATI, lane_f64=L.CMPC_FLAG_LANE, lane_fp32=L.CMPC_FLAG_FP32)[a.only]
+        run(a.only, flags, 1e-6 if a.only == "lane_fp32" else None)
+        return
     zr, sr, _ = run("riccati_f64", L.CMPC_FLAG_RICCATI)
     zl, sl, _ = run("lane_f64", L.CMPC_FLAG_LANE)
     zf, sf, _ = run("lane_fp32", L.CMPC_FLAG_FP32, 1e-6)

@@ -41,11 +41,11 @@ extern "C" int lane_cpu_solve(int nx, int nu, int N, int ns, int mc, int batch, 
     P.z = z; P.kkt = kkt; P.iters = iters; P.status = status; P.ws = ws.data();
     for (int b = 0; b < batch; ++b) {
         if (nx == 6 && nu == 3 && mc == 6 && ns == 3) {
-            if (mixed) lane_agent<6, 3, 6, 3, true>(c, P, batch, b);
-            else lane_agent<6, 3, 6, 3, false>(c, P, batch, b);
+            if (mixed) lane_agent<6, 3, 6, 3, true>(c, P, batch, b, nullptr);
+            else lane_agent<6, 3, 6, 3, false>(c, P, batch, b, nullptr);
         } else if (nx == 4 && nu == 2 && mc == 6 && ns == 3) {
-            if (mixed) lane_agent<4, 2, 6, 3, true>(c, P, batch, b);
-            else lane_agent<4, 2, 6, 3, false>(c, P, batch, b);
+            if (mixed) lane_agent<4, 2, 6, 3, true>(c, P, batch, b, nullptr);
+            else lane_agent<4, 2, 6, 3, false>(c, P, batch, b, nullptr);
         } else {
             return -1;
         }
