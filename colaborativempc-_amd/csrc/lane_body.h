@@ -14,36 +14,42 @@ namespace {
 
 constexpr int kF32Stall = 2;  // fp32 iterations without a new best iterate before an agent goes fp64
 
-// Lane-interleaved view: element i of this lane's agent at byte (region + i) * batch * sizeof(T) +
-// b * sizeof(T) of the scratch.  On the device every access is a raw buffer load / store whose
-// element offset is a wave-uniform SGPR and whose lane offset is one VGPR for all arrays (plain
-// 64-bit addresses per element made the compiler precompute and spill hundreds of them); on the
-// host (tools/lane_cpu.cpp) a pointer.  Accesses go through a small proxy (read / assign).
+// Lane-interleaved view, in PAIRS: elements 2p and 2p+1 of agent b sit side by side at double
+// index (p * batch + b) * 2 (+1) of the scratch (floats in quads: (q * batch + b) * 4 + w), so that
+// one 16-byte load per lane brings two elements of that lane's OWN agent — the stage images below
+// are filled per lane, and a lane whose agent has converged (inactive) does not leave a hole in
+// another agent's image.  On the device every access is a raw buffer load / store whose element
+// offset is a wave-uniform SGPR and whose lane offset (b * 16 bytes) is one VGPR for all arrays; on
+// the host (tools/lane_cpu.cpp) a pointer.  Accesses go through a small proxy (read / assign).
 template <class T>
 struct LV {
+    static constexpr unsigned G = 16 / sizeof(T);  // elements per 16-byte group
 #if defined(__HIP_DEVICE_COMPILE__)
     __amdgpu_buffer_rsrc_t r;
-    unsigned base, s, vo;  // region start (elements of T), batch stride, lane byte offset
+    unsigned base, s, vo;  // region start (elements of T, a multiple of G), batch, lane byte offset b * 16
+    __device__ __forceinline__ int soff(int i) const {
+        const unsigned a = base + (unsigned)i;
+        return (int)((a / G) * s * 16u + (a % G) * (unsigned)sizeof(T));
+    }
     __device__ __forceinline__ T ld(int i) const {
-        const int so = (int)((base + (unsigned)i) * s * (unsigned)sizeof(T));
         if constexpr (sizeof(T) == 8)
-            return __builtin_bit_cast(T, __builtin_amdgcn_raw_buffer_load_b64(r, (int)vo, so, 0));
+            return __builtin_bit_cast(T, __builtin_amdgcn_raw_buffer_load_b64(r, (int)vo, soff(i), 0));
         else
-            return __builtin_bit_cast(T, __builtin_amdgcn_raw_buffer_load_b32(r, (int)vo, so, 0));
+            return __builtin_bit_cast(T, __builtin_amdgcn_raw_buffer_load_b32(r, (int)vo, soff(i), 0));
     }
     __device__ __forceinline__ void st(int i, T v) const {
-        const int so = (int)((base + (unsigned)i) * s * (unsigned)sizeof(T));
         if constexpr (sizeof(T) == 8)
             __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(__attribute__((ext_vector_type(2))) unsigned, v), r,
-                                                  (int)vo, so, 0);
+                                                  (int)vo, soff(i), 0);
         else
-            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), r, (int)vo, so, 0);
+            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), r, (int)vo, soff(i), 0);
     }
 #else
-    T* p;
-    size_t s;
-    T ld(int i) const { return p[(size_t)i * s]; }
-    void st(int i, T v) const { p[(size_t)i * s] = v; }
+    T* p;        // the region's group 0 of agent b
+    size_t s;    // batch
+    size_t idx(int i) const { return ((size_t)i / G) * s * G + (size_t)i % G; }
+    T ld(int i) const { return p[idx(i)]; }
+    void st(int i, T v) const { p[idx(i)] = v; }
 #endif
     struct Ref {
         const LV* v;
@@ -63,38 +69,44 @@ struct LV {
 
 struct LaneLayout {
     size_t X, U, sig, t, lam, bU, bsig, rd, dUp, Fd, dta, dla, dU, dX, dsig, dt, dl, Ff;
-    size_t iA, iB, iC, ih, ip;  // the inputs, lane-interleaved by lane_pack (mpc_lane.hip)
+    size_t iA, iB, iC, ih, ip;  // the inputs, pair-interleaved by lane_pack (mpc_lane.hip)
     size_t total;
+    int nup, nsp;               // per-stage strides of the input-like (U, dU, rd, dUp) and slack arrays
 };
+
+__host__ __device__ constexpr int lane_ev(int x) { return (x + 1) & ~1; }
 
 __host__ __device__ inline LaneLayout lane_layout(const MpcConst& c) {
     LaneLayout L;
-    const size_t N = c.N, nx = c.nx, nu = c.nu, ns = c.ns, m = c.m, n = c.n;
+    const size_t N = c.N, nx = c.nx, nu = c.nu, m = c.m;
+    const size_t nup = lane_ev(c.nu), nsp = lane_ev(c.ns);
+    L.nup = (int)nup;
+    L.nsp = (int)nsp;
     const size_t sF = nu * (nx + nu) + nu * nu;
     size_t o = 0;
-    auto take = [&](size_t cnt) {
+    auto take = [&](size_t cnt) {  // regions start on a pair
         const size_t r = o;
-        o += cnt;
+        o += (cnt + 1) & ~(size_t)1;
         return r;
     };
     L.X = take((N + 1) * nx);
-    L.U = take(n);
-    L.sig = take(N * ns);
+    L.U = take(N * nup);
+    L.sig = take(N * nsp);
     L.t = take(m);
     L.lam = take(m);
-    L.bU = take(n);
-    L.bsig = take(N * ns);
-    L.rd = take(n);
-    L.dUp = take(n);
+    L.bU = take(N * nup);
+    L.bsig = take(N * nsp);
+    L.rd = take(N * nup);
+    L.dUp = take(N * nup);
     L.Fd = take(N * sF);
     L.dta = take(m);
     L.dla = take(m);
-    L.dU = take(n);
+    L.dU = take(N * nup);
     L.dX = take((N + 1) * nx);
-    L.dsig = take(N * ns);
+    L.dsig = take(N * nsp);
     L.dt = take(m);
     L.dl = take(m);
-    L.Ff = take((N * sF + 1) / 2);  // floats
+    L.Ff = take((N * sF + 3) / 4 * 2);  // floats, in quads (Ff * 2 is a multiple of 4)
     L.iA = take(N * nx * nx);
     L.iB = take(N * nx * nu);
     L.iC = take(N * c.mc * nx);
@@ -124,7 +136,7 @@ __host__ __device__ constexpr int sy(int i, int j) { return i >= j ? i * (i + 1)
 // (the other 32 lanes exit at once): an image row is one element for those agents, 256 bytes, and
 // one dwordx4 LDS load of 32 lanes fills two rows.  The map below (rows; runs start on even rows,
 // float runs on multiples of 4 float rows) is the union of what the sweeps fetch.
-constexpr int kLaneAP = 32;
+constexpr int kLaneAP = 32;  // agents per wavefront (measured at 8192 agents: 32 -> 106 ms, 8 -> 129 ms, 4 -> 208 ms)
 
 template <int NX, int NU, int MC, int NS>
 struct IMap {
@@ -132,6 +144,7 @@ struct IMap {
     static constexpr int ev(int x) { return (x + 1) & ~1; }
     static constexpr int A = 0, B = A + ev(NX * NX), C = B + ev(NX * NU), h = C + ev(MC * NX), p = h + ev(MC);
     static constexpr int X = p + ev(NX), U = X + ev(NX), sig = U + ev(NU), tB = sig + ev(NS), lB = tB + ev(MC);
+    static_assert(NX % 2 == 0 && MC % 2 == 0 && SF % 4 == 0, "pair layout: even NX, MC; SF a multiple of 4");
     static constexpr int tI = lB + ev(MC), lI = tI + ev(2 * NU), dX = lI + ev(2 * NU), dsig = dX + ev(NX);
     static constexpr int dtB = dsig + ev(NS), dlB = dtB + ev(MC), dU = dlB + ev(MC), dtI = dU + ev(NU);
     static constexpr int dlI = dtI + ev(2 * NU), rd = dlI + ev(2 * NU), dUp = rd + ev(NU), aB = dUp + ev(NU);
@@ -156,6 +169,7 @@ template <int NX, int NU, int MC, int NS, bool MIXED>
 __host__ __device__ inline void lane_agent(const MpcConst& c, const MpcPtrs& P, int batch, int b, char* smem) {
     using M = IMap<NX, NU, MC, NS>;
     constexpr int NA = NX + NU, SF = M::SF;
+    constexpr int NUP = lane_ev(NU), NSP = lane_ev(NS);  // per-stage strides of U-like / slack arrays
     const int N = c.N, ms = c.ms, m = c.m;
     const LaneLayout L = lane_layout(c);
     const size_t S = (size_t)batch;
@@ -167,44 +181,47 @@ __host__ __device__ inline void lane_agent(const MpcConst& c, const MpcPtrs& P, 
         __builtin_amdgcn_make_buffer_rsrc(ws, 0, (int)(L.total * S * 8 < 0x7fffffffull ? L.total * S * 8 : 0x7fffffffull),
                                           0x00020000);
     const unsigned Su = (unsigned)S;
-    auto mk = [&](size_t region) { return LV<double>{rs, (unsigned)region, Su, (unsigned)b * 8u}; };
-    const LV<float> Ff{rs, (unsigned)(2 * L.Ff), Su, (unsigned)b * 4u};  // float elements from byte 8 * Ff * S
-    const unsigned b0 = (unsigned)(b - j);
-    // lane offsets of the image fills: 2 double rows (16 lanes x 16 B each) / 4 float rows per instruction
-    const int vo_d = (int)((((unsigned)j >> 4) * Su + b0 + 2u * ((unsigned)j & 15u)) * 8u);
-    const int vo_f = (int)((((unsigned)j >> 3) * Su + b0 + 4u * ((unsigned)j & 7u)) * 4u);
-    // image rows (double run of cnt rows from global element ge, float run from float element gf)
-    auto fd = [&](int buf, int row, size_t ge, int cnt) {
-        char* dst = smem + buf * M::bytes + row * (kLaneAP * 8);
+    auto mk = [&](size_t region) { return LV<double>{rs, (unsigned)region, Su, (unsigned)b * 16u}; };
+    const LV<float> Ff{rs, (unsigned)(2 * L.Ff), Su, (unsigned)b * 16u};  // float elements from float index 2 * Ff
+    // image fills: per lane 16 bytes of its own agent (a pair of double rows / a quad of float rows)
+    const int vo = (int)((unsigned)b * 16u);
+    auto fd = [&](int buf, int row, size_t ge, int cnt) {  // ge, row even
+        char* dst = smem + buf * M::bytes + (row >> 1) * (kLaneAP * 16);
         for (int q = 0; q < cnt; q += 2)
-            __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)(dst + q * (kLaneAP * 8)),
-                                                     16, vo_d, (int)((ge + q) * Su * 8u), 0, 0);
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)(dst + (q >> 1) * (kLaneAP * 16)),
+                                                     16, vo, (int)((ge + q) / 2 * Su * 16u), 0, 0);
     };
-    auto ff = [&](int buf, size_t gf, int cnt) {
+    auto ff = [&](int buf, size_t gf, int cnt) {  // gf a multiple of 4
         char* dst = smem + buf * M::bytes + M::rows * (kLaneAP * 8);
         for (int q = 0; q < cnt; q += 4)
-            __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)(dst + q * (kLaneAP * 4)),
-                                                     16, vo_f, (int)((gf + q) * Su * 4u), 0, 0);
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)(dst + (q >> 2) * (kLaneAP * 16)),
+                                                     16, vo, (int)((gf + q) / 4 * Su * 16u), 0, 0);
     };
     const double* imd0 = reinterpret_cast<const double*>(smem);
-    auto im = [&](int buf, int row) -> double { return imd0[buf * (M::bytes / 8) + row * kLaneAP + j]; };
-    auto imf = [&](int buf, int row) -> float {
-        return reinterpret_cast<const float*>(smem + buf * M::bytes + M::rows * (kLaneAP * 8))[row * kLaneAP + j];
+    auto im = [&](int buf, int row) -> double {
+        return imd0[buf * (M::bytes / 8) + (row >> 1) * (2 * kLaneAP) + 2 * j + (row & 1)];
     };
-    // every image fill (and store) of this wavefront retired
-    auto img_wait = [&]() { __builtin_amdgcn_s_waitcnt(0x0F70); };
+    auto imf = [&](int buf, int row) -> float {
+        return reinterpret_cast<const float*>(smem + buf * M::bytes + M::rows * (kLaneAP * 8))[(row >> 2) * (4 * kLaneAP) +
+                                                                                               4 * j + (row & 3)];
+    };
+    // every image fill (and store) of this wavefront retired and every LDS read of the image done; a
+    // compiler memory barrier too, so no image read moves above it (the LDS-DMA writes are invisible
+    // to the compiler's dependence tracking)
+    auto img_wait = [&]() { asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory"); };
 #else
     (void)smem;
-    auto mk = [&](size_t region) { return LV<double>{ws + region * S + b, S}; };
-    const LV<float> Ff{reinterpret_cast<float*>(ws + L.Ff * S) + b, S};
+    auto mk = [&](size_t region) { return LV<double>{ws + region * S + 2 * (size_t)b, S}; };
+    const LV<float> Ff{reinterpret_cast<float*>(ws + L.Ff * S) + 4 * (size_t)b, S};
     double hd[2][M::rows];
     float hf[2][M::frows];
     auto fd = [&](int buf, int row, size_t ge, int cnt) {
-        for (int q = 0; q < cnt; ++q) hd[buf][row + q] = ws[(ge + q) * S + b];
+        const LV<double> v{ws + 2 * (size_t)b, S};
+        for (int q = 0; q < cnt; ++q) hd[buf][row + q] = v.ld((int)(ge + q));
     };
     auto ff = [&](int buf, size_t gf, int cnt) {
-        const float* f = reinterpret_cast<const float*>(ws);
-        for (int q = 0; q < cnt; ++q) hf[buf][q] = f[(gf + q) * S + b];
+        const LV<float> v{reinterpret_cast<float*>(ws) + 4 * (size_t)b, S};
+        for (int q = 0; q < cnt; ++q) hf[buf][q] = v.ld((int)(gf + q));
     };
     auto im = [&](int buf, int row) -> double { return hd[buf][row]; };
     auto imf = [&](int buf, int row) -> float { return hf[buf][row]; };
@@ -248,9 +265,9 @@ __host__ __device__ inline void lane_agent(const MpcConst& c, const MpcPtrs& P, 
                 X[(k + 1) * NX + s] = xn[s];
             }
 #pragma unroll
-            for (int i = 0; i < NU; ++i) U[k * NU + i] = 0.0;
+            for (int i = 0; i < NU; ++i) U[k * NUP + i] = 0.0;
 #pragma unroll
-            for (int q = 0; q < NS; ++q) sig[k * NS + q] = 0.0;
+            for (int q = 0; q < NS; ++q) sig[k * NSP + q] = 0.0;
 #pragma unroll
             for (int r = 0; r < MC; ++r) {
                 const int R = k * MC + r;
@@ -470,18 +487,18 @@ __host__ __device__ inline void lane_agent(const MpcConst& c, const MpcPtrs& P, 
             fd(buf, M::h, L.ih + (size_t)kb * MC, MC);
             fd(buf, M::p, L.ip + (size_t)jb * NX, NX);
             fd(buf, M::X, L.X + (size_t)jb * NX, NX);
-            fd(buf, M::sig, L.sig + (size_t)kb * NS, NS);
+            fd(buf, M::sig, L.sig + (size_t)kb * NSP, NS);
             fd(buf, M::tB, L.t + (size_t)kb * MC, MC);
             fd(buf, M::lB, L.lam + (size_t)kb * MC, MC);
-            fd(buf, M::U, L.U + (size_t)kb * NU, NU);
+            fd(buf, M::U, L.U + (size_t)kb * NUP, NU);
             fd(buf, M::tI, L.t + ms + (size_t)kb * 2 * NU, 2 * NU);
             fd(buf, M::lI, L.lam + ms + (size_t)kb * 2 * NU, 2 * NU);
             if (apply) {
                 fd(buf, M::dX, L.dX + (size_t)jb * NX, NX);
-                fd(buf, M::dsig, L.dsig + (size_t)kb * NS, NS);
+                fd(buf, M::dsig, L.dsig + (size_t)kb * NSP, NS);
                 fd(buf, M::dtB, L.dt + (size_t)kb * MC, MC);
                 fd(buf, M::dlB, L.dl + (size_t)kb * MC, MC);
-                fd(buf, M::dU, L.dU + (size_t)kb * NU, NU);
+                fd(buf, M::dU, L.dU + (size_t)kb * NUP, NU);
                 fd(buf, M::dtI, L.dt + ms + (size_t)kb * 2 * NU, 2 * NU);
                 fd(buf, M::dlI, L.dl + ms + (size_t)kb * 2 * NU, 2 * NU);
             }
@@ -530,7 +547,7 @@ __host__ __device__ inline void lane_agent(const MpcConst& c, const MpcPtrs& P, 
 #pragma unroll
                     for (int q = 0; q < NS; ++q) {
                         sg[q] = fma(al, im(buf, M::dsig + q), sg[q]);
-                        sig[kb * NS + q] = sg[q];
+                        sig[kb * NSP + q] = sg[q];
                     }
 #pragma unroll
                     for (int r = 0; r < MC; ++r)
@@ -543,7 +560,7 @@ __host__ __device__ inline void lane_agent(const MpcConst& c, const MpcPtrs& P, 
 #pragma unroll
                     for (int i = 0; i < NU; ++i) {
                         um[i] = fma(al, im(buf, M::dU + i), um[i]);
-                        U[kb * NU + i] = um[i];
+                        U[kb * NUP + i] = um[i];
                     }
 #pragma unroll
                     for (int i = 0; i < 2 * NU; ++i)
@@ -596,7 +613,7 @@ __host__ __device__ inline void lane_agent(const MpcConst& c, const MpcPtrs& P, 
                     o.gsc = lane_nmax(o.gsc, fabs(gf + rr));
                     const double rdv = gd + rr + lamu[i];
                     o.nrd = lane_nmax(o.nrd, fabs(rdv));
-                    rd[k * NU + i] = rdv;
+                    rd[k * NUP + i] = rdv;
                     rhs[i] = -rdv - (g3 + rtu[i]);
                 }
             }
@@ -781,7 +798,7 @@ __host__ __device__ inline void lane_agent(const MpcConst& c, const MpcPtrs& P, 
                             RF v = 0;
 #pragma unroll
                             for (int e = 0; e < NU; ++e) v -= Hi[cc * NU + e] * g[e];
-                            dUp[k * NU + cc] = (double)v;
+                            dUp[k * NUP + cc] = (double)v;
                         }
 #pragma unroll
                         for (int jj = 0; jj < NA; ++jj) {
@@ -868,13 +885,13 @@ __host__ __device__ inline void lane_agent(const MpcConst& c, const MpcPtrs& P, 
         fd(buf, M::C, L.iC + (size_t)k * MC * NX, MC * NX);
         fd(buf, M::h, L.ih + (size_t)k * MC, MC);
         fd(buf, M::X, L.X + (size_t)(k + 1) * NX, NX);
-        fd(buf, M::U, L.U + (size_t)k * NU, NU);
-        fd(buf, M::sig, L.sig + (size_t)k * NS, NS);
+        fd(buf, M::U, L.U + (size_t)k * NUP, NU);
+        fd(buf, M::sig, L.sig + (size_t)k * NSP, NS);
         fd(buf, M::tB, L.t + (size_t)k * MC, MC);
         fd(buf, M::lB, L.lam + (size_t)k * MC, MC);
         fd(buf, M::tI, L.t + ms + (size_t)k * 2 * NU, 2 * NU);
         fd(buf, M::lI, L.lam + ms + (size_t)k * 2 * NU, 2 * NU);
-        fd(buf, M::dUp, L.dUp + (size_t)k * NU, NU);
+        fd(buf, M::dUp, L.dUp + (size_t)k * NUP, NU);
         fetchF(rf_tag, buf, k);
         if (pass) {
             fd(buf, M::aB, L.dta + (size_t)k * MC, MC);
@@ -944,7 +961,7 @@ __host__ __device__ inline void lane_agent(const MpcConst& c, const MpcPtrs& P, 
             for (int s = 0; s < NX; ++s) dx[s] = dxn[s];
             if (pass) {
 #pragma unroll
-                for (int cc = 0; cc < NU; ++cc) dU[k * NU + cc] = du[cc];
+                for (int cc = 0; cc < NU; ++cc) dU[k * NUP + cc] = du[cc];
 #pragma unroll
                 for (int s = 0; s < NX; ++s) dX[(k + 1) * NX + s] = dx[s];
             }
@@ -1004,7 +1021,7 @@ __host__ __device__ inline void lane_agent(const MpcConst& c, const MpcPtrs& P, 
                 for (int r = 0; r < MC; ++r)
                     if (c.row_slack[r] == qq) v += (double)c.row_sign[r] * (rho[r] + q.th[r] * gdu[r]);
                 ds[qq] = -v / q.Dsig[qq];
-                if (pass) dsig[k * NS + qq] = ds[qq];
+                if (pass) dsig[k * NSP + qq] = ds[qq];
             }
 #pragma unroll
             for (int r = 0; r < MC; ++r) {
@@ -1033,8 +1050,8 @@ __host__ __device__ inline void lane_agent(const MpcConst& c, const MpcPtrs& P, 
         if (jb <= N - 1) {
             fd(buf, M::A, L.iA + (size_t)jb * NX * NX, NX * NX);
             fd(buf, M::B, L.iB + (size_t)jb * NX * NU, NX * NU);
-            fd(buf, M::rd, L.rd + (size_t)jb * NU, NU);
-            fd(buf, M::U, L.U + (size_t)jb * NU, NU);
+            fd(buf, M::rd, L.rd + (size_t)jb * NUP, NU);
+            fd(buf, M::U, L.U + (size_t)jb * NUP, NU);
             fd(buf, M::tI, L.t + ms + (size_t)jb * 2 * NU, 2 * NU);
             fd(buf, M::lI, L.lam + ms + (size_t)jb * 2 * NU, 2 * NU);
             fd(buf, M::aI, L.dta + ms + (size_t)jb * 2 * NU, 2 * NU);
@@ -1046,7 +1063,7 @@ __host__ __device__ inline void lane_agent(const MpcConst& c, const MpcPtrs& P, 
             fd(buf, M::C, L.iC + (size_t)kb * MC * NX, MC * NX);
             fd(buf, M::h, L.ih + (size_t)kb * MC, MC);
             fd(buf, M::X, L.X + (size_t)jb * NX, NX);
-            fd(buf, M::sig, L.sig + (size_t)kb * NS, NS);
+            fd(buf, M::sig, L.sig + (size_t)kb * NSP, NS);
             fd(buf, M::tB, L.t + (size_t)kb * MC, MC);
             fd(buf, M::lB, L.lam + (size_t)kb * MC, MC);
             fd(buf, M::aB, L.dta + (size_t)kb * MC, MC);
@@ -1092,7 +1109,7 @@ __host__ __device__ inline void lane_agent(const MpcConst& c, const MpcPtrs& P, 
                 double dup[NU];
                 bsolve_img(rf_tag, buf, rhs, pv, dup);
 #pragma unroll
-                for (int i = 0; i < NU; ++i) dUp[k * NU + i] = dup[i];
+                for (int i = 0; i < NU; ++i) dUp[k * NUP + i] = dup[i];
             }
             if (jb >= 1) {
                 double xn[NX], sg[NS], tB[MC], lB[MC];
@@ -1188,8 +1205,8 @@ __host__ __device__ inline void lane_agent(const MpcConst& c, const MpcPtrs& P, 
             best_m = merit;
             best_kkt = kkt;
             best_it = it;
-            for (int i = 0; i < c.n; ++i) bU[i] = U[i];
-            for (int i = 0; i < N * NS; ++i) bsig[i] = sig[i];
+            for (int i = 0; i < N * NUP; ++i) bU[i] = U[i];
+            for (int i = 0; i < N * NSP; ++i) bsig[i] = sig[i];
         }
         if (merit < tol) {
             stop = kStopConverged;
@@ -1240,8 +1257,8 @@ __host__ __device__ inline void lane_agent(const MpcConst& c, const MpcPtrs& P, 
     int status = CMPC_SOLVED;
     if (stop != kStopConverged) {
         if (best_it > 0) {
-            for (int i = 0; i < c.n; ++i) U[i] = bU[i];
-            for (int i = 0; i < N * NS; ++i) sig[i] = bsig[i];
+            for (int i = 0; i < N * NUP; ++i) U[i] = bU[i];
+            for (int i = 0; i < N * NSP; ++i) sig[i] = bsig[i];
             kkt = best_kkt;
         }
         status = stop_status(stop, best_m, tol);
@@ -1261,7 +1278,7 @@ __host__ __device__ inline void lane_agent(const MpcConst& c, const MpcPtrs& P, 
     for (int k = 0; k < N; ++k) {
         double u[NU];
 #pragma unroll
-        for (int i = 0; i < NU; ++i) u[i] = U[k * NU + i];
+        for (int i = 0; i < NU; ++i) u[i] = U[k * NUP + i];
         double xn[NX];
 #pragma unroll
         for (int s = 0; s < NX; ++s) {
@@ -1278,11 +1295,11 @@ __host__ __device__ inline void lane_agent(const MpcConst& c, const MpcPtrs& P, 
             z[(size_t)(k + 1) * nxe + s] = x[s];
         }
 #pragma unroll
-        for (int j = 0; j < NS; ++j) z[(size_t)(k + 1) * nxe + NX + j] = sig[k * NS + j];
+        for (int j = 0; j < NS; ++j) z[(size_t)(k + 1) * nxe + NX + j] = sig[k * NSP + j];
 #pragma unroll
         for (int i = 0; i < NU; ++i) {
             z[(size_t)(N + 1) * nxe + k * NU + i] = u[i];
-            z[(size_t)(N + 1) * nxe + c.n + k * NU + i] = u[i] - (k ? U[(k - 1) * NU + i] : up[i]);
+            z[(size_t)(N + 1) * nxe + c.n + k * NU + i] = u[i] - (k ? U[(k - 1) * NUP + i] : up[i]);
         }
     }
     if (P.kkt) P.kkt[b] = kkt;

@@ -47,8 +47,9 @@ __global__ __launch_bounds__(kWave) void mpc_lane_kernel(const MpcConst c, const
 
 size_t mpc_lane_ws_doubles(const MpcConst& c) { return lane_layout(c).total; }
 
-// dst[e * batch + b] = src[b * T + e]: agent-major inputs -> lane-interleaved copy, through a
-// 64 x 64 LDS tile so both the reads (along e) and the writes (along b) are coalesced
+// agent-major inputs -> the pair-interleaved copy of lane_body.h (element e of agent b at
+// ((e / 2) * batch + b) * 2 + e % 2), through a 64 x 64 LDS tile so that the reads (along e) and
+// the writes (along b) are both coalesced
 __global__ __launch_bounds__(256) void lane_pack_kernel(const double* __restrict__ src, double* __restrict__ dst,
                                                         int batch, int T) {
     __shared__ double tile[64][65];
@@ -60,7 +61,7 @@ __global__ __launch_bounds__(256) void lane_pack_kernel(const double* __restrict
     __syncthreads();
     for (int r = ty; r < 64; r += 4) {
         const int e = e0 + r, b = b0 + tx;
-        if (b < batch && e < T) dst[(size_t)e * batch + b] = tile[tx][r];
+        if (b < batch && e < T) dst[((size_t)(e >> 1) * batch + b) * 2 + (e & 1)] = tile[tx][r];
     }
 }
 

@@ -24,6 +24,7 @@ def main():
     ap.add_argument("--sample", type=int, default=128)
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--no-oracle", action="store_true")
+    ap.add_argument("--lanes", action="store_true", help="histogram of unsolved agents over the lane index")
     ap.add_argument("--only", default=None, help="run one solver only: riccati_f64 | lane_f64 | lane_fp32")
     a = ap.parse_args()
     import torch
@@ -59,6 +60,9 @@ def main():
         print(f"{name}: ms {['%.2f' % m for m in ms]} -> {a.agents / (min(ms) * 1e-3):.0f} QP/s | status "
               f"{dict(zip(u.tolist(), c.tolist()))} | iters mean {it.mean():.2f} max {it.max()} | kkt max {kkt.max():.2e}",
               flush=True)
+        if a.lanes:
+            bad = st != 1
+            print("   not-solved by lane b%32:", np.bincount(np.flatnonzero(bad) % 32, minlength=32).tolist(), flush=True)
         out[name] = dict(ms=min(ms), qps=a.agents / (min(ms) * 1e-3), status=dict(zip(map(int, u), map(int, c))),
                          iters_mean=float(it.mean()), iters_max=int(it.max()))
         return z, st, it

@@ -29,7 +29,7 @@ extern "C" int lane_cpu_solve(int nx, int nu, int N, int ns, int mc, int batch, 
     std::vector<double> ws(L.total * (size_t)batch);
     auto pack = [&](const double* src, size_t off, int T) {  // lane_pack_kernel on the host
         for (int b = 0; b < batch; ++b)
-            for (int e = 0; e < T; ++e) ws[off * batch + (size_t)e * batch + b] = src[(size_t)b * T + e];
+            for (int e = 0; e < T; ++e) ws[off * batch + ((size_t)(e >> 1) * batch + b) * 2 + (e & 1)] = src[(size_t)b * T + e];
     };
     pack(A, L.iA, N * nx * nx);
     pack(B, L.iB, N * nx * nu);
