@@ -26,6 +26,7 @@ sys.path.insert(0, ROOT)
 
 METRIC = "agent-QP solves/sec (whole node) at N=30, nx=4 nu=2; max KKT residual vs ref"
 FP64_PEAK_TFLOPS = 78.6   # MI355X dense FP64 (vector == matrix), spec
+FP32_PEAK_TFLOPS = 157.3  # MI355X FP32 vector, spec
 HBM_PEAK_GBS = 8000.0
 
 
@@ -37,6 +38,9 @@ def main():
     ap.add_argument("--config", choices=["cfg3", "cfg5"], default="cfg3",
                     help="cfg3 (the metric's config, default) or cfg5: 8192 agents/GPU, N=50, 3-D double "
                          "integrator (nx=6, nu=3) on the fp64 stage-wise Riccati kernel")
+    ap.add_argument("--fp32", action="store_true",
+                    help="cfg5 only: BASELINE cfg5's fp32 path (the lane-per-agent kernel with an fp32 Riccati "
+                         "factorisation, fp64 iterates / residuals, tol 1e-6), checked against the fp64 solve")
     ap.add_argument("--agents", type=int, default=None, help="agents per GPU (default: the config's)")
     ap.add_argument("--horizon", type=int, default=None)
     ap.add_argument("--nb", type=int, default=2)
@@ -45,6 +49,8 @@ def main():
     ap.add_argument("--no-ref", action="store_true", help="skip the reference-configuration (N=125) line")
     args = ap.parse_args()
     cfg5 = args.config == "cfg5"
+    if args.fp32 and not cfg5:
+        raise SystemExit("--fp32 is the cfg5 path (use --config cfg5 --fp32)")
     args.agents = args.agents or (8192 if cfg5 else 1024)
     args.horizon = args.horizon or (50 if cfg5 else 30)
     dim = 3 if cfg5 else 2
@@ -77,7 +83,7 @@ def main():
     n_total = args.agents * world
     scen = S.make_di(n_total, args.horizon, args.nb, dim)
     ctx = cmpc.Context(local)
-    R = DIRounds(scen, rank=rank, world=world, device=local, ctx=ctx)
+    R = DIRounds(scen, rank=rank, world=world, device=local, ctx=ctx, fp32=args.fp32)
 
     def barrier():
         torch.cuda.synchronize()
@@ -125,7 +131,10 @@ def main():
     flops = S.riccati_flops(nx, nu, N, mean_iters) if cfg5 else S.alg_flops(nx, nu, N, m_rows, mean_iters)
     achieved_tf = flops * args.agents / (kern_ms * 1e-3) / 1e12
     alg_bytes = S.di_alg_bytes(nx, nu, N, args.nb)
-    traffic, traffic_src = pmc_traffic()
+    pmc_kind = ("cfg5fp32" if args.fp32 else "cfg5") if cfg5 else None
+    traffic, traffic_src = pmc_traffic(pmc_kind)
+    peak = FP32_PEAK_TFLOPS if args.fp32 else FP64_PEAK_TFLOPS
+    fp32_check = fp32_vs_fp64(R) if (args.fp32 and rank == 0) else None
 
     cpu = None
     max_err = None
@@ -151,32 +160,39 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "f64",
+            "dtype": "f32 factorisation / f64 residuals" if args.fp32 else "f64",
             "data": "synthetic (seeded double-integrator agent population, SURVEY.md §8d)",
             "config": {
                 "workload": (f"cfg5: {args.agents} agents/GPU, N={N}, 3-D double integrator nx={nx} nu={nu}, "
-                             f"nb={args.nb}, fp64 stage-wise Riccati IPM (BASELINE asks fp32; fp64 >= it); "
-                             f"step = build+solve+advance+all-gather") if cfg5 else
+                             f"nb={args.nb}, " +
+                             ("fp32 path: lane-per-agent stage-wise IPM, fp32 Riccati factorisation and Newton "
+                              "recursions, fp64 iterates and residuals, per-agent fp64 finish, tol 1e-6"
+                              if args.fp32 else
+                              "fp64 stage-wise Riccati IPM (BASELINE asks fp32; fp64 >= it)") +
+                             "; step = build+solve+advance+all-gather") if cfg5 else
                             (f"cfg3: {args.agents} agents/GPU, N={N}, 2-D double integrator nx={nx} nu={nu}, "
                              f"nb={args.nb}, fp64 condensed IPM; step = build+solve+advance+all-gather"),
                 "agents_total": n_total, "horizon": N, "nx": nx, "nu": nu, "neighbours": args.nb,
                 "parallelism": f"agents sharded over {world} GPU(s), "
                                f"{'RCCL' if backend == 'nccl' else backend} all-gather per round",
             },
+            "fp32_vs_fp64": fp32_check,
             "max_kkt": kkt_all,
             "unsolved": int(bad_all),
             "solved_inaccurate": int(inacc_all),
             "mean_ipm_iters": mean_iters,
             "max_abs_err_vs_cpu": max_err,
             "roofline": {
-                "kernel": "mpc_riccati_kernel<Cfg<2,6,3,6>>" if cfg5 else "mpc_ipm3_kernel<4,4,2,2>",
+                "kernel": ("mpc_lane_kernel<6,3,6,3,true> (+ lane_pack_kernel)" if args.fp32 else
+                           "mpc_riccati_kernel<Cfg<2,6,3,6>>") if cfg5 else "mpc_ipm3_kernel<4,4,2,2>",
                 "bound": "mfma",
                 "achieved": achieved_tf,
-                "peak": FP64_PEAK_TFLOPS,
+                "peak": peak,
+                "peak_note": "fp32 vector (the factorisation's precision)" if args.fp32 else "fp64 vector = matrix",
                 "unit": "TFLOP/s",
-                "frac": achieved_tf / FP64_PEAK_TFLOPS,
-                "traffic": None if cfg5 else traffic,
-                "traffic_source": None if cfg5 else traffic_src,
+                "frac": achieved_tf / peak,
+                "traffic": traffic,
+                "traffic_source": traffic_src,
                 "kernel_ms_per_launch": kern_ms,
                 "alg_flops_per_qp": flops,
                 "alg_bytes_per_qp": alg_bytes,
@@ -448,8 +464,33 @@ def osqp_dropin(ctx, reps=20):
             "reps": reps}
 
 
-def pmc_traffic():
-    """HBM bytes per solver launch from the newest committed PMC summary (profiles/pmc_r*.json,
+def fp32_vs_fp64(R):
+    """BASELINE cfg5's tolerance check of the fp32 path: the next round's problem solved by the fp32
+    path (this DIRounds) and by the fp64 stage-wise Riccati kernel, every agent: statuses and the
+    largest |z32 - z64| / max(1, |z64|)."""
+    import torch
+
+    import cmpc
+
+    R.build()
+    R.solve()
+    torch.cuda.synchronize()
+    z32, st32 = R.z.cpu().numpy().copy(), R.status.cpu().numpy().copy()
+    p = R.snapshot()
+    z64, _, _, st64 = cmpc.solve_mpc(p, R.ctx, riccati=True)
+    err = np.abs(z32 - z64) / np.maximum(1.0, np.abs(z64))
+    both = (st32 == cmpc.CMPC_SOLVED) & (st64 == cmpc.CMPC_SOLVED)
+    return {"agents": int(len(st32)), "fp32_solved": float(np.mean(st32 == cmpc.CMPC_SOLVED)),
+            "fp32_status_counts": {int(k): int(v) for k, v in zip(*np.unique(st32, return_counts=True))},
+            "fp64_solved": float(np.mean(st64 == cmpc.CMPC_SOLVED)),
+            "max_rel_err": float(err.max()), "p99_rel_err": float(np.quantile(err.max(1), 0.99)),
+            "max_rel_err_both_solved": float(err[both].max()) if both.any() else None,
+            "reference": "fp64 stage-wise Riccati kernel (double-double near the solution), same problems"}
+
+
+def pmc_traffic(kind=None):
+    """HBM bytes per solver launch from the newest committed PMC summary (profiles/pmc_r*.json;
+    cfg5 lines: profiles/pmc_{kind}_r*.json,
     FETCH_SIZE and WRITE_SIZE in separate rocprofv3 --pmc passes, tools/prof_summary.py).  PMC
     counters cannot be collected inside this process, so the figure carries its provenance:
     the commit it was measured at, and "stale" = whether the kernel sources (sha256 over
@@ -459,7 +500,7 @@ def pmc_traffic():
     sys.path.insert(0, os.path.join(ROOT, "tools"))
     from prof_summary import solver_sources_sha
 
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "pmc_r*.json")))
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"pmc_{kind}_r*.json" if kind else "pmc_r*.json")))
     if not files:
         return None, None
     try:

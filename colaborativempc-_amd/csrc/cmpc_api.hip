@@ -431,7 +431,7 @@ int cmpc_di_solve_dev(cmpc_ctx* ctx, const cmpc_di_params* prm, const cmpc_di_di
     if (dims->batch == 0) return CMPC_OK;
     const int flags = opts ? opts->flags : 0;
     hipStream_t s = (hipStream_t)stream;
-    if (!c.wg && !c.riccati && !c.rescue && !(flags & CMPC_FLAG_GENERIC)) {  // rescue needs materialised rows
+    if (!c.wg && !c.lane && !c.riccati && !c.rescue && !(flags & CMPC_FLAG_GENERIC)) {  // rescue needs materialised rows
         cmpc::MpcPtrs p{in->A, in->B, in->x0, in->u_prev, nullptr, nullptr, nullptr, out->z, out->kkt, out->iters,
                         out->status, opts ? (unsigned long long*)opts->stamps : nullptr, nullptr};
         p.fuse = cmpc::DiFuse{nbr, lane, traj_all, dc, 1};

@@ -526,32 +526,99 @@ def test_cfg5_population_on_riccati_kernel(gpu_ctx):
     assert np.abs(z[:ns][both] - zc[both]).max() < Z_TOL
 
 
-# fp32 bar (BASELINE cfg5 "fp32 path with tolerance check vs fp64 reference"): every z entry
-# (states, slacks, inputs) within FP32_ZTOL * max(1, |z|) of the fp64 optimum; measured 2.3e-3
-# on this batch (fp32 resolves mu only to ~1e-6 under the 1e7 slack weights)
-# within FP32_ZTOL * max(1, |z|) of the fp64 optimum
-FP32_ZTOL = 5e-3
+# fp32 bar (BASELINE cfg5 "fp32 path with tolerance check vs fp64 reference"): every z entry (states,
+# slacks, inputs, input increments) within FP32_ZTOL * max(1, |z|) of the fp64 optimum, and >= 99 %
+# of the agents CMPC_SOLVED at the fp32 path's tol 1e-6 (merit max(res, 1e4 mu), as every solver).
+# Measured on the GPU: 99.8 % solved, 5.9e-4 worst over 8192 agents (tools/lane_check.py).
+FP32_ZTOL = 1e-3
 
 
-def test_cfg5_fp32_path_vs_fp64_reference(gpu_ctx):
-    """BASELINE cfg5 shape (3-D dynamics nx=6 nu=3, N=50, nb=2) on the fp32 workgroup solver,
-    checked against the fp64 C restatement on the same problems."""
+def _cfg5_problem(n, rounds=2):
+    """BASELINE cfg5 problems (3-D double integrator, N = 50, nb = 2) after `rounds` closed-loop
+    rounds, built by the device builder (bit-equal to the oracle builder, test above) and copied out."""
+    import torch
+
+    from cmpc import scenarios as S
+    from cmpc.rounds import DIRounds
+
+    R = DIRounds(S.make_di(n, 50, 2, 3), fused=False)
+    for _ in range(rounds):
+        R.step()
+    R.build()
+    torch.cuda.synchronize()
+    return R.snapshot()
+
+
+def test_cfg5_fp32_path_at_scale_vs_fp64(gpu_ctx):
+    """BASELINE cfg5 at its size: 8192 agents on the fp32 path (lane-per-agent kernel, fp32 Riccati
+    factorisation, fp64 iterates) against the fp64 stage-wise Riccati kernel on every agent and the
+    fp64 C restatement (Riccati, double-double near the solution) on a 128-agent sample."""
+    import cmpc
+    from oracle import cmpc_oracle as CO
+
+    n, ns = 8192, 128
+    P = _cfg5_problem(n)
+    z, kkt, it, st = cmpc.solve_mpc(P, gpu_ctx, fp32=True)
+    zr, _, _, sr = cmpc.solve_mpc(P, gpu_ctx, riccati=True)
+    frac = float((st == cmpc.CMPC_SOLVED).mean())
+    err = (np.abs(z - zr) / np.maximum(1.0, np.abs(zr))).max(1)
+    print(f"cfg5 fp32 x{n}: solved {frac:.4f} status {np.unique(st, return_counts=True)} iters mean {it.mean():.1f} "
+          f"max {it.max()} | vs fp64 kernel: max rel err {err.max():.2e} (fp64 solved {np.mean(sr == 1):.4f})")
+    assert frac >= 0.99 and np.isin(st, (cmpc.CMPC_SOLVED, cmpc.CMPC_SOLVED_INACCURATE)).all()
+    assert np.isfinite(z).all() and err.max() < FP32_ZTOL
+    Ps = {k: (v[:ns] if isinstance(v, np.ndarray) and v.ndim and v.shape[0] == n else v) for k, v in P.items()}
+    zc, _, _, stc = CO.solve_batch(Ps, nthreads=8, newton=3)
+    ec = np.abs(z[:ns] - zc) / np.maximum(1.0, np.abs(zc))
+    assert np.isin(stc, (1, 2)).all() and ec.max() < FP32_ZTOL, ec.max()
+
+
+def test_cfg5_fp32_path_small_batches(gpu_ctx):
+    """Ragged batches (not a multiple of the 32 agents of a wavefront) and a single agent: same
+    answers agent by agent as the full batch (no cross-lane coupling)."""
+    import cmpc
+
+    P = _cfg5_problem(100, rounds=1)
+    z, _, it, st = cmpc.solve_mpc(P, gpu_ctx, fp32=True)
+    for sl in (slice(0, 1), slice(3, 40), slice(37, 100)):
+        Q = {k: (v[sl] if isinstance(v, np.ndarray) and v.ndim and v.shape[0] == 100 else v) for k, v in P.items()}
+        zq, _, iq, sq = cmpc.solve_mpc(Q, gpu_ctx, fp32=True)
+        np.testing.assert_array_equal(zq, z[sl])
+        np.testing.assert_array_equal(iq, it[sl])
+
+
+def test_lane_kernel_fp64_vs_c_restatement(gpu_ctx):
+    """The lane-per-agent kernel in fp64 (CMPC_FLAG_LANE) runs the C restatement's Riccati method
+    (oracle newton 1): same statuses, z within 1e-6 wherever both solve (the kernel's fused sweeps
+    sum in another order, so agents at the rounding floor may end one iteration apart)."""
+    import cmpc
+    from oracle import cmpc_oracle as CO
+
+    n = 256
+    P = _cfg5_problem(n)
+    z, kkt, it, st = cmpc.solve_mpc(P, gpu_ctx, lane=True)
+    zc, kc, ic, stc = CO.solve_batch(P, nthreads=8, newton=1)
+    same = st == stc
+    both = (st == 1) & (stc == 1)
+    print(f"lane fp64: status agree {same.mean():.3f}, iterations agree {np.mean(it == ic):.3f}")
+    assert same.mean() >= 0.95 and both.mean() >= 0.85
+    assert np.abs(z[both] - zc[both]).max() < Z_TOL
+
+
+def test_fp32_flag_off_lane_dims_uses_workgroup_solver(gpu_ctx):
+    """Dimensions the lane kernel is not instantiated for (nb = 3: 7 rows per stage) keep the fp32
+    workgroup-per-agent condensed solver: finite answers near the fp64 optimum (its bar: 5e-3)."""
     import cmpc
     from cmpc import scenarios as S
     from oracle import cmpc_oracle as CO
     from oracle import synth
 
-    sc = S.make_di(64, 50, 2, 3)
-    P = synth.structured(sc.shared, sc.params, sc.A, sc.B, sc.x0, sc.u_prev, sc.lane, sc.nbr, sc.traj,
-                         np.arange(64))
-    z, kkt, it, st = cmpc.solve_mpc(P, gpu_ctx, fp32=True)
-    zc, kc, _, stc = CO.solve_batch(P)
-    assert np.isin(stc, (1, 2)).all() and kc.max() < 1e-6   # fp64 reference: solved (or at its rounding floor)
-    assert np.isin(st, (cmpc.CMPC_SOLVED, cmpc.CMPC_SOLVED_INACCURATE)).all(), st
+    sc = S.make_di(16, 20, 3, 2)
+    P = synth.structured(sc.shared, sc.params, sc.A, sc.B, sc.x0, sc.u_prev, sc.lane, sc.nbr, sc.traj, np.arange(16))
+    z, kkt, it, st = cmpc.solve_mpc(P, gpu_ctx, fp32=True, tol=1e-5)
+    zc, _, _, _ = CO.solve_batch(P)
     err = np.abs(z - zc) / np.maximum(1.0, np.abs(zc))
-    print(f"cfg5 fp32: max rel err {err.max():.2e}, iters mean {it.mean():.1f} max {it.max()}, "
-          f"status {np.unique(st, return_counts=True)}")
-    assert err.max() < FP32_ZTOL
+    print(f"wg fp32: status {np.unique(st, return_counts=True)}, max rel err {err.max():.2e}")
+    assert np.isfinite(z).all() and err.max() < 5e-3
 
 
 def test_ocd_dual_update_and_convergence_match_reference(gpu_ctx):

@@ -5,6 +5,8 @@
       launches (dispatches warmup .. warmup+steps-1) is the number bench.py's
       roofline.kernel_ms_per_launch must agree with.
   python tools/prof_summary.py pmc <counter_collection.csv (FETCH pass)> <(WRITE pass)> <out.json> [commit]
+  SOLVER=<kernel name substring> selects the solver kernel (default mpc_ipm; cfg5: mpc_riccati,
+  the fp32 path: mpc_lane_kernel).
       HBM bytes per launch of the solver kernel from FETCH_SIZE / WRITE_SIZE (kB), with the
       gfx950 correction of /opt/skills/guides/MI355X_MICROARCH.md (FETCH_SIZE counts half the
       bytes of wide coalesced reads: x2).
@@ -32,7 +34,7 @@ def solver_sources_sha():
             h.update(fh.read())
     return h.hexdigest()[:16]
 
-SOLVER = "mpc_ipm"   # matches mpc_ipm_kernel<...> and mpc_ipm2_kernel<...>
+SOLVER = os.environ.get("SOLVER", "mpc_ipm")   # default: mpc_ipm_kernel<...>, mpc_ipm3_kernel<...>
 
 
 def _rows(path):
@@ -74,7 +76,8 @@ def pmc(fetch_csv, write_csv, out, commit=None):
     res = {"solve_kernel": {"fetch_bytes_per_launch": fetch_b, "write_bytes_per_launch": write_b,
                             "hbm_bytes_per_launch": fetch_b + write_b,
                             "fetch_kB_raw": fk, "write_kB_raw": wk,
-                            "note": "FETCH_SIZE x2 (gfx950 half-count of wide reads); first dispatch skipped"},
+                            "note": "FETCH_SIZE x2 (gfx950 half-count of wide reads); first dispatch skipped",
+                            "kernel_filter": SOLVER},
            "commit": commit, "sources_sha": solver_sources_sha()}
     json.dump(res, open(out, "w"), indent=1)
     print(json.dumps(res))
