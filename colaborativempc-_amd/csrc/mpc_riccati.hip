@@ -44,7 +44,12 @@ constexpr int kStageMax = CMPC_MAX_NX * CMPC_MAX_NX + CMPC_MAX_NX * CMPC_MAX_NU 
 constexpr int kPerMax = (kStageMax + kWave - 1) / kWave;  // stage-image values per lane (largest dims)
 constexpr int kPerSmall = 2;                               // ... when the stage image fits 128 values
 constexpr int kDepth = 3;  // stage images in flight: a sweep step waits for a load issued 2 steps earlier
-constexpr double kDdTh = 1e10;   // max th above which an iteration runs in double-double
+constexpr double kDdTh = 1e10;   // max th above which an iteration runs in double-double ...
+// ... once the solve has made no new best iterate for kDdStall iterations (or the fp64 factorisation
+// broke down): on 2048 BASELINE cfg5 agents the double-double iterations drop 3136 -> 181 (25 % ->
+// 1.5 % of all) with the same statuses to 3 agents and z to 8e-10, and every captured reference QP
+// (N = 10 .. 125) takes the same iterations to the same statuses (oracle newton 3, tools/f32_lab.py)
+constexpr int kDdStall = 2;
 constexpr int kRefineMax = 6;    // refinement steps of a double-double iteration's direction
 // ... in a continued (rescue hand-over) solve: 2 — over the 22 lpv_lab rounds the continued
 // agents end with the same statuses as with 6 (278 vs 279 at the rounding floor; oracle
@@ -1058,6 +1063,9 @@ __global__ __launch_bounds__(kWave) void mpc_riccati_kernel(const MpcConst c_arg
     // pass over an agent this one leaves CMPC_UNSOLVED starts cold
     double* hand = ws + gl.hand;
     const bool warm = c_arg.rescue && hand[0] != 0.0;
+    // double-double near the solution: a continued (rescue) solve from the start, a cold one only
+    // once the fp64 recursion stops making progress or breaks down (kDdStall)
+    bool dd_on = warm;
     const int it0 = warm ? (int)hand[1] : 0;
     if (warm) {
         for (int i = l; i < n; i += kWave) U[i] = hand[2 + i];
@@ -1215,10 +1223,17 @@ __global__ __launch_bounds__(kWave) void mpc_riccati_kernel(const MpcConst c_arg
         gsync();  // W_k: stored by one lane, read by others
         double thm_l = 0.0;
         for (int r = l; r < m; r += kWave) thm_l = fmax(thm_l, th[r]);
-        const bool hp = wave_max(thm_l) > kDdTh;  // wave-uniform
+        const bool above = wave_max(thm_l) > kDdTh;  // wave-uniform
+        if (!dd_on && it - best_it >= kDdStall) dd_on = true;
+        bool hp = above && dd_on;
         wsync();
         RSTAMP(1);
-        const bool fact_ok = hp ? riccati_factor_dd<G>(c, d, L, sm, A, B, Wg, F) : riccati_factor<G>(c, d, L, sm, A, B, Wg, F);
+        bool fact_ok = hp ? riccati_factor_dd<G>(c, d, L, sm, A, B, Wg, F) : riccati_factor<G>(c, d, L, sm, A, B, Wg, F);
+        if (!fact_ok && !hp && above) {  // fp64 breakdown above the threshold: this iteration and the rest in dd
+            gsync();
+            dd_on = hp = true;
+            fact_ok = riccati_factor_dd<G>(c, d, L, sm, A, B, Wg, F);
+        }
         gsync();  // gains F: stored by the factor's lanes, read by every lane of the solves
         if (!fact_ok) {
             stop = kStopBreakdown;

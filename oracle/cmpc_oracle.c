@@ -1266,6 +1266,10 @@ static int solve_one(const shared_t* S, const agent_t* a, double tol, int max_it
 #ifdef RIC_F32
     int f32_on = 1;          /* lab: this agent still factors in fp32 */
 #endif
+#ifndef DD_STALL
+#define DD_STALL 2           /* kDdStall of mpc_riccati.hip */
+#endif
+    int dd_on = 0;           /* newton 3: this solve has switched to double-double near the solution */
 #ifdef GONDZIO
     /* lab: Gondzio centrality correctors (up to GONDZIO per iteration) on the Mehrotra direction */
     long gz_used = 0;
@@ -1382,10 +1386,20 @@ static int solve_one(const shared_t* S, const agent_t* a, double tol, int max_it
         double* W = wk->W;
         if (S->newton) {
                         hp = 0;
+            double thm_last = 0.0;
             if (S->newton == 3) {
                 double thm = 0.0;
                 for (int r = 0; r < m; ++r) if (wk->act[r] && wk->th[r] > thm) thm = wk->th[r];
-                hp = thm > RIC_DD_TH;
+                thm_last = thm;
+                /* double-double only once the fp64 recursion stops making progress (no new best iterate
+                   for DD_STALL iterations) or breaks down while max th > RIC_DD_TH — not at every such
+                   iteration (kDdStall of mpc_riccati.hip): on 2048 cfg5 agents 3136 -> 181 dd iterations,
+                   the same statuses to 2 agents and z to 5e-8; a continued (rescue) solve keeps it on */
+                if (!dd_on && it - best_it >= DD_STALL) dd_on = 1;
+                hp = thm > RIC_DD_TH && dd_on;
+#ifdef DD_PROACTIVE
+                hp = thm > RIC_DD_TH;   /* lab: the round-2 rule */
+#endif
 #ifdef DD_COUNT
                 if (hp) {
 #pragma omp atomic
@@ -1419,6 +1433,15 @@ static int solve_one(const shared_t* S, const agent_t* a, double tol, int max_it
             }
             if (!f32_on)
 #endif
+            if (!hp && S->newton == 3 && thm_last > RIC_DD_TH && ric_factor(S, a, wk->th, wk->Dsig, wk->F)) {
+                dd_on = 1;   /* fp64 breakdown above the threshold: this iteration and the rest in double-double */
+                hp = 1;
+#ifdef DD_COUNT
+#pragma omp atomic
+                cmpc_dd_iters += 1;
+#endif
+                if (ric_factor_dd(S, a, wk->th, wk->Dsig, wk->F)) { stop = 2; break; }
+            } else if (hp || S->newton != 3 || !(thm_last > RIC_DD_TH))
             if (hp ? ric_factor_dd(S, a, wk->th, wk->Dsig, wk->F) : ric_factor(S, a, wk->th, wk->Dsig, wk->F)) { stop = 2; break; }
 #endif
         }
@@ -1518,6 +1541,7 @@ static int solve_one(const shared_t* S, const agent_t* a, double tol, int max_it
                 /* hand over: redo this iteration (its residuals are those of the same iterate) with
                    the Riccati solve; the best iterate is tracked afresh, as the rescue kernel does */
                 S = &S_ric;
+                dd_on = 1;   /* a continued solve factors in double-double whenever max th > RIC_DD_TH */
                 best_m = INFINITY;
                 best_kkt = INFINITY;
                 best_it = 0;

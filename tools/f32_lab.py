@@ -126,6 +126,10 @@ def main():
             cnt = f" | fp32 iters {f32i} fp64 iters {f64i} switched agents {f64a}"
         except ValueError:
             pass
+        try:
+            cnt += f" | dd iters {ct.c_long.in_dll(lib, 'cmpc_dd_iters').value}"
+        except ValueError:
+            pass
         print(f"{v}: status {dict(zip(u.tolist(), c.tolist()))} solved {np.mean(st == 1):.4f} iters mean {it.mean():.1f} "
               f"max {it.max()} | rel err max {err.max():.2e} p99 {np.quantile(err, 0.99):.2e} "
               f"median {np.median(err):.2e} | solved-only max {e1:.2e}{cnt}", flush=True)
