@@ -149,3 +149,22 @@ def test_lpvrounds_rejects_short_initial_prediction(gpu_ctx):
         LPVRounds(bp, args[0], args[1][:2], args[2], args[3], **kw)
     with pytest.raises(ValueError):
         LPVRounds(bp, args[0], args[1][:, :-1], args[2], args[3], **kw)
+
+
+def test_lpv_rounds_at_scale_against_c_restatement(gpu_ctx):
+    """The bench's population of the reference's agent model (1023 agents: 341 jittered copies of
+    the 3-agent N = 30 Highway scenario), 20 device-resident rounds with the rescue policy: no agent
+    unsolved, every agent's KKT residual <= 1e-6, and each round a 128-agent sample re-solved by the
+    C restatement with the same rescue policy (oracle.cmpc_oracle.solve_batch_rescue) within 1e-6
+    wherever both reach the tolerance."""
+    import bench
+
+    out = bench.lpv_rounds(gpu_ctx, replicas=341, rounds=20, warmup=2, check=True, sample=128)
+    st = out["status_counts"]
+    print({k: v for k, v in out.items() if k in ("agent_qp_per_s", "status_counts", "max_kkt", "oracle_sample")})
+    assert all(k in (1, 2) for k in st), st
+    assert out["max_kkt"] <= 1e-6
+    smp = out["oracle_sample"]
+    assert smp["checked"] == 20 * 128, smp
+    assert smp["both_solved"] >= 0.9 * smp["checked"], smp
+    assert smp["max_abs_err_vs_cpu"] <= 1e-6, smp
