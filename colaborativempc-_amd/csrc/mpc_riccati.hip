@@ -392,7 +392,28 @@ __device__ __forceinline__ void fwd_sim(const MpcConst& c, const Dims& d, const 
     wsync();
     sweep(pp, [&](int k, const double* Ak) {
         const double* Bk = Ak + d.sA;
-        if (l < nx) {
+        if constexpr (G::NX != 0) {  // fixed dimensions: every read issued before the chain (same sums)
+            constexpr int NX = G::NX, NU = G::NU;
+            const int r = l < NX ? l : NX - 1;
+            double a[NX], x[NX], bb[NU], u[NU];
+#pragma unroll
+            for (int t = 0; t < NX; ++t) {
+                a[t] = Ak[r * NX + t];
+                x[t] = X[k * NX + t];
+            }
+#pragma unroll
+            for (int i = 0; i < NU; ++i) {
+                bb[i] = Bk[r * NU + i];
+                u[i] = U[k * NU + i];
+            }
+            __builtin_amdgcn_sched_barrier(0);
+            double v = 0.0;
+#pragma unroll
+            for (int t = 0; t < NX; ++t) v = fma(a[t], x[t], v);
+#pragma unroll
+            for (int i = 0; i < NU; ++i) v = fma(bb[i], u[i], v);
+            if (l < NX) X[(k + 1) * NX + l] = v;
+        } else if (l < nx) {
             double v = 0.0;
             for (int t = 0; t < nx; ++t) v = fma(Ak[l * nx + t], X[k * nx + t], v);
             for (int i = 0; i < nu; ++i) v = fma(Bk[l * nu + i], U[k * nu + i], v);
@@ -414,7 +435,28 @@ __device__ __forceinline__ void adjoint(const MpcConst& c, const Dims& d, const 
         const double* Bk = Ak + d.sA;
         const double* pa = psi2 + ((N - 1 - k) & 1) * nx;
         double* pb = psi2 + ((N - k) & 1) * nx;
-        if (l < nu) {
+        if constexpr (G::NX != 0) {
+            // fixed dimensions: lanes < nu (B' psi) and 32..32+nx (psi) run one chain shape,
+            // every read issued before it (same sums as below)
+            constexpr int NX = G::NX, NU = G::NU;
+            const bool bl = l < 32;
+            const int t = bl ? (l < NU ? l : NU - 1) : (l - 32 < NX ? l - 32 : NX - 1);
+            const double* col = bl ? Bk + t : Ak + t;
+            const int ld = bl ? NU : NX;
+            double cv[NX], pv[NX];
+#pragma unroll
+            for (int s2 = 0; s2 < NX; ++s2) {
+                cv[s2] = col[s2 * ld];
+                pv[s2] = pa[s2];
+            }
+            const double y0 = yb[k * NX + (bl ? 0 : t)];
+            __builtin_amdgcn_sched_barrier(0);
+            double v = bl ? 0.0 : y0;
+#pragma unroll
+            for (int s2 = 0; s2 < NX; ++s2) v = fma(cv[s2], pv[s2], v);
+            if (l < NU) out[k * NU + l] = v;
+            else if (k > 0 && l >= 32 && l < 32 + NX) pb[l - 32] = v;
+        } else if (l < nu) {
             double v = 0.0;
             for (int s = 0; s < nx; ++s) v = fma(Bk[s * nu + l], pa[s], v);
             out[k * nu + l] = v;
@@ -486,14 +528,289 @@ __device__ __forceinline__ void stage_weights(const MpcConst& c, const RLds& L, 
     }
 }
 
+// Lower-triangle entry t of an n x n matrix -> (i, j), j <= i (row-major over the triangle).
+__device__ __forceinline__ void tri_ij(int t, int n, int& i, int& j) {
+    i = 0;
+    for (int r = 1; r < n; ++r) i += (r * (r + 1) / 2 <= t) ? 1 : 0;
+    j = t - i * (i + 1) / 2;
+}
+
+// One stage of the fp64 factor sweep for compile-time dimensions (G::NX != 0): the arithmetic of
+// the generic stage below, every sum in the same order (the gains and P are bit-identical), in
+// three phases instead of four, each issuing all of its LDS reads before its first FMA.
+//   1. T = P[:, :nx] [A_k | B_k]          (the old P_uu block is read here too)
+//   2. G = [A_k | B_k]' T[:nx, :]         (lower triangle)
+//   3. every lane: Hvv, its Cholesky factor and inverse; the lane's gain entries (into F);
+//      its entries of P_k = blkdiag(W_k + A'Pxx A, 2dR) + Hvy' K_k, the Hvy / K columns they
+//      need formed from G and T in registers — no hand-off through LDS between K and P_k.
+// The generic stage let the compiler interleave its reads with the FMA chains that consume
+// them (one LDS latency per two products) and ran the A / B column cases of T as divergent
+// branches: ~2 k clocks per phase (tools/ric_stamps.py, lab build CMPC_RIC_SUBSTAMP).
+template <class G>
+__device__ __forceinline__ bool factor_stage_fixed(const MpcConst& c, int k, const double* Ak, double* P, double* T,
+                                                   double* Gm, const double* th, double* __restrict__ Fk,
+                                                   unsigned long long* sub) {
+    constexpr int NX = G::NX, NU = G::NU, NA = NX + NU, NC = NA;
+    constexpr int NE = NA * NC, RT = (NE + kWave - 1) / kWave;           // T entries, rounds
+    constexpr int NT = NC * (NC + 1) / 2, RG = (NT + kWave - 1) / kWave; // G lower entries
+    constexpr int NP = NA * (NA + 1) / 2, RP = (NP + kWave - 1) / kWave; // P lower entries
+    const int l = threadIdx.x;
+    const double* Bk = Ak + NX * NX;
+    const double* Wk = Ak + NX * NX + NX * NU;
+#ifdef CMPC_RIC_SUBSTAMP
+    unsigned long long s_a = sub ? clock64_() : 0;
+#define FSTAMP(slot)                                    \
+    if (sub) {                                          \
+        const unsigned long long s_b = clock64_();      \
+        if (l == 0) sub[slot] += s_b - s_a;             \
+        s_a = s_b;                                      \
+    }
+#else
+#define FSTAMP(slot)
+#endif
+    // ---- phase 1: T ----
+    {
+        double pr[RT][NX], cv[RT][NX];
+        double pu[NU][NU];
+#pragma unroll
+        for (int q = 0; q < RT; ++q) {
+            int e = l + q * kWave;
+            e = e < NE ? e : NE - 1;
+            const int i = e / NC, j = e - i * NC;
+            const double* col = (j < NX) ? Ak + j : Bk + (j - NX);
+            const int ld = (j < NX) ? NX : NU;
+#pragma unroll
+            for (int s = 0; s < NX; ++s) {
+                pr[q][s] = P[i * NA + s];
+                cv[q][s] = col[s * ld];
+            }
+        }
+#pragma unroll
+        for (int a = 0; a < NU; ++a)
+#pragma unroll
+            for (int b = 0; b <= a; ++b) pu[a][b] = P[(NX + a) * NA + NX + b];
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int q = 0; q < RT; ++q) {
+            double v = 0.0;
+#pragma unroll
+            for (int s = 0; s < NX; ++s) v = fma(pr[q][s], cv[q][s], v);
+            if (l + q * kWave < NE) T[l + q * kWave] = v;
+        }
+        wsync();  // (pu: P_uu of P_{k+1}, held in registers; phase 3 overwrites P)
+        FSTAMP(9)
+        // ---- phase 2: G (lower triangle) ----
+        double tr[RG][NX], cg[RG][NX];
+        int ge[RG];
+#pragma unroll
+        for (int q = 0; q < RG; ++q) {
+            int t = l + q * kWave;
+            t = t < NT ? t : NT - 1;
+            int i, j;
+            tri_ij(t, NC, i, j);
+            ge[q] = i * NC + j;
+            const double* ci = (i < NX) ? Ak + i : Bk + (i - NX);
+            const int ldi = (i < NX) ? NX : NU;
+#pragma unroll
+            for (int s = 0; s < NX; ++s) {
+                cg[q][s] = ci[s * ldi];
+                tr[q][s] = T[s * NC + j];
+            }
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int q = 0; q < RG; ++q) {
+            double v = 0.0;
+#pragma unroll
+            for (int s = 0; s < NX; ++s) v = fma(cg[q][s], tr[q][s], v);
+            if (l + q * kWave < NT) Gm[ge[q]] = v;
+        }
+        wsync();
+        FSTAMP(10)
+        // ---- phase 3 ----
+        // reads: Hvv's G / T entries, the lane's gain column, its P entries' columns
+        // (the weights live in LDS too (c): their reads belong before the barrier as well)
+        double hg[NU][NU], ht1[NU][NU], ht2[NU][NU], thu[NU][2], r2[NU][NU], dr2[NU][NU];
+#pragma unroll
+        for (int a = 0; a < NU; ++a) {
+#pragma unroll
+            for (int b = 0; b <= a; ++b) {
+                hg[a][b] = Gm[(NX + a) * NC + NX + b];
+                ht1[a][b] = T[(NX + a) * NC + NX + b];
+                ht2[a][b] = T[(NX + b) * NC + NX + a];
+                r2[a][b] = c.R[a * NU + b];
+                dr2[a][b] = c.dR[a * NU + b];
+            }
+            const int rr = c.ms + 2 * (k * NU + a);
+            thu[a][0] = th[rr];
+            thu[a][1] = th[rr + 1];
+        }
+        // gain entry e = l (a = e / NA, column j): hv(b, j) = G[nx+b][j] + T[nx+b][j] (j < nx)
+        constexpr int NK = NU * NA;
+        const int ek = l < NK ? l : NK - 1;
+        const int ka = ek / NA, kj = ek - ka * NA;
+        double kg[NU], kt[NU], kd[NU];
+#pragma unroll
+        for (int b = 0; b < NU; ++b) {
+            const int jj = kj < NX ? kj : 0;
+            kg[b] = Gm[(NX + b) * NC + jj];
+            kt[b] = T[(NX + b) * NC + jj];
+            kd[b] = c.dR[b * NU + (kj < NX ? 0 : kj - NX)];
+        }
+        // P entries (i, j), j <= i: W + G[i][j] and the columns i, j of Hvy
+        double pw[RP], pg[RP], pd[RP], ci_g[RP][NU], ci_t[RP][NU], cj_g[RP][NU], cj_t[RP][NU], ci_d[RP][NU],
+            cj_d[RP][NU];
+        int pi_[RP], pj_[RP];
+#pragma unroll
+        for (int q = 0; q < RP; ++q) {
+            int t = l + q * kWave;
+            t = t < NP ? t : NP - 1;
+            int i, j;
+            tri_ij(t, NA, i, j);
+            pi_[q] = i;
+            pj_[q] = j;
+            const int ix = i < NX ? i : 0, jx = j < NX ? j : 0;
+            const int iu = i < NX ? 0 : i - NX, ju = j < NX ? 0 : j - NX;
+            pw[q] = Wk[ix * NX + jx];
+            pg[q] = Gm[ix * NC + jx];
+            pd[q] = c.dR[iu * NU + ju];
+#pragma unroll
+            for (int b = 0; b < NU; ++b) {
+                ci_g[q][b] = Gm[(NX + b) * NC + ix];
+                ci_t[q][b] = T[(NX + b) * NC + ix];
+                cj_g[q][b] = Gm[(NX + b) * NC + jx];
+                cj_t[q][b] = T[(NX + b) * NC + jx];
+                ci_d[q][b] = c.dR[b * NU + iu];
+                cj_d[q][b] = c.dR[b * NU + ju];
+            }
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        // Hvv and its Cholesky factor / inverse (as the generic stage)
+        double Lf[CMPC_MAX_NU][CMPC_MAX_NU], Hi[CMPC_MAX_NU][CMPC_MAX_NU];
+        bool ok = true;
+#pragma unroll
+        for (int a = 0; a < CMPC_MAX_NU; ++a)
+#pragma unroll
+            for (int b = 0; b < CMPC_MAX_NU; ++b) {
+                double v = 0.0;
+                if (a < NU && b <= a) {
+                    v = 2.0 * r2[a][b] + 2.0 * dr2[a][b] + hg[a][b] + ht1[a][b] + ht2[a][b] + pu[a][b];
+                    if (a == b) v += thu[a][0] + thu[a][1];
+                }
+                Lf[a][b] = v;
+            }
+#pragma unroll
+        for (int j = 0; j < NU; ++j) {
+            double dj = Lf[j][j];
+#pragma unroll
+            for (int p = 0; p < j; ++p) dj = fma(-Lf[j][p], Lf[j][p], dj);
+            ok = ok && (dj > 0.0);
+            const double rs = rsqrt_d(dj > 0.0 ? dj : 1.0);
+            Lf[j][j] = dj * rs;
+#pragma unroll
+            for (int i = j + 1; i < NU; ++i) {
+                double v = Lf[i][j];
+#pragma unroll
+                for (int p = 0; p < j; ++p) v = fma(-Lf[i][p], Lf[j][p], v);
+                Lf[i][j] = v * rs;
+            }
+        }
+        double Li[CMPC_MAX_NU][CMPC_MAX_NU];
+#pragma unroll
+        for (int i = 0; i < CMPC_MAX_NU; ++i)
+#pragma unroll
+            for (int j = 0; j < CMPC_MAX_NU; ++j) Li[i][j] = 0.0;
+#pragma unroll
+        for (int i = 0; i < NU; ++i) {
+            const double di = rcp_d(Lf[i][i]);
+            Li[i][i] = di;
+#pragma unroll
+            for (int j = 0; j < i; ++j) {
+                double v = 0.0;
+#pragma unroll
+                for (int p = j; p < i; ++p) v = fma(Lf[i][p], Li[p][j], v);
+                Li[i][j] = -v * di;
+            }
+        }
+#pragma unroll
+        for (int a = 0; a < CMPC_MAX_NU; ++a)
+#pragma unroll
+            for (int b = 0; b < CMPC_MAX_NU; ++b) {
+                double v = 0.0;
+#pragma unroll
+                for (int p = 0; p < CMPC_MAX_NU; ++p) v = fma(Li[p][a], Li[p][b], v);
+                Hi[a][b] = v;
+            }
+        // hv(b, col) and K(a, col) = sum_b -Hinv[a][b] hv(b, col), in the generic stage's order
+        auto hv = [&](int col, double g, double t, double dr) { return (col < NX) ? g + t : -2.0 * dr; };
+        // the lane's gain entry and Hinv entry
+        {
+            double kv = 0.0;
+#pragma unroll
+            for (int b = 0; b < NU; ++b) {
+                double hab = 0.0;
+#pragma unroll
+                for (int a2 = 0; a2 < NU; ++a2)
+                    if (a2 == ka) hab = Hi[a2][b];
+                kv = fma(-hab, hv(kj, kg[b], kt[b], kd[b]), kv);
+            }
+            if (l < NK) Fk[l] = kv;
+            if (l < NU * NU) {
+                const int a = l / NU, b = l - a * NU;
+                double v = 0.0;
+#pragma unroll
+                for (int a2 = 0; a2 < NU; ++a2)
+#pragma unroll
+                    for (int b2 = 0; b2 < NU; ++b2)
+                        if (a2 == a && b2 == b) v = Hi[a2][b2];
+                Fk[NK + l] = v;
+            }
+        }
+        // P_k entries (k > 0)
+        if (k > 0) {
+#pragma unroll
+            for (int q = 0; q < RP; ++q) {
+                const int i = pi_[q], j = pj_[q];
+                double v = (i < NX) ? pw[q] + pg[q] : ((j >= NX) ? 2.0 * pd[q] : 0.0);
+#pragma unroll
+                for (int a = 0; a < NU; ++a) {
+                    double kv = 0.0;
+#pragma unroll
+                    for (int b = 0; b < NU; ++b) kv = fma(-Hi[a][b], hv(j, cj_g[q][b], cj_t[q][b], cj_d[q][b]), kv);
+                    v = fma(hv(i, ci_g[q][a], ci_t[q][a], ci_d[q][a]), kv, v);
+                }
+                if (l + q * kWave < NP) {
+                    P[i * NA + j] = v;
+                    P[j * NA + i] = v;
+                }
+            }
+        }
+        FSTAMP(11)
+#undef FSTAMP
+        return ok;
+    }
+}
+
 // Riccati factorisation of the Newton system at the current (th, Dsig), with the stage weights
 // Wg of stage_weights: writes the gains K_k = -Hvv^-1 Hvy and Hinv_k = Hvv^-1 of every stage
 // into F.  Returns false on a non-positive pivot (wave-uniform).
 template <class G>
 __device__ __forceinline__ bool riccati_factor(const MpcConst& c, const Dims& d, const RLds& L, double* sm,
                                const double* __restrict__ A, const double* __restrict__ B,
-                               const double* __restrict__ Wg, double* __restrict__ F) {
+                               const double* __restrict__ Wg, double* __restrict__ F,
+                               unsigned long long* sub = nullptr) {
     const int l = threadIdx.x, nx = d.nx, nu = d.nu, na = d.na, nc = d.nc, N = c.N;
+#ifdef CMPC_RIC_SUBSTAMP  // lab build (tools/ric_stamps.py --sub): per-phase clocks of the fp64 factor sweep
+    unsigned long long s_a = sub ? clock64_() : 0;
+#define SUBSTAMP(slot)                                  \
+    if (sub) {                                          \
+        const unsigned long long s_b = clock64_();      \
+        if (slot >= 0 && l == 0) sub[slot] += s_b - s_a; \
+        s_a = s_b;                                      \
+    }
+#else
+#define SUBSTAMP(slot)
+#endif
     double* P = sm + L.P;
     double* T = sm + L.T;
     double* Gm = sm + L.G;
@@ -512,7 +829,11 @@ __device__ __forceinline__ bool riccati_factor(const MpcConst& c, const Dims& d,
     wsync();
     bool ok = true;
     sweep(pp, [&](int k, const double* Ak) {
+      if constexpr (G::NX != 0) {
+        ok = factor_stage_fixed<G>(c, k, Ak, P, T, Gm, th, F + (size_t)k * d.sF, sub) && ok;
+      } else {
         const double* Bk = Ak + d.sA;
+        SUBSTAMP(-1)  // slots 9-11: T, G, Hvv..K; the rest of the factor (P update, stage advance) is slot 2 minus them
         // T = P[:, :nx] [A_k | B_k]   (na x nc)
         for (int e = l; e < na * nc; e += kWave) {
             const int i = e / nc, j = e - i * nc;
@@ -524,6 +845,7 @@ __device__ __forceinline__ bool riccati_factor(const MpcConst& c, const Dims& d,
             T[e] = v;
         }
         wsync();
+        SUBSTAMP(9)
         // G = [A_k | B_k]' T[:nx, :]   (nc x nc, lower triangle)
         for (int e = l; e < nc * nc; e += kWave) {
             const int i = e / nc, j = e - i * nc;
@@ -535,6 +857,7 @@ __device__ __forceinline__ bool riccati_factor(const MpcConst& c, const Dims& d,
             Gm[e] = v;
         }
         wsync();
+        SUBSTAMP(10)
         // Hvv = 2R + 2dR + diag(th_u) + B'Pxx B + Pux B + B'Pxu + Puu  (every lane, nu <= 4),
         // its Cholesky factor and inverse in registers
         double Lf[CMPC_MAX_NU][CMPC_MAX_NU], Hi[CMPC_MAX_NU][CMPC_MAX_NU];
@@ -634,6 +957,7 @@ __device__ __forceinline__ bool riccati_factor(const MpcConst& c, const Dims& d,
             Fk[nu * na + l] = v;
         }
         wsync();
+        SUBSTAMP(11)
         // P_k = blkdiag(W_k + A'Pxx A, 2dR) + Hvy' K_k   (symmetric: lower triangle mirrored)
         for (int e = l; e < na * na && k > 0; e += kWave) {
             const int i = e / na, j = e - i * na;
@@ -644,7 +968,9 @@ __device__ __forceinline__ bool riccati_factor(const MpcConst& c, const Dims& d,
             P[i * na + j] = v;
             P[j * na + i] = v;
         }
+      }
     });
+#undef SUBSTAMP
     return ok;
 }
 
@@ -847,7 +1173,51 @@ __device__ __forceinline__ void riccati_solve(const MpcConst& c, const Dims& d, 
             const double* Hg = Kg + nu * na;
             const double* pc = pv + ((N - 1 - k) & 1) * na;
             double* pn = pv + ((N - k) & 1) * na;
-            if (l < na) {
+            if constexpr (G::NX != 0) {
+                // fixed dimensions: every read of the step issued before its chains (same sums)
+                constexpr int NX = G::NX, NU = G::NU, NA = NX + NU;
+                const int lx = l < NX ? l : NX - 1, la = l < NA ? l : NA - 1, lu = l < NU ? l : NU - 1;
+                double p[NA], bm[NX][NU], ac[NX], kg[NU], hg[NU], r0[NU];
+#pragma unroll
+                for (int s2 = 0; s2 < NX; ++s2) {
+#pragma unroll
+                    for (int a = 0; a < NU; ++a) bm[s2][a] = Bk[s2 * NU + a];
+                    ac[s2] = Ak[s2 * NX + lx];
+                }
+#pragma unroll
+                for (int a = 0; a < NU; ++a) {
+                    const int ci = k * NU + a;
+                    r0[a] = yb ? rd[ci] + (rt[c.ms + 2 * ci] - rt[c.ms + 2 * ci + 1]) : -rh[ci];
+                    kg[a] = Kg[a * NA + la];
+                    hg[a] = Hg[lu * NU + a];
+                }
+                const double y0 = (yb && l < NX) ? yb[k * NX + l] : 0.0;
+#pragma unroll
+                for (int s2 = 0; s2 < NA; ++s2) p[s2] = pc[s2];
+                __builtin_amdgcn_sched_barrier(0);
+                double g[NU];
+#pragma unroll
+                for (int a = 0; a < NU; ++a) {
+                    double v = p[NX + a] + r0[a];
+#pragma unroll
+                    for (int s2 = 0; s2 < NX; ++s2) v = fma(bm[s2][a], p[s2], v);
+                    g[a] = v;
+                }
+                double v = y0;
+                if (l < NX) {
+#pragma unroll
+                    for (int s2 = 0; s2 < NX; ++s2) v = fma(ac[s2], p[s2], v);
+                }
+#pragma unroll
+                for (int a = 0; a < NU; ++a) v = fma(kg[a], g[a], v);
+                if (l < NA) pn[l] = v;
+                if (l < NU) {
+                    double u = 0.0;
+#pragma unroll
+                    for (int b = 0; b < NU; ++b) u = fma(-hg[b], g[b], u);
+                    dU[k * NU + l] = u;
+                }
+            } else if (l < na) {
                 double g[CMPC_MAX_NU];
 #pragma unroll
                 for (int a = 0; a < CMPC_MAX_NU; ++a) {
@@ -889,7 +1259,48 @@ __device__ __forceinline__ void riccati_solve(const MpcConst& c, const Dims& d, 
             const double* Bk = Ak + d.sA;
             const double* Kg = Bk + d.sB;
             const double* xc = xb + (k & 1) * nx;
-            if (l < nx || l < nu) {
+            if constexpr (G::NX != 0) {
+                // fixed dimensions: every read of the step issued before its chains (same sums)
+                constexpr int NX = G::NX, NU = G::NU, NA = NX + NU;
+                const int lx = l < NX ? l : NX - 1;
+                double x[NX], kg[NU][NA], d0[NU], dp[NU], ar[NX], br[NU];
+#pragma unroll
+                for (int a = 0; a < NU; ++a) {
+#pragma unroll
+                    for (int j = 0; j < NA; ++j) kg[a][j] = Kg[a * NA + j];
+                    d0[a] = dU[k * NU + a];
+                    dp[a] = dU[(k > 0 ? k - 1 : 0) * NU + a];
+                    br[a] = Bk[lx * NU + a];
+                }
+#pragma unroll
+                for (int t = 0; t < NX; ++t) ar[t] = Ak[lx * NX + t];
+#pragma unroll
+                for (int t = 0; t < NX; ++t) x[t] = xc[t];
+                __builtin_amdgcn_sched_barrier(0);
+                double vk[NU];
+#pragma unroll
+                for (int a = 0; a < NU; ++a) {
+                    double v = d0[a];
+#pragma unroll
+                    for (int j = 0; j < NX; ++j) v = fma(kg[a][j], x[j], v);
+                    if (k > 0)
+#pragma unroll
+                        for (int b = 0; b < NU; ++b) v = fma(kg[a][NX + b], dp[b], v);
+                    vk[a] = v;
+                }
+                double v = 0.0;
+#pragma unroll
+                for (int t = 0; t < NX; ++t) v = fma(ar[t], x[t], v);
+#pragma unroll
+                for (int a = 0; a < NU; ++a) v = fma(br[a], vk[a], v);
+                if (l < NX) {
+                    xb[((k + 1) & 1) * NX + l] = v;
+                    if (dX) dX[(k + 1) * NX + l] = v;
+                }
+#pragma unroll
+                for (int a = 0; a < NU; ++a)
+                    if (l == a) dU[k * NU + a] = vk[a];
+            } else if (l < nx || l < nu) {
                 double vk[CMPC_MAX_NU];
 #pragma unroll
                 for (int a = 0; a < CMPC_MAX_NU; ++a) {
@@ -1228,7 +1639,8 @@ __global__ __launch_bounds__(kWave) void mpc_riccati_kernel(const MpcConst c_arg
         bool hp = above && dd_on;
         wsync();
         RSTAMP(1);
-        bool fact_ok = hp ? riccati_factor_dd<G>(c, d, L, sm, A, B, Wg, F) : riccati_factor<G>(c, d, L, sm, A, B, Wg, F);
+        bool fact_ok = hp ? riccati_factor_dd<G>(c, d, L, sm, A, B, Wg, F)
+                          : riccati_factor<G>(c, d, L, sm, A, B, Wg, F, stamp ? tsum : nullptr);
         if (!fact_ok && !hp && above) {  // fp64 breakdown above the threshold: this iteration and the rest in dd
             gsync();
             dd_on = hp = true;

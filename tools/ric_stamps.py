@@ -19,6 +19,8 @@ SLOTS = 16
 NAMES = {14: "setup + output", 0: "residuals (2 adjoints)", 1: "stage weights, max th", 2: "factor (fp64)",
          3: "factor (double-double)", 4: "rhs (rho, C'rt, adjoint)", 5: "solve (2 sweeps)",
          6: "refinement (dd residual + solve)", 7: "rows, slacks, step", 8: "update"}
+# lab build with -DCMPC_RIC_SUBSTAMP (CMPC_LIB_PATH): phases of the fp64 factor sweep, inside slot 2
+SUB = {9: "  factor: T = P[A|B]", 10: "  factor: G = [A|B]'T", 11: "  factor: Hvv, chol, K"}
 
 
 def report(st, iters, label, ms):
@@ -28,6 +30,9 @@ def report(st, iters, label, ms):
     tot = a[:, [k for k in NAMES]].sum(1)
     for k, nm in NAMES.items():
         print(f"  {nm:34s} " + " ".join(f"{v / 1e6:8.3f}M" for v in a[:, k]) + "   clk per agent")
+        if k == 2 and a[:, 9:12].any():
+            for k2, nm2 in SUB.items():
+                print(f"  {nm2:34s} " + " ".join(f"{v / 1e6:8.3f}M" for v in a[:, k2]) + "   clk per agent")
     it = np.maximum(a[:, SLOTS - 1], 1)
     print(f"  {'total':34s} " + " ".join(f"{v / 1e6:8.3f}M" for v in tot) +
           "   | per iteration " + " ".join(f"{v / 1e3:.0f}k" for v in tot / it))
@@ -87,6 +92,9 @@ def cfg5(agents):
     tot = a[:, list(NAMES)].sum(1)
     for k, nm in NAMES.items():
         print(f"  {nm:34s} {a[:, k].sum() / it.sum() / 1e3:9.1f}k clk/iter  {a[:, k].sum() / tot.sum() * 100:5.1f} %")
+        if k == 2 and a[:, 9:12].any():
+            for k2, nm2 in SUB.items():
+                print(f"  {nm2:34s} {a[:, k2].sum() / it.sum() / 1e3:9.1f}k clk/iter")
     print(f"  {'total':34s} {tot.sum() / it.sum() / 1e3:9.1f}k clk/iter; slowest agent {tot.max() / 1e6:.2f}M clk")
 
 
