@@ -46,7 +46,8 @@ CMPC_FLAG_LANE = 128    # lane-per-agent stage-wise kernel, fp64
 
 
 class cmpc_opts(ct.Structure):
-    _fields_ = [("tol", ct.c_double), ("max_iter", ct.c_int), ("flags", ct.c_int), ("stamps", ct.c_void_p)]
+    _fields_ = [("tol", ct.c_double), ("max_iter", ct.c_int), ("flags", ct.c_int), ("stamps", ct.c_void_p),
+                ("order", ct.c_void_p)]
 
 
 class cmpc_mpc_dims(ct.Structure):
@@ -245,8 +246,9 @@ def i32(a):
     return np.ascontiguousarray(a, dtype=np.int32)
 
 
-def opts(tol=None, max_iter=None, flags=0, stamps=None):
-    return cmpc_opts(float(tol or 0.0), int(max_iter or 0), int(flags), stamps)
+def opts(tol=None, max_iter=None, flags=0, stamps=None, order=None):
+    """cmpc_opts; stamps / order: device pointers (int) or None."""
+    return cmpc_opts(float(tol or 0.0), int(max_iter or 0), int(flags), stamps, order)
 
 
 class Context:

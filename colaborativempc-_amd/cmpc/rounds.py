@@ -55,7 +55,7 @@ def exchange_positions(traj_all, traj_local, world=1, group=None, comm=None):
 
 class DIRounds:
     def __init__(self, scen, rank=0, world=1, device=None, ctx=None, tol=None, max_iter=None, group=None,
-                 fp32=False, comm=None, fused=True):
+                 fp32=False, comm=None, fused=True, lpt=None):
         import torch
 
         self.torch = torch
@@ -99,6 +99,13 @@ class DIRounds:
         from .solver import FP32_TOL
 
         self.opts = L.opts(tol or (FP32_TOL if fp32 else None), max_iter, L.CMPC_FLAG_FP32 if fp32 else 0)
+        # lpt: launch the Riccati solver's agents longest-first, by last round's IPM iterations
+        # (cmpc_opts.order; many agents per SIMD there, so the launch otherwise ends with whichever
+        # slow agents happened to start last).  Default: on where the stage-wise solver runs (the
+        # condensed kernels have one agent per SIMD and ignore the order); the fp32 lane kernel packs
+        # its wavefronts in that order (agents of one wavefront then leave it together).
+        self.lpt = (self.N * sh["nu"] > 64) if lpt is None else bool(lpt)
+        self._order = None
         self.data = L.cmpc_mpc_data(*[_tptr(t) for t in (self.A, self.Bm, self.x0, self.u_prev, self.qlin,
                                                           self.C, self.h)])
         self.out = L.cmpc_mpc_out(_tptr(self.z), _tptr(self.kkt), _tptr(self.iters), _tptr(self.status))
@@ -124,20 +131,31 @@ class DIRounds:
                                              _tptr(self.lane), _tptr(self.traj_all), _tptr(self.qlin),
                                              _tptr(self.C), _tptr(self.h), self._stream()))
 
+    def _order_in(self):
+        self.opts.order = self._order.data_ptr() if (self.lpt and self._order is not None) else None
+
+    def _order_out(self):
+        if self.lpt:  # next round's launch order (stream-ordered after this solve)
+            self._order = self.torch.argsort(self.iters, descending=True, stable=True).to(self.torch.int32)
+
     def solve(self):
+        self._order_in()
         self.ctx.check(self.ctx.lib.cmpc_solve_mpc_batch_dev(self.ctx.h, ct.byref(self.mdims), ct.byref(self.w),
                                                              ct.byref(self.data), ct.byref(self.out),
                                                              ct.byref(self.opts), self._stream()))
+        self._order_out()
 
     def build_solve(self):
         """build() + solve() as one launch where the v3 kernel covers the problem (the rows go
         from traj_all straight into the solver's LDS, bit-identical to build()); qlin / C / h are
         then left untouched — call build() before snapshot() to materialise them."""
         lib = self.ctx.lib
+        self._order_in()
         self.ctx.check(lib.cmpc_di_solve_dev(self.ctx.h, ct.byref(self.dprm), ct.byref(self.ddims), _tptr(self.nbr),
                                              _tptr(self.lane), _tptr(self.traj_all), ct.byref(self.mdims),
                                              ct.byref(self.w), ct.byref(self.data), ct.byref(self.out),
                                              ct.byref(self.opts), self._stream()))
+        self._order_out()
 
     def advance(self):
         self.ctx.check(self.ctx.lib.cmpc_di_advance_dev(self.ctx.h, ct.byref(self.dprm), ct.byref(self.ddims),

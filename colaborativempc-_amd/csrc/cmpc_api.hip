@@ -212,6 +212,7 @@ int cmpc_solve_mpc_batch_dev(cmpc_ctx* ctx, const cmpc_mpc_dims* dims, const cmp
     }
     cmpc::MpcPtrs p{in->A, in->B, in->x0, in->u_prev, in->qlin, in->C, in->h, out->z, out->kkt, out->iters, out->status,
                     opts ? (unsigned long long*)opts->stamps : nullptr, ws};
+    p.order = opts ? opts->order : nullptr;
     HIP_TRY(cmpc::mpc_launch(c, p, dims->batch, (hipStream_t)stream, opts ? opts->flags : 0));
     return CMPC_OK;
 }

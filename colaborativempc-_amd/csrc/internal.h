@@ -72,6 +72,7 @@ struct MpcPtrs {
     unsigned long long* stamps;  // optional: batch x kStampSlots per-section s_memtime counts (v3 kernel)
     double* ws;                  // device scratch, batch x mpc_ws_doubles(c) (Riccati kernel; else unused)
     DiFuse fuse;                 // fused row build (v3 kernel only; on = 0 elsewhere)
+    const int* order;            // optional launch order (Riccati kernel: workgroup i solves agent order[i])
 };
 
 // Interior-point safeguards shared by both solver kernels and the C oracle (oracle/cmpc_oracle.c).

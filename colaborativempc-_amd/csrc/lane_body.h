@@ -164,9 +164,13 @@ struct S1Out {
 
 // One agent's solve (lane j = b % kLaneAP of its wavefront).  __host__ __device__: the kernel runs it
 // per lane; tools/lane_cpu.cpp runs the same code on the host (images emulated per agent) to check it
-// against the C restatement.  `smem`: the two stage images of this wavefront (device).
+// against the C restatement.  `smem`: the two stage images of this wavefront (device).  `b` is the
+// agent's slot in the packed scratch; `ag` (default: b) its index in the caller's arrays (x0, u_prev
+// and the outputs): they differ under a launch order (cmpc_opts.order, packed by lane_pack).
 template <int NX, int NU, int MC, int NS, bool MIXED>
-__host__ __device__ inline void lane_agent(const MpcConst& c, const MpcPtrs& P, int batch, int b, char* smem) {
+__host__ __device__ inline void lane_agent(const MpcConst& c, const MpcPtrs& P, int batch, int b, char* smem,
+                                           int ag = -1) {
+    const size_t a_ = (size_t)(ag < 0 ? b : ag);
     using M = IMap<NX, NU, MC, NS>;
     constexpr int NA = NX + NU, SF = M::SF;
     constexpr int NUP = lane_ev(NU), NSP = lane_ev(NS);  // per-stage strides of U-like / slack arrays
@@ -234,9 +238,9 @@ __host__ __device__ inline void lane_agent(const MpcConst& c, const MpcPtrs& P, 
     const LV<double> gA = mk(L.iA), gB = mk(L.iB), gC = mk(L.iC), gh = mk(L.ih);
     double x0[NX], up[NU];
 #pragma unroll
-    for (int s = 0; s < NX; ++s) x0[s] = P.x0[(size_t)b * NX + s];
+    for (int s = 0; s < NX; ++s) x0[s] = P.x0[a_ * NX + s];
 #pragma unroll
-    for (int i = 0; i < NU; ++i) up[i] = P.up[(size_t)b * NU + i];
+    for (int i = 0; i < NU; ++i) up[i] = P.up[a_ * NU + i];
     // input-row bound of row q (0: u <= ub, 1: -u <= -lb) of input i
     auto w_in = [&](int i, int q) -> double { return q ? -c.u_lb[i] : c.u_ub[i]; };
 
@@ -1266,7 +1270,7 @@ __host__ __device__ inline void lane_agent(const MpcConst& c, const MpcPtrs& P, 
     // ---- output: exact re-simulation of the states from U, slacks, inputs, input increments ----
     const int nxe = NX + NS;
     const size_t nz = (size_t)nxe * (N + 1) + 2 * (size_t)c.n;
-    double* z = P.z + (size_t)b * nz;
+    double* z = P.z + a_ * nz;
     double x[NX];
 #pragma unroll
     for (int s = 0; s < NX; ++s) {
@@ -1302,9 +1306,9 @@ __host__ __device__ inline void lane_agent(const MpcConst& c, const MpcPtrs& P, 
             z[(size_t)(N + 1) * nxe + c.n + k * NU + i] = u[i] - (k ? U[(k - 1) * NUP + i] : up[i]);
         }
     }
-    if (P.kkt) P.kkt[b] = kkt;
-    if (P.iters) P.iters[b] = it;
-    if (P.status) P.status[b] = status;
+    if (P.kkt) P.kkt[a_] = kkt;
+    if (P.iters) P.iters[a_] = it;
+    if (P.status) P.status[a_] = status;
 }
 
 }  // namespace cmpc

@@ -42,7 +42,11 @@ __global__ __launch_bounds__(kWave) void mpc_lane_kernel(const MpcConst c, const
     extern __shared__ __attribute__((aligned(16))) char lane_smem[];
     if (threadIdx.x >= kLaneAP) return;
     const int b = blockIdx.x * kLaneAP + threadIdx.x;
-    if (b < batch) lane_agent<NX, NU, MC, NS, MIXED>(c, P, batch, b, lane_smem);
+    // launch order (cmpc_opts.order): slot b holds agent order[b] (clamped; lane_pack gathered it),
+    // so the agents of a wavefront have similar iteration counts and leave it together
+    if (b < batch)
+        lane_agent<NX, NU, MC, NS, MIXED>(c, P, batch, b, lane_smem,
+                                          P.order ? min(max(P.order[b], 0), batch - 1) : b);
 }
 
 size_t mpc_lane_ws_doubles(const MpcConst& c) { return lane_layout(c).total; }
@@ -51,12 +55,15 @@ size_t mpc_lane_ws_doubles(const MpcConst& c) { return lane_layout(c).total; }
 // ((e / 2) * batch + b) * 2 + e % 2), through a 64 x 64 LDS tile so that the reads (along e) and
 // the writes (along b) are both coalesced
 __global__ __launch_bounds__(256) void lane_pack_kernel(const double* __restrict__ src, double* __restrict__ dst,
-                                                        int batch, int T) {
+                                                        int batch, int T, const int* __restrict__ order) {
     __shared__ double tile[64][65];
     const int e0 = blockIdx.x * 64, b0 = blockIdx.y * 64, tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
     for (int r = ty; r < 64; r += 4) {
         const int b = b0 + r, e = e0 + tx;
-        if (b < batch && e < T) tile[r][tx] = src[(size_t)b * T + e];
+        if (b < batch && e < T) {
+            const int a = order ? min(max(order[b], 0), batch - 1) : b;  // slot b <- agent order[b]
+            tile[r][tx] = src[(size_t)a * T + e];
+        }
     }
     __syncthreads();
     for (int r = ty; r < 64; r += 4) {
@@ -65,9 +72,10 @@ __global__ __launch_bounds__(256) void lane_pack_kernel(const double* __restrict
     }
 }
 
-static hipError_t lane_pack(const double* src, double* dst, int batch, int T, hipStream_t s) {
+static hipError_t lane_pack(const double* src, double* dst, int batch, int T, const int* order, hipStream_t s) {
     if (T <= 0) return hipSuccess;
-    hipLaunchKernelGGL(lane_pack_kernel, dim3((T + 63) / 64, (batch + 63) / 64), dim3(256), 0, s, src, dst, batch, T);
+    hipLaunchKernelGGL(lane_pack_kernel, dim3((T + 63) / 64, (batch + 63) / 64), dim3(256), 0, s, src, dst, batch, T,
+                       order);
     return hipGetLastError();
 }
 
@@ -96,11 +104,11 @@ hipError_t mpc_lane_launch(const MpcConst& c, const MpcPtrs& p, int batch, hipSt
     const size_t S = (size_t)batch;
     const int N = c.N, nx = c.nx, nu = c.nu, mc = c.mc;
     hipError_t e;
-    if ((e = lane_pack(p.A, p.ws + L.iA * S, batch, N * nx * nx, s)) != hipSuccess) return e;
-    if ((e = lane_pack(p.B, p.ws + L.iB * S, batch, N * nx * nu, s)) != hipSuccess) return e;
-    if ((e = lane_pack(p.C, p.ws + L.iC * S, batch, N * mc * nx, s)) != hipSuccess) return e;
-    if ((e = lane_pack(p.h, p.ws + L.ih * S, batch, N * mc, s)) != hipSuccess) return e;
-    if ((e = lane_pack(p.p, p.ws + L.ip * S, batch, (N + 1) * nx, s)) != hipSuccess) return e;
+    if ((e = lane_pack(p.A, p.ws + L.iA * S, batch, N * nx * nx, p.order, s)) != hipSuccess) return e;
+    if ((e = lane_pack(p.B, p.ws + L.iB * S, batch, N * nx * nu, p.order, s)) != hipSuccess) return e;
+    if ((e = lane_pack(p.C, p.ws + L.iC * S, batch, N * mc * nx, p.order, s)) != hipSuccess) return e;
+    if ((e = lane_pack(p.h, p.ws + L.ih * S, batch, N * mc, p.order, s)) != hipSuccess) return e;
+    if ((e = lane_pack(p.p, p.ws + L.ip * S, batch, (N + 1) * nx, p.order, s)) != hipSuccess) return e;
     e = hipErrorInvalidValue;
     if (lane_try<6, 3, 6, 3>(c, p, batch, s, &e)) return e;  // BASELINE cfg5 (3-D double integrator, nb = 2)
     if (lane_try<4, 2, 6, 3>(c, p, batch, s, &e)) return e;  // cfg1-4 shape (2-D double integrator, nb = 2)

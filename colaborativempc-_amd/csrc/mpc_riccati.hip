@@ -1403,7 +1403,8 @@ __device__ __forceinline__ void kres_dd(const MpcConst& c, const Dims& d, const 
 template <class G>
 __global__ __launch_bounds__(kWave) void mpc_riccati_kernel(const MpcConst c_arg, const MpcPtrs P) {
     extern __shared__ __attribute__((aligned(16))) double sm[];
-    const int b = blockIdx.x;
+    // launch order (cmpc_opts.order): clamped into range, so a bad entry cannot address outside the batch
+    const int b = P.order ? min(max(P.order[blockIdx.x], 0), (int)gridDim.x - 1) : (int)blockIdx.x;
     if (c_arg.rescue) {  // rescue pass: agents handed over at a breakdown, or left CMPC_UNSOLVED, only
         const RGlb g0 = r_glb(c_arg);
         if (P.ws[(size_t)b * g0.total + g0.hand] == 0.0 && P.status[b] != CMPC_UNSOLVED) return;

@@ -64,6 +64,7 @@ int cmpc_lpv_rounds_create(cmpc_ctx* ctx, const cmpc_lpv_params* prm, const cmpc
     h->d = d;
     if (opts) h->opts = *opts;
     h->opts.stamps = nullptr;
+    h->opts.order = nullptr;
     h->last_rows = d.N + 1;
     const int ns = track->nseg;
     std::memcpy(h->seg[0], track->s0, sizeof(double) * ns);

@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define CMPC_ABI_VERSION 2   /* 2: cmpc_lpv_advance_dev status / infeasible, cmpc_lpv_rounds_* */
+#define CMPC_ABI_VERSION 3   /* 2: cmpc_lpv_advance_dev status / infeasible, cmpc_lpv_rounds_*; 3: cmpc_opts.order */
 
 /* API error codes */
 #define CMPC_OK 0
@@ -95,6 +95,14 @@ typedef struct {
     int flags;     /* CMPC_FLAG_* */
     void* stamps;  /* optional DEVICE buffer, batch x 16 uint64: per-section shader-clock counts of the
                       specialised kernel (diagnostic; NULL in production) */
+    const int* order; /* optional DEVICE array, batch int32, a permutation of 0..batch-1: the launch order of
+                         the stage-wise Riccati solver (workgroup i solves agent order[i]; every output stays
+                         at its agent's index).  With many agents per SIMD the launch ends with its slowest
+                         solves; listing last round's agents by descending IPM iterations starts them first
+                         (cmpc.rounds.DIRounds(lpt=True)).  The lane-per-agent solver (CMPC_FLAG_FP32 /
+                         LANE) packs its wavefronts in this order, so each holds agents of similar
+                         iteration counts.  Honoured by cmpc_solve_mpc_batch_dev; NULL:
+                         identity.  Entries are clamped into range; a non-permutation leaves agents unsolved. */
 } cmpc_opts;
 
 int cmpc_abi_version(void);

@@ -526,6 +526,50 @@ def test_cfg5_population_on_riccati_kernel(gpu_ctx):
     assert np.abs(z[:ns][both] - zc[both]).max() < Z_TOL
 
 
+def test_riccati_launch_order_is_invisible(gpu_ctx):
+    """cmpc_opts.order (the longest-first launch order of DIRounds(lpt=True)) only reorders the
+    workgroups (Riccati kernel) or the packing of the wavefronts (fp32 lane kernel): z / kkt /
+    iterations / status are bit-identical at every agent's own index, for a random permutation and
+    for DIRounds rounds with and without LPT (cfg5 shape, 2048 agents, fp64 and the fp32 path)."""
+    import ctypes as ct
+
+    import torch
+
+    from cmpc import _lib as L
+    from cmpc import scenarios as S
+    from cmpc.rounds import DIRounds
+
+    n = 2048
+    for fp32 in (False, True):
+        outs = []
+        for lpt in (False, True):
+            R = DIRounds(S.make_di(n, 50, 2, 3), lpt=lpt, fp32=fp32)
+            rec = []
+            for _ in range(3):
+                R.step()
+                torch.cuda.synchronize()
+                rec.append([t.cpu().numpy().copy() for t in (R.z, R.kkt, R.iters, R.status)])
+            outs.append(rec)
+            if lpt:
+                assert R._order is not None and sorted(R._order.cpu().numpy().tolist()) == list(range(n))
+        for ra, rb in zip(*outs):
+            for a, b in zip(ra, rb):
+                assert np.array_equal(a.view(np.uint8), b.view(np.uint8)), fp32
+    # an explicit random permutation through the C ABI
+    R = DIRounds(S.make_di(n, 50, 2, 3), lpt=False, fused=False)
+    R.build()
+    R.solve()
+    torch.cuda.synchronize()
+    base = [t.cpu().numpy().copy() for t in (R.z, R.kkt, R.iters, R.status)]
+    perm = torch.as_tensor(np.random.default_rng(7).permutation(n), dtype=torch.int32, device=R.dev)
+    R.opts = L.opts(order=perm.data_ptr())
+    R.ctx.check(R.ctx.lib.cmpc_solve_mpc_batch_dev(R.ctx.h, ct.byref(R.mdims), ct.byref(R.w), ct.byref(R.data),
+                                                   ct.byref(R.out), ct.byref(R.opts), R._stream()))
+    torch.cuda.synchronize()
+    for a, t in zip(base, (R.z, R.kkt, R.iters, R.status)):
+        assert np.array_equal(a.view(np.uint8), t.cpu().numpy().view(np.uint8))
+
+
 # fp32 bar (BASELINE cfg5 "fp32 path with tolerance check vs fp64 reference"): every z entry (states,
 # slacks, inputs, input increments) within FP32_ZTOL * max(1, |z|) of the fp64 optimum, and >= 99 %
 # of the agents CMPC_SOLVED at the fp32 path's tol 1e-6 (merit max(res, 1e4 mu), as every solver).

@@ -21,6 +21,8 @@ NAMES = {14: "setup + output", 0: "residuals (2 adjoints)", 1: "stage weights, m
          6: "refinement (dd residual + solve)", 7: "rows, slacks, step", 8: "update"}
 # lab build with -DCMPC_RIC_SUBSTAMP (CMPC_LIB_PATH): phases of the fp64 factor sweep, inside slot 2
 SUB = {9: "  factor: T = P[A|B]", 10: "  factor: G = [A|B]'T", 11: "  factor: Hvv, chol, K"}
+if os.environ.get("CMPC_SUB_MODE") == "2":  # lab build -DCMPC_RIC_SUBSTAMP=2: sweep bodies (without the stage advance)
+    SUB = {9: "  solve: backward bodies", 10: "  solve: forward bodies", 11: "  residual adjoint bodies"}
 
 
 def report(st, iters, label, ms):
