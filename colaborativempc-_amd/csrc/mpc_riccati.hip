@@ -469,6 +469,49 @@ __device__ __forceinline__ void adjoint(const MpcConst& c, const Dims& d, const 
     });
 }
 
+// Two independent adjoint recursions in one backward sweep (fixed dimensions): out1 / out2 from
+// yb1 / yb2, the arithmetic of two adjoint() calls (bit-identical), one stage advance per stage
+// and two chains in flight.  Lanes: 0..nu-1 B'psi1, 16..16+nu-1 B'psi2, 32..32+nx-1 psi1,
+// 48..48+nx-1 psi2.  psi4: 4 nx doubles (two ping-pong pairs).
+template <class G>
+__device__ __forceinline__ void adjoint2(const MpcConst& c, const Dims& d, const StageSrc& src, double* sb,
+                                         const double* yb1, double* out1, const double* yb2, double* out2,
+                                         double* psi4) {
+    constexpr int NX = G::NX, NU = G::NU;
+    static_assert(NX != 0 && NX <= 16 && NU <= 16, "fixed dimensions");
+    const int l = threadIdx.x, N = c.N;
+    Pipe<G::KP> pp(src, d.sAB, N, d.Sl, true, sb);
+    pp.prime();
+    const bool second = (l & 16) != 0;  // lanes 16..31, 48..63
+    const double* yb = second ? yb2 : yb1;
+    double* psi = psi4 + (second ? 2 * NX : 0);
+    if ((l & 15) < NX && l >= 32) psi[l & 15] = yb[N * NX + (l & 15)];
+    wsync();
+    const bool bl = l < 32;
+    const int t = bl ? ((l & 15) < NU ? (l & 15) : NU - 1) : ((l & 15) < NX ? (l & 15) : NX - 1);
+    double* out = second ? out2 : out1;
+    sweep(pp, [&](int k, const double* Ak) {
+        const double* Bk = Ak + NX * NX;
+        const double* pa = psi + ((N - 1 - k) & 1) * NX;
+        double* pb = psi + ((N - k) & 1) * NX;
+        const double* col = bl ? Bk + t : Ak + t;
+        const int ld = bl ? NU : NX;
+        double cv[NX], pv[NX];
+#pragma unroll
+        for (int s2 = 0; s2 < NX; ++s2) {
+            cv[s2] = col[s2 * ld];
+            pv[s2] = pa[s2];
+        }
+        const double y0 = yb[k * NX + (bl ? 0 : t)];
+        __builtin_amdgcn_sched_barrier(0);
+        double v = bl ? 0.0 : y0;
+#pragma unroll
+        for (int s2 = 0; s2 < NX; ++s2) v = fma(cv[s2], pv[s2], v);
+        if (bl && (l & 15) < NU) out[k * NU + (l & 15)] = v;
+        else if (!bl && k > 0 && (l & 15) < NX) pb[l & 15] = v;
+    });
+}
+
 // W_k = 2Q + M_k of the state X_{k+1} for every block k (global scratch, one pass of all lanes)
 template <class G>
 __device__ __forceinline__ void stage_weights(const MpcConst& c, const RLds& L, const double* sm,
@@ -1551,21 +1594,37 @@ __global__ __launch_bounds__(kWave) void mpc_riccati_kernel(const MpcConst c_arg
             yb[i] = v;
         }
         wsync();
-        adjoint<G>(c, d, sAB, sb, yb, gU, psi);
+        if constexpr (G::NX != 0) {
+            // both residual adjoints in one sweep: gU from yb, rd from yb2 = yb + C' lambda (stages 1..N)
+            double* yb2 = sm + L.yb2;
+            for (int i = l; i < (N + 1) * nx; i += kWave) {
+                const int k = i / nx, s = i - k * nx;
+                double v = 0.0;
+                if (k > 0)
+                    for (int r = 0; r < mc; ++r) v = fma(lam[(k - 1) * mc + r], C[((size_t)(k - 1) * mc + r) * nx + s], v);
+                yb2[i] = k > 0 ? yb[i] + v : yb[i];
+            }
+            wsync();
+            adjoint2<G>(c, d, sAB, sb, yb, gU, yb2, rd, sm + L.psid);
+        } else {
+            adjoint<G>(c, d, sAB, sb, yb, gU, psi);
+        }
         double gs_l = 1.0;
         for (int i = l; i < n; i += kWave) {
             gU[i] += rdr_grad<G>(c, U, up, i);
             gs_l = nmax(gs_l, fabs(gU[i]));
         }
         const double gscale = wave_max(gs_l);
-        for (int i = l; i < N * nx; i += kWave) {  // + C' lambda on stages 1..N
-            const int k = i / nx, s = i - k * nx;
-            double v = 0.0;
-            for (int r = 0; r < mc; ++r) v = fma(lam[k * mc + r], C[((size_t)k * mc + r) * nx + s], v);
-            yb[(k + 1) * nx + s] += v;
+        if constexpr (G::NX == 0) {
+            for (int i = l; i < N * nx; i += kWave) {  // + C' lambda on stages 1..N
+                const int k = i / nx, s = i - k * nx;
+                double v = 0.0;
+                for (int r = 0; r < mc; ++r) v = fma(lam[k * mc + r], C[((size_t)k * mc + r) * nx + s], v);
+                yb[(k + 1) * nx + s] += v;
+            }
+            wsync();
+            adjoint<G>(c, d, sAB, sb, yb, rd, psi);
         }
-        wsync();
-        adjoint<G>(c, d, sAB, sb, yb, rd, psi);
         double nrd_l = 0.0, nrs_l = 0.0, nrp_l = 0.0, mu_l = 0.0;
         for (int i = l; i < n; i += kWave) {
             const int r = ms + 2 * i;
