@@ -281,23 +281,45 @@ struct Pipe {
     const int cnt, N, S;
     const bool back;
     double* const sb;
+    // per lane and load q: the element's address at stage 0, its per-stage stride and whether it
+    // is in the lagged third segment — fixed for the sweep, so a fetch is one multiply-add per
+    // load (stage_fetch re-derived the segment and the 64-bit offsets at every step)
+    const double* pb[KP];
+    int ps[KP];
+    bool pf[KP];
     __device__ Pipe(const StageSrc& s_, int cnt_, int N_, int S_, bool back_, double* sb_)
-        : src(s_), cnt(cnt_), N(N_), S(S_), back(back_), sb(sb_) {}
+        : src(s_), cnt(cnt_), N(N_), S(S_), back(back_), sb(sb_) {
+#pragma unroll
+        for (int q = 0; q < KP; ++q) {
+            int e = (int)threadIdx.x + q * kWave;
+            e = e < cnt ? e : cnt - 1;
+            const bool ia = e < src.sA, ib = !ia && e < src.sA + src.sB;
+            pb[q] = ia ? src.A + e : (ib ? src.B + (e - src.sA) : src.F + (e - src.sA - src.sB));
+            ps[q] = ia ? src.sA : (ib ? src.sB : src.sF);
+            pf[q] = !ia && !ib;
+        }
+    }
+    // the loads of stage_fetch (same addresses)
+    __device__ void fetch(int k, double (&r_)[KP]) const {
+        const int kf = k - src.lag > 0 ? k - src.lag : 0;
+#pragma unroll
+        for (int q = 0; q < KP; ++q) r_[q] = pb[q][(pf[q] ? kf : k) * ps[q]];
+    }
     __device__ int stg(int j) const { return back ? N - 1 - j : j; }
     // stage of step j, clamped into the horizon (steps past the end fetch a real stage, unused)
     __device__ int stc(int j) const { return stg(j < N ? j : N - 1); }
     // fetch the first kDepth stages, store the first; follow with wsync()
     __device__ void prime() {
-        static_for<0, kDepth>([&](auto i) { stage_fetch<KP>(src, stc(i), cnt, r[i]); });
+        static_for<0, kDepth>([&](auto i) { fetch(stc(i), r[i]); });
         stage_put<KP>(sb + (stg(0) & 1) * S, cnt, r[0]);
-        stage_fetch<KP>(src, stc(kDepth), cnt, r[0]);
+        fetch(stc(kDepth), r[0]);
     }
     // after step j: store stage j+1 (register set I = (j+1) % kDepth) into the other slot and
     // refill the set with stage j+1+kDepth — unconditionally (see stage_fetch)
     template <int I>
     __device__ void advance(int j) {
         stage_put<KP>(sb + ((stg(j) + 1) & 1) * S, cnt, r[I]);
-        stage_fetch<KP>(src, stc(j + 1 + kDepth), cnt, r[I]);
+        fetch(stc(j + 1 + kDepth), r[I]);
     }
 };
 
@@ -591,7 +613,7 @@ __device__ __forceinline__ void tri_ij(int t, int n, int& i, int& j) {
 // branches: ~2 k clocks per phase (tools/ric_stamps.py, lab build CMPC_RIC_SUBSTAMP).
 template <class G>
 __device__ __forceinline__ bool factor_stage_fixed(const MpcConst& c, int k, const double* Ak, double* P, double* T,
-                                                   double* Gm, const double* th, double* __restrict__ Fk,
+                                                   double* Gm, const double* th, double* __restrict__ Fk, int ms,
                                                    unsigned long long* sub) {
     constexpr int NX = G::NX, NU = G::NU, NA = NX + NU, NC = NA;
     constexpr int NE = NA * NC, RT = (NE + kWave - 1) / kWave;           // T entries, rounds
@@ -684,7 +706,7 @@ __device__ __forceinline__ bool factor_stage_fixed(const MpcConst& c, int k, con
                 r2[a][b] = c.R[a * NU + b];
                 dr2[a][b] = c.dR[a * NU + b];
             }
-            const int rr = c.ms + 2 * (k * NU + a);
+            const int rr = ms + 2 * (k * NU + a);
             thu[a][0] = th[rr];
             thu[a][1] = th[rr + 1];
         }
@@ -843,6 +865,7 @@ __device__ __forceinline__ bool riccati_factor(const MpcConst& c, const Dims& d,
                                const double* __restrict__ Wg, double* __restrict__ F,
                                unsigned long long* sub = nullptr) {
     const int l = threadIdx.x, nx = d.nx, nu = d.nu, na = d.na, nc = d.nc, N = c.N;
+    const int ms = c.ms;  // (a register: see riccati_solve)
 #ifdef CMPC_RIC_SUBSTAMP  // lab build (tools/ric_stamps.py --sub): per-phase clocks of the fp64 factor sweep
     unsigned long long s_a = sub ? clock64_() : 0;
 #define SUBSTAMP(slot)                                  \
@@ -873,7 +896,7 @@ __device__ __forceinline__ bool riccati_factor(const MpcConst& c, const Dims& d,
     bool ok = true;
     sweep(pp, [&](int k, const double* Ak) {
       if constexpr (G::NX != 0) {
-        ok = factor_stage_fixed<G>(c, k, Ak, P, T, Gm, th, F + (size_t)k * d.sF, sub) && ok;
+        ok = factor_stage_fixed<G>(c, k, Ak, P, T, Gm, th, F + (size_t)k * d.sF, ms, sub) && ok;
       } else {
         const double* Bk = Ak + d.sA;
         SUBSTAMP(-1)  // slots 9-11: T, G, Hvv..K; the rest of the factor (P update, stage advance) is slot 2 minus them
@@ -1199,6 +1222,7 @@ __device__ __forceinline__ void riccati_solve(const MpcConst& c, const Dims& d, 
                               const double* __restrict__ F, const double* rh, double* dU, double* dX,
                               const double* yb = nullptr, const double* rd = nullptr, const double* rt = nullptr) {
     const int l = threadIdx.x, nx = d.nx, nu = d.nu, na = d.na, N = c.N;
+    const int ms = c.ms;  // in a register: a read of c (LDS) inside a step waits on every read before it
     double* sb = sm + L.sb;
     double* pv = sm + L.pv;
     double* xb = sm + L.xpp;  // dX_k, ping-pong
@@ -1230,7 +1254,7 @@ __device__ __forceinline__ void riccati_solve(const MpcConst& c, const Dims& d, 
 #pragma unroll
                 for (int a = 0; a < NU; ++a) {
                     const int ci = k * NU + a;
-                    r0[a] = yb ? rd[ci] + (rt[c.ms + 2 * ci] - rt[c.ms + 2 * ci + 1]) : -rh[ci];
+                    r0[a] = yb ? rd[ci] + (rt[ms + 2 * ci] - rt[ms + 2 * ci + 1]) : -rh[ci];
                     kg[a] = Kg[a * NA + la];
                     hg[a] = Hg[lu * NU + a];
                 }
