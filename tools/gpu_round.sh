@@ -1,6 +1,7 @@
 # usage: bash tools/gpu_round.sh TAG — GPU tests, smoke, bench (cfg3 default, cfg5, cfg5 --fp32), rocprofv3
 # kernel-trace stats of the same bench command, and PMC passes (FETCH_SIZE, WRITE_SIZE, one each) of the
-# cfg3 solver, the cfg5 Riccati kernel and the cfg5 fp32 lane kernel for the HBM traffic figures.
+# cfg3 solver, the cfg5 Riccati kernel and the cfg5 fp32 lane kernel for the HBM traffic figures, and the
+# per-section clocks of the Riccati kernel (tools/ric_stamps.py: N = 125 captured QPs, cfg5).
 # Every GPU step has its own time limit; steps are chained with && (stop at the first failure).
 set -o pipefail
 TAG=${1:-r1}
@@ -24,7 +25,9 @@ timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE -d $O/pmc_write -o run --output-f
 timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -d $O/pmc5_fetch -o run --output-format csv -- python3 bench.py --config cfg5 --steps 3 --warmup 1 --no-cpu > $O/pmc5_fetch.log 2>&1 &&
 timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE -d $O/pmc5_write -o run --output-format csv -- python3 bench.py --config cfg5 --steps 3 --warmup 1 --no-cpu > $O/pmc5_write.log 2>&1 &&
 timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -d $O/pmc5f_fetch -o run --output-format csv -- python3 bench.py --config cfg5 --fp32 --steps 3 --warmup 1 --no-cpu > $O/pmc5f_fetch.log 2>&1 &&
-timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE -d $O/pmc5f_write -o run --output-format csv -- python3 bench.py --config cfg5 --fp32 --steps 3 --warmup 1 --no-cpu > $O/pmc5f_write.log 2>&1
+timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE -d $O/pmc5f_write -o run --output-format csv -- python3 bench.py --config cfg5 --fp32 --steps 3 --warmup 1 --no-cpu > $O/pmc5f_write.log 2>&1 &&
+timeout -k 10 120 python tools/ric_stamps.py > $O/ric_n125.txt 2>&1 &&
+timeout -k 10 120 python tools/ric_stamps.py --cfg5 > $O/ric_cfg5.txt 2>&1
 rc=$?
 echo "rc=$rc" > $O/rc.txt
 find $O -name "*.csv" | head -80 >> $O/rc.txt
