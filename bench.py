@@ -39,7 +39,7 @@ def main():
                     help="cfg3 (the metric's config, default) or cfg5: 8192 agents/GPU, N=50, 3-D double "
                          "integrator (nx=6, nu=3) on the fp64 stage-wise Riccati kernel")
     ap.add_argument("--fp32", action="store_true",
-                    help="cfg5 only: BASELINE cfg5's fp32 path (the lane-per-agent kernel with an fp32 Riccati "
+                    help="cfg5 only: BASELINE cfg5's fp32 path (the Riccati kernel's fp32 mode: an fp32 Riccati "
                          "factorisation, fp64 iterates / residuals, tol 1e-6), checked against the fp64 solve")
     ap.add_argument("--agents", type=int, default=None, help="agents per GPU (default: the config's)")
     ap.add_argument("--horizon", type=int, default=None)
@@ -165,8 +165,9 @@ def main():
             "config": {
                 "workload": (f"cfg5: {args.agents} agents/GPU, N={N}, 3-D double integrator nx={nx} nu={nu}, "
                              f"nb={args.nb}, " +
-                             ("fp32 path: lane-per-agent stage-wise IPM, fp32 Riccati factorisation and Newton "
-                              "recursions, fp64 iterates and residuals, per-agent fp64 finish, tol 1e-6"
+                             ("fp32 path: stage-wise Riccati IPM (one wavefront per agent) with the Riccati "
+                              "factorisation and Newton recursions in fp32, fp64 iterates and residuals, per-agent "
+                              "fp64 finish, tol 1e-6"
                               if args.fp32 else
                               "fp64 stage-wise Riccati IPM (BASELINE asks fp32; fp64 >= it)") +
                              "; step = build+solve+advance+all-gather") if cfg5 else
@@ -183,8 +184,8 @@ def main():
             "mean_ipm_iters": mean_iters,
             "max_abs_err_vs_cpu": max_err,
             "roofline": {
-                "kernel": ("mpc_lane_kernel<6,3,6,3,true> (+ lane_pack_kernel)" if args.fp32 else
-                           "mpc_riccati_kernel<Cfg<2,6,3,6>>") if cfg5 else "mpc_ipm3_kernel<4,4,2,2>",
+                "kernel": ("mpc_riccati_kernel<Cfg<2,6,3,6,GR,F32>>" if args.fp32 else
+                           "mpc_riccati_kernel<Cfg<2,6,3,6,GR>>") if cfg5 else "mpc_ipm3_kernel<4,4,2,2>",
                 "bound": "mfma",
                 "achieved": achieved_tf,
                 "peak": peak,

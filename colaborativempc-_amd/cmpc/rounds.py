@@ -104,8 +104,10 @@ class DIRounds:
         # slow agents happened to start last).  Default: on where the stage-wise solver runs (the
         # condensed kernels have one agent per SIMD and ignore the order).  The fp32 lane kernel packs
         # its wavefronts in that order, but at cfg5 all of its 256 wavefronts run at once (one per CU),
-        # so its launch still ends with the slowest agent: measured 91.9 -> 99.8 ms, off by default.
-        self.lpt = (self.N * sh["nu"] > 64 and not fp32) if lpt is None else bool(lpt)
+        # so its launch still ends with the slowest agent (measured 91.9 -> 99.8 ms): off where fp32
+        # runs on it, i.e. on dimensions without the Riccati kernel's fp32 instantiation (6, 3, 6).
+        ric32 = (sh["nx"], sh["nu"], sh["mc"]) == (6, 3, 6)
+        self.lpt = (self.N * sh["nu"] > 64 and (not fp32 or ric32)) if lpt is None else bool(lpt)
         self._order = None
         self.data = L.cmpc_mpc_data(*[_tptr(t) for t in (self.A, self.Bm, self.x0, self.u_prev, self.qlin,
                                                           self.C, self.h)])

@@ -27,7 +27,9 @@ struct MpcConst {
     int rescue;   // 1: CMPC_FLAG_RESCUE on a condensed solve (Riccati re-solve of broken-down agents)
     int lpv;      // 1: data made by lpv_build.hip with Q diagonal (the v3 kernel's LS layout applies)
     int finish;   // 1: CMPC_FLAG_FINISH (rescue also continues breakdowns at the rounding floor)
-    int lane;     // lane-per-agent kernel (mpc_lane.hip): 1 fp64 (CMPC_FLAG_LANE), 2 mixed fp32 (CMPC_FLAG_FP32)
+    int lane;     // lane-per-agent kernel (mpc_lane.hip): 1 fp64 (CMPC_FLAG_LANE), 2 mixed fp32 (CMPC_FLAG_FP32 | LANE,
+                  // or CMPC_FLAG_FP32 on dimensions without an fp32 Riccati instantiation)
+    int f32;      // 1: CMPC_FLAG_FP32 on the stage-wise Riccati kernel (Cfg::F32; riccati = 1 as well)
     unsigned long long ws_stride;  // doubles of MpcPtrs::ws per agent (set by mpc_launch; 0: no scratch)
     double tol;
     double qs_max;  // max(1, 2*max(Qs)) — slack residual scale
@@ -140,6 +142,7 @@ __host__ __device__ inline bool hand_over(int stop, double best_m, const MpcCons
 
 // Stage-wise Riccati kernel (mpc_riccati.hip): any horizon whose per-agent rows fit LDS.
 size_t mpc_riccati_lds_bytes(const MpcConst& c);
+bool mpc_riccati_f32_supported(const MpcConst& c);  // Cfg::F32 instantiations (BASELINE cfg5 dimensions)
 size_t mpc_riccati_ws_doubles(const MpcConst& c);
 hipError_t mpc_riccati_launch(const MpcConst& c, const MpcPtrs& p, int batch, hipStream_t s);
 // Lane-per-agent stage-wise kernel (mpc_lane.hip): the dimension sets it is instantiated for.

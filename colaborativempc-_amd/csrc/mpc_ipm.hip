@@ -710,9 +710,13 @@ int mpc_prepare(const cmpc_mpc_dims* d, const cmpc_mpc_weights* wt, const cmpc_o
     c->ldk = (c->n & 1) ? c->n : c->n + 1;
     c->tol = (o && o->tol > 0) ? o->tol : 1e-9;
     c->max_iter = (o && o->max_iter > 0) ? o->max_iter : 60;
-    c->lane = (fp32 && lane_ok) ? 2 : (lane_req ? 1 : 0);
-    c->wg = (fp32 && !c->lane) ? 2 : 0;
-    c->riccati = (!fp32 && !c->lane && (c->n > CMPC_MAX_NCOND || (o && (o->flags & CMPC_FLAG_RICCATI)))) ? 1 : 0;
+    // fp32: the stage-wise Riccati kernel's fp32 mode where it is instantiated (BASELINE cfg5), unless
+    // CMPC_FLAG_LANE asks for the lane-per-agent kernel; else the lane kernel; else the workgroup kernel
+    c->f32 = (fp32 && !lane_req && mpc_riccati_f32_supported(*c)) ? 1 : 0;
+    c->lane = (fp32 && lane_ok && !c->f32) ? 2 : (lane_req ? 1 : 0);
+    c->wg = (fp32 && !c->lane && !c->f32) ? 2 : 0;
+    c->riccati = (c->f32 || (!fp32 && !c->lane && (c->n > CMPC_MAX_NCOND || (o && (o->flags & CMPC_FLAG_RICCATI)))))
+                     ? 1 : 0;
     double qs = 1.0;
     for (int i = 0; i < d->nx * d->nx; ++i) c->Q[i] = wt->Q[i];
     for (int i = 0; i < d->nu * d->nu; ++i) {

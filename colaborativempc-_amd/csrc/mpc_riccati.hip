@@ -50,6 +50,9 @@ constexpr double kDdTh = 1e10;   // max th above which an iteration runs in doub
 // 1.5 % of all) with the same statuses to 3 agents and z to 8e-10, and every captured reference QP
 // (N = 10 .. 125) takes the same iterations to the same statuses (oracle newton 3, tools/f32_lab.py)
 constexpr int kDdStall = 2;
+// Cfg::F32: an agent leaves fp32 for good after this many iterations without a new best iterate
+// (or at an fp32 factorisation breakdown) — the lane kernel's kF32Stall (lane_body.h)
+constexpr int kRicF32Stall = 2;
 constexpr int kRefineMax = 6;    // refinement steps of a double-double iteration's direction
 // ... in a continued (rescue hand-over) solve: 2 — over the 22 lpv_lab rounds the continued
 // agents end with the same statuses as with 6 (278 vs 279 at the rounding floor; oracle
@@ -83,10 +86,15 @@ struct Dims {
 // serial chains of short steps on one wavefront, so latency is all that counts.
 // GR: the six lane-owned row vectors (t, lam, w, rp, rho, GdU) live in the global scratch
 // instead of LDS (r_rows_global): fewer LDS bytes per wave, more waves per CU.
-template <int KP_, int NX_, int NU_, int MC_, bool GR_ = false>
+template <int KP_, int NX_, int NU_, int MC_, bool GR_ = false, bool F32_ = false>
 struct Cfg {
     static constexpr int KP = KP_, NX = NX_, NU = NU_, MC = MC_;
     static constexpr bool GR = GR_;
+    // F32: BASELINE cfg5's fp32 path (CMPC_FLAG_FP32, MpcConst::f32): the factorisation, its gains
+    // and both Newton recursions in fp32, iterates / residuals / rows / the direction's state
+    // recursion in fp64; an agent continues in fp64 after an fp32 breakdown or kF32Stall
+    // iterations without a new best iterate (the lane kernel's scheme, tools/f32_lab.py)
+    static constexpr bool F32 = F32_;
     // values per lane of the [A | B | W] images of the factor and residual sweeps
     static constexpr int KPW = NX_ ? (2 * NX_ * NX_ + NX_ * NU_ + kWave - 1) / kWave
                                    : (2 * CMPC_MAX_NX * CMPC_MAX_NX + CMPC_MAX_NX * CMPC_MAX_NU + kWave - 1) / kWave;
@@ -600,6 +608,18 @@ __device__ __forceinline__ void tri_ij(int t, int n, int& i, int& j) {
     j = t - i * (i + 1) / 2;
 }
 
+// 1/sqrt and 1/x in the factor's precision (hardware estimate + Newton steps to full precision)
+__device__ __forceinline__ double rsqrt_r(double x) { return rsqrt_d(x); }
+__device__ __forceinline__ double rcp_r(double x) { return rcp_d(x); }
+__device__ __forceinline__ float rsqrt_r(float x) {
+    const float y = __builtin_amdgcn_rsqf(x);
+    return y * fmaf(-0.5f * x, y * y, 1.5f);
+}
+__device__ __forceinline__ float rcp_r(float x) {
+    const float r = __builtin_amdgcn_rcpf(x);
+    return fmaf(r, fmaf(-x, r, 1.0f), r);
+}
+
 // One stage of the fp64 factor sweep for compile-time dimensions (G::NX != 0): the arithmetic of
 // the generic stage below, every sum in the same order (the gains and P are bit-identical), in
 // three phases instead of four, each issuing all of its LDS reads before its first FMA.
@@ -611,7 +631,9 @@ __device__ __forceinline__ void tri_ij(int t, int n, int& i, int& j) {
 // The generic stage let the compiler interleave its reads with the FMA chains that consume
 // them (one LDS latency per two products) and ran the A / B column cases of T as divergent
 // branches: ~2 k clocks per phase (tools/ric_stamps.py, lab build CMPC_RIC_SUBSTAMP).
-template <class G>
+// R = float: the same stage in fp32 (Cfg::F32; operands rounded to float on load, results
+// stored widened).
+template <class G, class R = double>
 __device__ __forceinline__ bool factor_stage_fixed(const MpcConst& c, int k, const double* Ak, double* P, double* T,
                                                    double* Gm, const double* th, double* __restrict__ Fk, int ms,
                                                    unsigned long long* sub) {
@@ -635,8 +657,8 @@ __device__ __forceinline__ bool factor_stage_fixed(const MpcConst& c, int k, con
 #endif
     // ---- phase 1: T ----
     {
-        double pr[RT][NX], cv[RT][NX];
-        double pu[NU][NU];
+        R pr[RT][NX], cv[RT][NX];
+        R pu[NU][NU];
 #pragma unroll
         for (int q = 0; q < RT; ++q) {
             int e = l + q * kWave;
@@ -646,18 +668,18 @@ __device__ __forceinline__ bool factor_stage_fixed(const MpcConst& c, int k, con
             const int ld = (j < NX) ? NX : NU;
 #pragma unroll
             for (int s = 0; s < NX; ++s) {
-                pr[q][s] = P[i * NA + s];
-                cv[q][s] = col[s * ld];
+                pr[q][s] = (R)P[i * NA + s];
+                cv[q][s] = (R)col[s * ld];
             }
         }
 #pragma unroll
         for (int a = 0; a < NU; ++a)
 #pragma unroll
-            for (int b = 0; b <= a; ++b) pu[a][b] = P[(NX + a) * NA + NX + b];
+            for (int b = 0; b <= a; ++b) pu[a][b] = (R)P[(NX + a) * NA + NX + b];
         __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int q = 0; q < RT; ++q) {
-            double v = 0.0;
+            R v = R(0);
 #pragma unroll
             for (int s = 0; s < NX; ++s) v = fma(pr[q][s], cv[q][s], v);
             if (l + q * kWave < NE) T[l + q * kWave] = v;
@@ -665,7 +687,7 @@ __device__ __forceinline__ bool factor_stage_fixed(const MpcConst& c, int k, con
         wsync();  // (pu: P_uu of P_{k+1}, held in registers; phase 3 overwrites P)
         FSTAMP(9)
         // ---- phase 2: G (lower triangle) ----
-        double tr[RG][NX], cg[RG][NX];
+        R tr[RG][NX], cg[RG][NX];
         int ge[RG];
 #pragma unroll
         for (int q = 0; q < RG; ++q) {
@@ -678,14 +700,14 @@ __device__ __forceinline__ bool factor_stage_fixed(const MpcConst& c, int k, con
             const int ldi = (i < NX) ? NX : NU;
 #pragma unroll
             for (int s = 0; s < NX; ++s) {
-                cg[q][s] = ci[s * ldi];
-                tr[q][s] = T[s * NC + j];
+                cg[q][s] = (R)ci[s * ldi];
+                tr[q][s] = (R)T[s * NC + j];
             }
         }
         __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int q = 0; q < RG; ++q) {
-            double v = 0.0;
+            R v = R(0);
 #pragma unroll
             for (int s = 0; s < NX; ++s) v = fma(cg[q][s], tr[q][s], v);
             if (l + q * kWave < NT) Gm[ge[q]] = v;
@@ -695,35 +717,35 @@ __device__ __forceinline__ bool factor_stage_fixed(const MpcConst& c, int k, con
         // ---- phase 3 ----
         // reads: Hvv's G / T entries, the lane's gain column, its P entries' columns
         // (the weights live in LDS too (c): their reads belong before the barrier as well)
-        double hg[NU][NU], ht1[NU][NU], ht2[NU][NU], thu[NU][2], r2[NU][NU], dr2[NU][NU];
+        R hg[NU][NU], ht1[NU][NU], ht2[NU][NU], thu[NU][2], r2[NU][NU], dr2[NU][NU];
 #pragma unroll
         for (int a = 0; a < NU; ++a) {
 #pragma unroll
             for (int b = 0; b <= a; ++b) {
-                hg[a][b] = Gm[(NX + a) * NC + NX + b];
-                ht1[a][b] = T[(NX + a) * NC + NX + b];
-                ht2[a][b] = T[(NX + b) * NC + NX + a];
-                r2[a][b] = c.R[a * NU + b];
-                dr2[a][b] = c.dR[a * NU + b];
+                hg[a][b] = (R)Gm[(NX + a) * NC + NX + b];
+                ht1[a][b] = (R)T[(NX + a) * NC + NX + b];
+                ht2[a][b] = (R)T[(NX + b) * NC + NX + a];
+                r2[a][b] = (R)c.R[a * NU + b];
+                dr2[a][b] = (R)c.dR[a * NU + b];
             }
             const int rr = ms + 2 * (k * NU + a);
-            thu[a][0] = th[rr];
-            thu[a][1] = th[rr + 1];
+            thu[a][0] = (R)th[rr];
+            thu[a][1] = (R)th[rr + 1];
         }
         // gain entry e = l (a = e / NA, column j): hv(b, j) = G[nx+b][j] + T[nx+b][j] (j < nx)
         constexpr int NK = NU * NA;
         const int ek = l < NK ? l : NK - 1;
         const int ka = ek / NA, kj = ek - ka * NA;
-        double kg[NU], kt[NU], kd[NU];
+        R kg[NU], kt[NU], kd[NU];
 #pragma unroll
         for (int b = 0; b < NU; ++b) {
             const int jj = kj < NX ? kj : 0;
-            kg[b] = Gm[(NX + b) * NC + jj];
-            kt[b] = T[(NX + b) * NC + jj];
-            kd[b] = c.dR[b * NU + (kj < NX ? 0 : kj - NX)];
+            kg[b] = (R)Gm[(NX + b) * NC + jj];
+            kt[b] = (R)T[(NX + b) * NC + jj];
+            kd[b] = (R)c.dR[b * NU + (kj < NX ? 0 : kj - NX)];
         }
         // P entries (i, j), j <= i: W + G[i][j] and the columns i, j of Hvy
-        double pw[RP], pg[RP], pd[RP], ci_g[RP][NU], ci_t[RP][NU], cj_g[RP][NU], cj_t[RP][NU], ci_d[RP][NU],
+        R pw[RP], pg[RP], pd[RP], ci_g[RP][NU], ci_t[RP][NU], cj_g[RP][NU], cj_t[RP][NU], ci_d[RP][NU],
             cj_d[RP][NU];
         int pi_[RP], pj_[RP];
 #pragma unroll
@@ -736,62 +758,62 @@ __device__ __forceinline__ bool factor_stage_fixed(const MpcConst& c, int k, con
             pj_[q] = j;
             const int ix = i < NX ? i : 0, jx = j < NX ? j : 0;
             const int iu = i < NX ? 0 : i - NX, ju = j < NX ? 0 : j - NX;
-            pw[q] = Wk[ix * NX + jx];
-            pg[q] = Gm[ix * NC + jx];
-            pd[q] = c.dR[iu * NU + ju];
+            pw[q] = (R)Wk[ix * NX + jx];
+            pg[q] = (R)Gm[ix * NC + jx];
+            pd[q] = (R)c.dR[iu * NU + ju];
 #pragma unroll
             for (int b = 0; b < NU; ++b) {
-                ci_g[q][b] = Gm[(NX + b) * NC + ix];
-                ci_t[q][b] = T[(NX + b) * NC + ix];
-                cj_g[q][b] = Gm[(NX + b) * NC + jx];
-                cj_t[q][b] = T[(NX + b) * NC + jx];
-                ci_d[q][b] = c.dR[b * NU + iu];
-                cj_d[q][b] = c.dR[b * NU + ju];
+                ci_g[q][b] = (R)Gm[(NX + b) * NC + ix];
+                ci_t[q][b] = (R)T[(NX + b) * NC + ix];
+                cj_g[q][b] = (R)Gm[(NX + b) * NC + jx];
+                cj_t[q][b] = (R)T[(NX + b) * NC + jx];
+                ci_d[q][b] = (R)c.dR[b * NU + iu];
+                cj_d[q][b] = (R)c.dR[b * NU + ju];
             }
         }
         __builtin_amdgcn_sched_barrier(0);
         // Hvv and its Cholesky factor / inverse (as the generic stage)
-        double Lf[CMPC_MAX_NU][CMPC_MAX_NU], Hi[CMPC_MAX_NU][CMPC_MAX_NU];
+        R Lf[CMPC_MAX_NU][CMPC_MAX_NU], Hi[CMPC_MAX_NU][CMPC_MAX_NU];
         bool ok = true;
 #pragma unroll
         for (int a = 0; a < CMPC_MAX_NU; ++a)
 #pragma unroll
             for (int b = 0; b < CMPC_MAX_NU; ++b) {
-                double v = 0.0;
+                R v = R(0);
                 if (a < NU && b <= a) {
-                    v = 2.0 * r2[a][b] + 2.0 * dr2[a][b] + hg[a][b] + ht1[a][b] + ht2[a][b] + pu[a][b];
+                    v = R(2.0) * r2[a][b] + R(2.0) * dr2[a][b] + hg[a][b] + ht1[a][b] + ht2[a][b] + pu[a][b];
                     if (a == b) v += thu[a][0] + thu[a][1];
                 }
                 Lf[a][b] = v;
             }
 #pragma unroll
         for (int j = 0; j < NU; ++j) {
-            double dj = Lf[j][j];
+            R dj = Lf[j][j];
 #pragma unroll
             for (int p = 0; p < j; ++p) dj = fma(-Lf[j][p], Lf[j][p], dj);
-            ok = ok && (dj > 0.0);
-            const double rs = rsqrt_d(dj > 0.0 ? dj : 1.0);
+            ok = ok && (dj > R(0));
+            const R rs = rsqrt_r(dj > R(0) ? dj : R(1));
             Lf[j][j] = dj * rs;
 #pragma unroll
             for (int i = j + 1; i < NU; ++i) {
-                double v = Lf[i][j];
+                R v = Lf[i][j];
 #pragma unroll
                 for (int p = 0; p < j; ++p) v = fma(-Lf[i][p], Lf[j][p], v);
                 Lf[i][j] = v * rs;
             }
         }
-        double Li[CMPC_MAX_NU][CMPC_MAX_NU];
+        R Li[CMPC_MAX_NU][CMPC_MAX_NU];
 #pragma unroll
         for (int i = 0; i < CMPC_MAX_NU; ++i)
 #pragma unroll
-            for (int j = 0; j < CMPC_MAX_NU; ++j) Li[i][j] = 0.0;
+            for (int j = 0; j < CMPC_MAX_NU; ++j) Li[i][j] = R(0);
 #pragma unroll
         for (int i = 0; i < NU; ++i) {
-            const double di = rcp_d(Lf[i][i]);
+            const R di = rcp_r(Lf[i][i]);
             Li[i][i] = di;
 #pragma unroll
             for (int j = 0; j < i; ++j) {
-                double v = 0.0;
+                R v = R(0);
 #pragma unroll
                 for (int p = j; p < i; ++p) v = fma(Lf[i][p], Li[p][j], v);
                 Li[i][j] = -v * di;
@@ -801,19 +823,19 @@ __device__ __forceinline__ bool factor_stage_fixed(const MpcConst& c, int k, con
         for (int a = 0; a < CMPC_MAX_NU; ++a)
 #pragma unroll
             for (int b = 0; b < CMPC_MAX_NU; ++b) {
-                double v = 0.0;
+                R v = R(0);
 #pragma unroll
                 for (int p = 0; p < CMPC_MAX_NU; ++p) v = fma(Li[p][a], Li[p][b], v);
                 Hi[a][b] = v;
             }
         // hv(b, col) and K(a, col) = sum_b -Hinv[a][b] hv(b, col), in the generic stage's order
-        auto hv = [&](int col, double g, double t, double dr) { return (col < NX) ? g + t : -2.0 * dr; };
+        auto hv = [&](int col, R g, R t, R dr) { return (col < NX) ? g + t : R(-2.0) * dr; };
         // the lane's gain entry and Hinv entry
         {
-            double kv = 0.0;
+            R kv = R(0);
 #pragma unroll
             for (int b = 0; b < NU; ++b) {
-                double hab = 0.0;
+                R hab = R(0);
 #pragma unroll
                 for (int a2 = 0; a2 < NU; ++a2)
                     if (a2 == ka) hab = Hi[a2][b];
@@ -822,7 +844,7 @@ __device__ __forceinline__ bool factor_stage_fixed(const MpcConst& c, int k, con
             if (l < NK) Fk[l] = kv;
             if (l < NU * NU) {
                 const int a = l / NU, b = l - a * NU;
-                double v = 0.0;
+                R v = R(0);
 #pragma unroll
                 for (int a2 = 0; a2 < NU; ++a2)
 #pragma unroll
@@ -836,10 +858,10 @@ __device__ __forceinline__ bool factor_stage_fixed(const MpcConst& c, int k, con
 #pragma unroll
             for (int q = 0; q < RP; ++q) {
                 const int i = pi_[q], j = pj_[q];
-                double v = (i < NX) ? pw[q] + pg[q] : ((j >= NX) ? 2.0 * pd[q] : 0.0);
+                R v = (i < NX) ? pw[q] + pg[q] : ((j >= NX) ? R(2.0) * pd[q] : R(0));
 #pragma unroll
                 for (int a = 0; a < NU; ++a) {
-                    double kv = 0.0;
+                    R kv = R(0);
 #pragma unroll
                     for (int b = 0; b < NU; ++b) kv = fma(-Hi[a][b], hv(j, cj_g[q][b], cj_t[q][b], cj_d[q][b]), kv);
                     v = fma(hv(i, ci_g[q][a], ci_t[q][a], ci_d[q][a]), kv, v);
@@ -858,8 +880,9 @@ __device__ __forceinline__ bool factor_stage_fixed(const MpcConst& c, int k, con
 
 // Riccati factorisation of the Newton system at the current (th, Dsig), with the stage weights
 // Wg of stage_weights: writes the gains K_k = -Hvv^-1 Hvy and Hinv_k = Hvv^-1 of every stage
-// into F.  Returns false on a non-positive pivot (wave-uniform).
-template <class G>
+// into F.  Returns false on a non-positive pivot (wave-uniform).  R = float: the fp32 stages of
+// Cfg::F32 (fixed dimensions only).
+template <class G, class R = double>
 __device__ __forceinline__ bool riccati_factor(const MpcConst& c, const Dims& d, const RLds& L, double* sm,
                                const double* __restrict__ A, const double* __restrict__ B,
                                const double* __restrict__ Wg, double* __restrict__ F,
@@ -896,7 +919,7 @@ __device__ __forceinline__ bool riccati_factor(const MpcConst& c, const Dims& d,
     bool ok = true;
     sweep(pp, [&](int k, const double* Ak) {
       if constexpr (G::NX != 0) {
-        ok = factor_stage_fixed<G>(c, k, Ak, P, T, Gm, th, F + (size_t)k * d.sF, ms, sub) && ok;
+        ok = factor_stage_fixed<G, R>(c, k, Ak, P, T, Gm, th, F + (size_t)k * d.sF, ms, sub) && ok;
       } else {
         const double* Bk = Ak + d.sA;
         SUBSTAMP(-1)  // slots 9-11: T, G, Hvv..K; the rest of the factor (P update, stage advance) is slot 2 minus them
@@ -1216,7 +1239,9 @@ __device__ __forceinline__ bool riccati_factor_dd(const MpcConst& c, const Dims&
 // is formed inside the backward sweep: with s = psi + p_x (p the Riccati costate) both
 // recursions become one, s_k = yb_k + A_k' s_{k+1} + (K_k'g)_x, g = p_u + rd_k + rt_u + B_k' s_{k+1}
 // — one sweep fewer per pass.
-template <class G>
+// R = float (Cfg::F32): the backward recursion (g, p) and the forward feedback v_k in fp32 with the
+// fp32 gains; the right-hand side, dU and the direction's state recursion dX in fp64.
+template <class G, class R = double>
 __device__ __forceinline__ void riccati_solve(const MpcConst& c, const Dims& d, const RLds& L, double* sm,
                               const double* __restrict__ A, const double* __restrict__ B,
                               const double* __restrict__ F, const double* rh, double* dU, double* dX,
@@ -1244,33 +1269,33 @@ __device__ __forceinline__ void riccati_solve(const MpcConst& c, const Dims& d, 
                 // fixed dimensions: every read of the step issued before its chains (same sums)
                 constexpr int NX = G::NX, NU = G::NU, NA = NX + NU;
                 const int lx = l < NX ? l : NX - 1, la = l < NA ? l : NA - 1, lu = l < NU ? l : NU - 1;
-                double p[NA], bm[NX][NU], ac[NX], kg[NU], hg[NU], r0[NU];
+                R p[NA], bm[NX][NU], ac[NX], kg[NU], hg[NU], r0[NU];
 #pragma unroll
                 for (int s2 = 0; s2 < NX; ++s2) {
 #pragma unroll
-                    for (int a = 0; a < NU; ++a) bm[s2][a] = Bk[s2 * NU + a];
-                    ac[s2] = Ak[s2 * NX + lx];
+                    for (int a = 0; a < NU; ++a) bm[s2][a] = (R)Bk[s2 * NU + a];
+                    ac[s2] = (R)Ak[s2 * NX + lx];
                 }
 #pragma unroll
                 for (int a = 0; a < NU; ++a) {
                     const int ci = k * NU + a;
-                    r0[a] = yb ? rd[ci] + (rt[ms + 2 * ci] - rt[ms + 2 * ci + 1]) : -rh[ci];
-                    kg[a] = Kg[a * NA + la];
-                    hg[a] = Hg[lu * NU + a];
+                    r0[a] = (R)(yb ? rd[ci] + (rt[ms + 2 * ci] - rt[ms + 2 * ci + 1]) : -rh[ci]);
+                    kg[a] = (R)Kg[a * NA + la];
+                    hg[a] = (R)Hg[lu * NU + a];
                 }
-                const double y0 = (yb && l < NX) ? yb[k * NX + l] : 0.0;
+                const R y0 = (R)((yb && l < NX) ? yb[k * NX + l] : 0.0);
 #pragma unroll
-                for (int s2 = 0; s2 < NA; ++s2) p[s2] = pc[s2];
+                for (int s2 = 0; s2 < NA; ++s2) p[s2] = (R)pc[s2];
                 __builtin_amdgcn_sched_barrier(0);
-                double g[NU];
+                R g[NU];
 #pragma unroll
                 for (int a = 0; a < NU; ++a) {
-                    double v = p[NX + a] + r0[a];
+                    R v = p[NX + a] + r0[a];
 #pragma unroll
                     for (int s2 = 0; s2 < NX; ++s2) v = fma(bm[s2][a], p[s2], v);
                     g[a] = v;
                 }
-                double v = y0;
+                R v = y0;
                 if (l < NX) {
 #pragma unroll
                     for (int s2 = 0; s2 < NX; ++s2) v = fma(ac[s2], p[s2], v);
@@ -1279,7 +1304,7 @@ __device__ __forceinline__ void riccati_solve(const MpcConst& c, const Dims& d, 
                 for (int a = 0; a < NU; ++a) v = fma(kg[a], g[a], v);
                 if (l < NA) pn[l] = v;
                 if (l < NU) {
-                    double u = 0.0;
+                    R u = R(0);
 #pragma unroll
                     for (int b = 0; b < NU; ++b) u = fma(-hg[b], g[b], u);
                     dU[k * NU + l] = u;
@@ -1330,13 +1355,14 @@ __device__ __forceinline__ void riccati_solve(const MpcConst& c, const Dims& d, 
                 // fixed dimensions: every read of the step issued before its chains (same sums)
                 constexpr int NX = G::NX, NU = G::NU, NA = NX + NU;
                 const int lx = l < NX ? l : NX - 1;
-                double x[NX], kg[NU][NA], d0[NU], dp[NU], ar[NX], br[NU];
+                double x[NX], ar[NX], br[NU];
+                R kg[NU][NA], d0[NU], dp[NU];
 #pragma unroll
                 for (int a = 0; a < NU; ++a) {
 #pragma unroll
-                    for (int j = 0; j < NA; ++j) kg[a][j] = Kg[a * NA + j];
-                    d0[a] = dU[k * NU + a];
-                    dp[a] = dU[(k > 0 ? k - 1 : 0) * NU + a];
+                    for (int j = 0; j < NA; ++j) kg[a][j] = (R)Kg[a * NA + j];
+                    d0[a] = (R)dU[k * NU + a];
+                    dp[a] = (R)dU[(k > 0 ? k - 1 : 0) * NU + a];
                     br[a] = Bk[lx * NU + a];
                 }
 #pragma unroll
@@ -1344,12 +1370,12 @@ __device__ __forceinline__ void riccati_solve(const MpcConst& c, const Dims& d, 
 #pragma unroll
                 for (int t = 0; t < NX; ++t) x[t] = xc[t];
                 __builtin_amdgcn_sched_barrier(0);
-                double vk[NU];
+                R vk[NU];
 #pragma unroll
                 for (int a = 0; a < NU; ++a) {
-                    double v = d0[a];
+                    R v = d0[a];
 #pragma unroll
-                    for (int j = 0; j < NX; ++j) v = fma(kg[a][j], x[j], v);
+                    for (int j = 0; j < NX; ++j) v = fma(kg[a][j], (R)x[j], v);
                     if (k > 0)
 #pragma unroll
                         for (int b = 0; b < NU; ++b) v = fma(kg[a][NX + b], dp[b], v);
@@ -1359,7 +1385,7 @@ __device__ __forceinline__ void riccati_solve(const MpcConst& c, const Dims& d, 
 #pragma unroll
                 for (int t = 0; t < NX; ++t) v = fma(ar[t], x[t], v);
 #pragma unroll
-                for (int a = 0; a < NU; ++a) v = fma(br[a], vk[a], v);
+                for (int a = 0; a < NU; ++a) v = fma(br[a], (double)vk[a], v);
                 if (l < NX) {
                     xb[((k + 1) & 1) * NX + l] = v;
                     if (dX) dX[(k + 1) * NX + l] = v;
@@ -1545,6 +1571,7 @@ __global__ __launch_bounds__(kWave) void mpc_riccati_kernel(const MpcConst c_arg
     // double-double near the solution: a continued (rescue) solve from the start, a cold one only
     // once the fp64 recursion stops making progress or breaks down (kDdStall)
     bool dd_on = warm;
+    bool f32_on = G::F32 && !warm;  // Cfg::F32: fp32 factorisation and recursions until kRicF32Stall
     const int it0 = warm ? (int)hand[1] : 0;
     if (warm) {
         for (int i = l; i < n; i += kWave) U[i] = hand[2 + i];
@@ -1719,12 +1746,25 @@ __global__ __launch_bounds__(kWave) void mpc_riccati_kernel(const MpcConst c_arg
         double thm_l = 0.0;
         for (int r = l; r < m; r += kWave) thm_l = fmax(thm_l, th[r]);
         const bool above = wave_max(thm_l) > kDdTh;  // wave-uniform
-        if (!dd_on && it - best_it >= kDdStall) dd_on = true;
-        bool hp = above && dd_on;
+        if (f32_on && it - best_it >= kRicF32Stall) f32_on = false;
+        if (!f32_on && !dd_on && it - best_it >= kDdStall) dd_on = true;
+        bool hp = above && dd_on && !f32_on;
         wsync();
         RSTAMP(1);
-        bool fact_ok = hp ? riccati_factor_dd<G>(c, d, L, sm, A, B, Wg, F)
-                          : riccati_factor<G>(c, d, L, sm, A, B, Wg, F, stamp ? tsum : nullptr);
+        bool fact_ok;
+        if constexpr (G::F32) {
+            fact_ok = f32_on ? riccati_factor<G, float>(c, d, L, sm, A, B, Wg, F)
+                             : (hp ? riccati_factor_dd<G>(c, d, L, sm, A, B, Wg, F)
+                                   : riccati_factor<G>(c, d, L, sm, A, B, Wg, F, stamp ? tsum : nullptr));
+            if (!fact_ok && f32_on) {  // fp32 breakdown: this iteration and the rest in fp64
+                gsync();
+                f32_on = false;
+                fact_ok = riccati_factor<G>(c, d, L, sm, A, B, Wg, F);
+            }
+        } else {
+            fact_ok = hp ? riccati_factor_dd<G>(c, d, L, sm, A, B, Wg, F)
+                         : riccati_factor<G>(c, d, L, sm, A, B, Wg, F, stamp ? tsum : nullptr);
+        }
         if (!fact_ok && !hp && above) {  // fp64 breakdown above the threshold: this iteration and the rest in dd
             gsync();
             dd_on = hp = true;
@@ -1779,7 +1819,14 @@ __global__ __launch_bounds__(kWave) void mpc_riccati_kernel(const MpcConst c_arg
             wsync();
             if (!hp) {
                 RSTAMP(4);
-                riccati_solve<G>(c, d, L, sm, A, B, F, nullptr, dU, dX, yb, rd, rt);  // rhs fused in
+                bool done = false;
+                if constexpr (G::F32) {
+                    if (f32_on) {
+                        riccati_solve<G, float>(c, d, L, sm, A, B, F, nullptr, dU, dX, yb, rd, rt);
+                        done = true;
+                    }
+                }
+                if (!done) riccati_solve<G>(c, d, L, sm, A, B, F, nullptr, dU, dX, yb, rd, rt);  // rhs fused in
                 RSTAMP(5);
             } else {
                 adjoint<G>(c, d, sAB, sb, yb, rh, psi);
@@ -1928,6 +1975,8 @@ __global__ __launch_bounds__(kWave) void mpc_riccati_kernel(const MpcConst c_arg
 
 }  // namespace
 
+bool mpc_riccati_f32_supported(const MpcConst& c) { return c.nx == 6 && c.nu == 3 && c.mc == 6; }
+
 size_t mpc_riccati_lds_bytes(const MpcConst& c) { return sizeof(double) * (size_t)r_layout(c).total; }
 
 size_t mpc_riccati_ws_doubles(const MpcConst& c) { return r_glb(c).total; }
@@ -1949,7 +1998,10 @@ hipError_t mpc_riccati_launch(const MpcConst& c, const MpcPtrs& p, int batch, hi
         return hipSuccess;
     };
     hipError_t e;
-    if (c.nx == 9 && c.nu == 2 && c.mc == 5) e = go(Cfg<kPerSmall, 9, 2, 5>{});
+    if (c.f32) {  // BASELINE cfg5's fp32 path (mpc_riccati_f32_supported)
+        if (!mpc_riccati_f32_supported(c)) return hipErrorInvalidValue;
+        e = r_rows_global(c) ? go(Cfg<kPerSmall, 6, 3, 6, true, true>{}) : go(Cfg<kPerSmall, 6, 3, 6, false, true>{});
+    } else if (c.nx == 9 && c.nu == 2 && c.mc == 5) e = go(Cfg<kPerSmall, 9, 2, 5>{});
     else if (c.nx == 9 && c.nu == 2 && c.mc == 6) e = go(Cfg<kPerSmall, 9, 2, 6>{});
     else if (c.nx == 9 && c.nu == 2 && c.mc == 7) e = go(Cfg<kPerSmall, 9, 2, 7>{});
     else if (c.nx == 4 && c.nu == 2) e = go(Cfg<kPerSmall, 4, 2, 0>{});

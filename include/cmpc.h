@@ -71,11 +71,12 @@ extern "C" {
 typedef struct cmpc_ctx cmpc_ctx;
 
 #define CMPC_FLAG_GENERIC 1  /* force the generic (runtime-dimension) kernel */
-#define CMPC_FLAG_FP32 8     /* fp32 path (BASELINE cfg5): where the lane-per-agent kernel is instantiated
-                                (nx,nu,mc,ns = 6,3,6,3 or 4,2,6,3) its Riccati factorisation and Newton
-                                recursions run in fp32 with fp64 iterates / residuals and a per-agent fp64
-                                finish (opts.tol ~1e-6); elsewhere the fp32 workgroup-per-agent condensed
-                                solver (N*nu <= 256, opts.tol ~1e-5) */
+#define CMPC_FLAG_FP32 8     /* fp32 path (BASELINE cfg5): the Riccati factorisation and Newton recursions in
+                                fp32 with fp64 iterates / residuals and a per-agent fp64 finish (opts.tol
+                                ~1e-6) — on the stage-wise Riccati kernel where it has an fp32 instantiation
+                                (nx,nu,mc = 6,3,6), on the lane-per-agent kernel with CMPC_FLAG_LANE or where
+                                only that one is instantiated (nx,nu,mc,ns = 6,3,6,3 or 4,2,6,3); elsewhere the
+                                fp32 workgroup-per-agent condensed solver (N*nu <= 256, opts.tol ~1e-5) */
 #define CMPC_FLAG_RICCATI 16 /* force the stage-wise Riccati solver (fp64; the default when N*nu > 64) */
 #define CMPC_FLAG_RESCUE 32 /* condensed solves (fp64): an agent whose factorisation breaks down short of
                                1e3 tol (status CMPC_UNSOLVED) continues from its last iterate on the

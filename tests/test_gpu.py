@@ -593,20 +593,22 @@ def _cfg5_problem(n, rounds=2):
     return R.snapshot()
 
 
-def test_cfg5_fp32_path_at_scale_vs_fp64(gpu_ctx):
-    """BASELINE cfg5 at its size: 8192 agents on the fp32 path (lane-per-agent kernel, fp32 Riccati
-    factorisation, fp64 iterates) against the fp64 stage-wise Riccati kernel on every agent and the
-    fp64 C restatement (Riccati, double-double near the solution) on a 128-agent sample."""
+@pytest.mark.parametrize("lane", [False, True])
+def test_cfg5_fp32_path_at_scale_vs_fp64(gpu_ctx, lane):
+    """BASELINE cfg5 at its size: 8192 agents on the fp32 path (fp32 Riccati factorisation and
+    Newton recursions, fp64 iterates; the Riccati kernel's fp32 mode, and with CMPC_FLAG_LANE the
+    lane-per-agent kernel) against the fp64 stage-wise Riccati kernel on every agent and the fp64 C
+    restatement (Riccati, double-double near the solution) on a 128-agent sample."""
     import cmpc
     from oracle import cmpc_oracle as CO
 
     n, ns = 8192, 128
     P = _cfg5_problem(n)
-    z, kkt, it, st = cmpc.solve_mpc(P, gpu_ctx, fp32=True)
+    z, kkt, it, st = cmpc.solve_mpc(P, gpu_ctx, fp32=True, lane=lane)
     zr, _, _, sr = cmpc.solve_mpc(P, gpu_ctx, riccati=True)
     frac = float((st == cmpc.CMPC_SOLVED).mean())
     err = (np.abs(z - zr) / np.maximum(1.0, np.abs(zr))).max(1)
-    print(f"cfg5 fp32 x{n}: solved {frac:.4f} status {np.unique(st, return_counts=True)} iters mean {it.mean():.1f} "
+    print(f"cfg5 fp32 ({'lane' if lane else 'riccati'}) x{n}: solved {frac:.4f} status {np.unique(st, return_counts=True)} iters mean {it.mean():.1f} "
           f"max {it.max()} | vs fp64 kernel: max rel err {err.max():.2e} (fp64 solved {np.mean(sr == 1):.4f})")
     assert frac >= 0.99 and np.isin(st, (cmpc.CMPC_SOLVED, cmpc.CMPC_SOLVED_INACCURATE)).all()
     assert np.isfinite(z).all() and err.max() < FP32_ZTOL
@@ -616,16 +618,17 @@ def test_cfg5_fp32_path_at_scale_vs_fp64(gpu_ctx):
     assert np.isin(stc, (1, 2)).all() and ec.max() < FP32_ZTOL, ec.max()
 
 
-def test_cfg5_fp32_path_small_batches(gpu_ctx):
-    """Ragged batches (not a multiple of the 32 agents of a wavefront) and a single agent: same
-    answers agent by agent as the full batch (no cross-lane coupling)."""
+@pytest.mark.parametrize("lane", [False, True])
+def test_cfg5_fp32_path_small_batches(gpu_ctx, lane):
+    """Ragged batches (not a multiple of the 32 agents of a lane-kernel wavefront) and a single
+    agent: same answers agent by agent as the full batch (no coupling between agents)."""
     import cmpc
 
     P = _cfg5_problem(100, rounds=1)
-    z, _, it, st = cmpc.solve_mpc(P, gpu_ctx, fp32=True)
+    z, _, it, st = cmpc.solve_mpc(P, gpu_ctx, fp32=True, lane=lane)
     for sl in (slice(0, 1), slice(3, 40), slice(37, 100)):
         Q = {k: (v[sl] if isinstance(v, np.ndarray) and v.ndim and v.shape[0] == 100 else v) for k, v in P.items()}
-        zq, _, iq, sq = cmpc.solve_mpc(Q, gpu_ctx, fp32=True)
+        zq, _, iq, sq = cmpc.solve_mpc(Q, gpu_ctx, fp32=True, lane=lane)
         np.testing.assert_array_equal(zq, z[sl])
         np.testing.assert_array_equal(iq, it[sl])
 

@@ -1,6 +1,6 @@
 # usage: bash tools/gpu_round.sh TAG — GPU tests, smoke, bench (cfg3 default, cfg5, cfg5 --fp32), rocprofv3
 # kernel-trace stats of the same bench command, and PMC passes (FETCH_SIZE, WRITE_SIZE, one each) of the
-# cfg3 solver, the cfg5 Riccati kernel and the cfg5 fp32 lane kernel for the HBM traffic figures, and the
+# cfg3 solver, the cfg5 Riccati kernel and its fp32 mode for the HBM traffic figures, and the
 # per-section clocks of the Riccati kernel (tools/ric_stamps.py: N = 125 captured QPs, cfg5).
 # Every GPU step has its own time limit; steps are chained with && (stop at the first failure).
 set -o pipefail
