@@ -133,7 +133,9 @@ def osqp_solve_qp_batch(qps, ctx=None, tol=None, max_iter=None, structured=True)
             groups.setdefault(St.shared_key(p), []).append(i)
     for idx in groups.values():
         batch = St.stack([recs[i] for i in idx])
-        z, kkt, it, st = solve_mpc(batch, ctx, tol=tol, max_iter=max_iter)
+        # CMPC_FLAG_RESCUE, as PlannerLPV / PlannerLPVBatch: a condensed factorisation breakdown
+        # continues on the stage-wise kernel instead of returning CMPC_UNSOLVED (OSQP's -10)
+        z, kkt, it, st = solve_mpc(batch, ctx, tol=tol, max_iter=max_iter, rescue=True)
         for a, i in enumerate(idx):
             P, q, G, h, A, b = qps[i][:6]
             x = z[a]
