@@ -27,10 +27,56 @@ LPV_LAYOUT = (9, 3, 2)   # PlannerLPV: n_s = 9 states, 3 slacks, n_u = 2 inputs 
 
 
 def _csr(a):
+    """Canonical csr (sorted indices, no duplicates, no stored zeros) of ``a``; a float64 csr
+    input that is canonical already is returned as it is (the reference's scipy matrices)."""
+    if sp.issparse(a) and a.format == "csr" and a.dtype == np.float64 and a.has_canonical_format \
+            and a.data.all():
+        return a
     m = sp.csr_matrix(a, dtype=np.float64)
     m.sum_duplicates()
     m.eliminate_zeros()
     return m
+
+
+def _canon(rows, cols, vals, shape):
+    """Canonical csr arrays (indptr, indices, data) of coordinate triples without duplicates:
+    stored zeros dropped, entries ordered by row then column, as _csr gives them."""
+    keep = vals != 0.0
+    rows, cols, vals = rows[keep], cols[keep], vals[keep]
+    o = np.lexsort((cols, rows))
+    rows, cols = rows[o], cols[o]
+    if rows.size > 1 and ((np.diff(rows) == 0) & (np.diff(cols) == 0)).any():
+        raise ValueError("duplicate entries")   # never for the reference form: one entry per slot
+    indptr = np.zeros(shape[0] + 1, np.int64)
+    np.cumsum(np.bincount(rows, minlength=shape[0]), out=indptr[1:])
+    return indptr, cols, vals[o], shape
+
+
+def _matrix(c):
+    indptr, indices, data, shape = c
+    return sp.csr_matrix((data, indices, indptr), shape=shape)
+
+
+def _same_canon(X, c):
+    """X (canonical csr) equal entry for entry to the canonical arrays c."""
+    indptr, indices, data, shape = c
+    return X.shape == shape and np.array_equal(X.indptr, indptr) and np.array_equal(X.indices, indices) \
+        and np.array_equal(X.data, data)
+
+
+def _rows_of(X):
+    return np.repeat(np.arange(X.shape[0]), np.diff(X.indptr))
+
+
+def _dense_block(X, r0, r1, c0, c1):
+    """X[r0:r1, c0:c1] as a dense array, read from the canonical csr arrays."""
+    out = np.zeros((r1 - r0, c1 - c0))
+    for r in range(r0, r1):
+        s, e = X.indptr[r], X.indptr[r + 1]
+        c = X.indices[s:e]
+        m = (c >= c0) & (c < c1)
+        out[r - r0, c[m] - c0] = X.data[s:e][m]
+    return out
 
 
 def dims_of(nz, m_ineq, m_eq, layout=LPV_LAYOUT):
@@ -58,16 +104,25 @@ def _cost_matrix(N, ne, nu, qt, r, dr):
     if P is None:
         blocks = [np.frombuffer(qt).reshape(ne, ne)] * (N + 1) + [np.frombuffer(r).reshape(nu, nu)] * N + \
                  [np.frombuffer(dr).reshape(nu, nu)] * N
-        P = _csr(sp.block_diag(blocks, format="csr") * 2.0)
+        m = _csr(sp.block_diag(blocks, format="csr") * 2.0)
+        P = (m.indptr.astype(np.int64), m.indices.astype(np.int64), m.data.copy(), m.shape)
+        for a_ in P[:3]:
+            a_.setflags(write=False)
         if len(_COST_CACHE) > 64:
             _COST_CACHE.clear()
         _COST_CACHE[key] = P
-    return P.copy()
+    return P
 
 
 def reference_form(p, a=0):
     """Sparse reference-form QP (P, q, G, h, Aeq, beq) of agent ``a`` of a structured problem
     dict (the keys of include/cmpc.h; row_slack / row_sign give the slack pattern)."""
+    P, q, G, h, Aeq, beq = _reference_canon(p, a)
+    return _matrix(P), q, _matrix(G), h, _matrix(Aeq), beq
+
+
+def _reference_canon(p, a=0):
+    """reference_form with the three matrices as canonical csr arrays (see _canon)."""
     nx, nu, N, ns, mc = (int(p[k]) for k in ("nx", "nu", "N", "ns", "mc"))
     ne = nx + ns
     nz = ne * (N + 1) + 2 * nu * N
@@ -103,8 +158,8 @@ def reference_form(p, a=0):
     rows += [ru.ravel(), (ru + 1).ravel()]
     cols += [cu_i.ravel(), cu_i.ravel()]
     vals += [np.ones(N * nu), -np.ones(N * nu)]
-    G = sp.csr_matrix((np.concatenate(vals), (np.concatenate(rows), np.concatenate(cols))),
-                      shape=(ms + 2 * nu * N, nz))
+    G = _canon(np.concatenate(rows), np.concatenate(cols), np.concatenate(vals).astype(np.float64),
+               (ms + 2 * nu * N, nz))
     h = np.concatenate([np.asarray(p["h"][a], float).ravel(),
                         np.stack([np.broadcast_to(np.asarray(p["u_ub"], float), (N, nu)),
                                   np.broadcast_to(-np.asarray(p["u_lb"], float), (N, nu))], -1).ravel()])
@@ -129,16 +184,12 @@ def reference_form(p, a=0):
     rows += [rr, rr, rr[~first]]
     cols += [(cu + i * nu + j).ravel(), (cd + i * nu + j).ravel(), (cu + (i - 1) * nu + j).ravel()[~first]]
     vals += [np.where(first, 1.0, -1.0), np.where(first, -1.0, 1.0), np.ones((~first).sum())]
-    Aeq = sp.csr_matrix((np.concatenate(vals), (np.concatenate(rows), np.concatenate(cols))),
-                        shape=(ne * (N + 1) + nu * N, nz))
-    beq = np.zeros(Aeq.shape[0])
+    Aeq = _canon(np.concatenate(rows), np.concatenate(cols), np.concatenate(vals).astype(np.float64),
+                 (ne * (N + 1) + nu * N, nz))
+    beq = np.zeros(Aeq[3][0])
     beq[:nx] = p["x0"][a]
     beq[r0:r0 + nu] = p["u_prev"][a]
-    return _csr(P), q, _csr(G), h, _csr(Aeq), beq
-
-
-def _same(X, Y):
-    return X.shape == Y.shape and (X != Y).nnz == 0
+    return P, q, G, h, Aeq, beq
 
 
 def recognize(P, q, G, h, A, b, layout=LPV_LAYOUT):
@@ -162,16 +213,15 @@ def recognize(P, q, G, h, A, b, layout=LPV_LAYOUT):
     if not (np.isfinite(q).all() and np.isfinite(b).all()) or np.isnan(h).any():
         return None
     # cost (P / 2 and q / 2 are exact in binary floating point)
-    Pd = P[:ne, :ne].toarray() / 2.0
+    Pd = _dense_block(P, 0, ne, 0, ne) / 2.0
     Q, Qs = Pd[:nx, :nx], np.diag(Pd[nx:, nx:]).copy()
-    R = P[cu:cu + nu, cu:cu + nu].toarray() / 2.0
-    dR = P[cd:cd + nu, cd:cd + nu].toarray() / 2.0
+    R = _dense_block(P, cu, cu + nu, cu, cu + nu) / 2.0
+    dR = _dense_block(P, cd, cd + nu, cd, cd + nu) / 2.0
     if ns and not (Qs > 0).all():
         return None
     qlin = q[: ne * (N + 1)].reshape(N + 1, ne)[:, :nx] / 2.0
     # dynamics from the equality rows
-    Ac = A.tocoo()
-    r, c, v = Ac.row, Ac.col, Ac.data
+    r, c, v = _rows_of(A), A.indices, A.data
     kr, sr = r // ne, r % ne
     dyn = (r < ne * (N + 1)) & (kr >= 1) & (sr < nx)
     Am = np.zeros((N, nx, nx))
@@ -183,8 +233,7 @@ def recognize(P, q, G, h, A, b, layout=LPV_LAYOUT):
     x0 = b[:nx].copy()
     u_prev = b[ne * (N + 1): ne * (N + 1) + nu].copy()
     # stage rows and input bounds from the inequality rows
-    Gc = G.tocoo()
-    r, c, v = Gc.row, Gc.col, Gc.data
+    r, c, v = _rows_of(G), G.indices, G.data
     ms = N * mc
     st = (r < ms) & (c // ne == r // mc + 1) & (c < ne * (N + 1))
     Cm = np.zeros((N, mc, nx))
@@ -204,9 +253,9 @@ def recognize(P, q, G, h, A, b, layout=LPV_LAYOUT):
     prob = dict(nx=nx, nu=nu, N=N, ns=ns, mc=mc, Q=Q, R=R, dR=dR, Qs=Qs, u_ub=u_ub, u_lb=u_lb,
                 row_slack=row_slack, row_sign=row_sign, A=Am[None], B=Bm[None], x0=x0[None], u_prev=u_prev[None],
                 qlin=qlin[None], C=Cm[None], h=hh[None])
-    P2, q2, G2, h2, A2, b2 = reference_form(prob, 0)
-    if not (_same(P, P2) and _same(G, G2) and _same(A, A2) and np.array_equal(q, q2) and np.array_equal(b, b2)
-            and np.array_equal(h, h2)):
+    P2, q2, G2, h2, A2, b2 = _reference_canon(prob, 0)
+    if not (_same_canon(P, P2) and _same_canon(G, G2) and _same_canon(A, A2) and np.array_equal(q, q2)
+            and np.array_equal(b, b2) and np.array_equal(h, h2)):
         return None
     return prob
 

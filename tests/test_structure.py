@@ -69,3 +69,27 @@ def test_stack_and_shared_key():
     assert len(keys) == 1
     s = St.stack(ps)
     assert s["A"].shape == (len(cs), 30, 9, 9) and s["C"].shape[0] == len(cs)
+
+
+def test_non_canonical_inputs_are_recognised_alike():
+    """The fast path compares canonical csr arrays; inputs that are not canonical (COO, an entry
+    split into two duplicates, stored zeros, dense arrays, unsorted indices) are canonicalised
+    first and give the same structured problem."""
+    _, c = next(iter(lpv_qps("lpv_n10_a2")))
+    P, q, G, h, A, b = _args(c)
+    ref = St.recognize(P, q, G, h, A, b)
+    Gc = G.tocoo()
+    split = sp.coo_matrix((np.concatenate([Gc.data * 0.5, Gc.data * 0.5, [0.0]]),
+                           (np.concatenate([Gc.row, Gc.row, [0]]), np.concatenate([Gc.col, Gc.col, [1]]))),
+                          shape=G.shape)
+    Au = A.copy()
+    Au.has_sorted_indices = False
+    for i in range(Au.shape[0]):                          # reverse every row's index order
+        s, e = Au.indptr[i], Au.indptr[i + 1]
+        Au.indices[s:e] = Au.indices[s:e][::-1].copy()
+        Au.data[s:e] = Au.data[s:e][::-1].copy()
+    for args in ((P.tocoo(), q, split, h, A.toarray(), b), (P, q, G, h, Au, b)):
+        p = St.recognize(*args)
+        assert p is not None
+        for k, v in ref.items():
+            np.testing.assert_array_equal(p[k], v)
