@@ -296,7 +296,7 @@ def reference_config_cpu(bp, args, res, z_cert):
             "max_abs_err_vs_gpu": max(errg)}
 
 
-def lpv_population(ctx, replicas=341, rescue=True, finish=False):
+def lpv_population(ctx, replicas=341, rescue=True, finish=False, riccati=False):
     """The population of the `lpv_rounds` line: `replicas` copies of the reference's 3-agent
     Highway scenario at its captured step 0 (tests/golden/lpv_n30_a3: x0, Last_xPredicted, uPred,
     OldSteering/OldAccelera, positions), each copy's initial v_x scaled by a seeded factor in
@@ -329,7 +329,9 @@ def lpv_population(ctx, replicas=341, rescue=True, finish=False):
                max_ac=5.0, max_dc=10.0, sm=0.9)
     bp = cmpc.PlannerLPVBatch(Q, 1e7 * np.eye(3), 0.0 * np.eye(2), 50.0 * np.eye(2), N, dt, track, 5.0, model, lim,
                               ctx=ctx)
-    if not rescue:
+    if riccati:
+        bp.opts = L.opts(flags=L.CMPC_FLAG_RICCATI)
+    elif not rescue:
         bp.opts = L.opts()
     elif finish:
         bp.opts = L.opts(flags=L.CMPC_FLAG_RESCUE | L.CMPC_FLAG_FINISH)
@@ -356,7 +358,8 @@ def lpv_check_round(bp, R, sample):
     return zc, sc
 
 
-def lpv_rounds(ctx, replicas=341, rounds=20, warmup=2, rescue=True, check=True, sample=128, finish=False):
+def lpv_rounds(ctx, replicas=341, rounds=20, warmup=2, rescue=True, check=True, sample=128, finish=False,
+               riccati=False):
     """The reference's own agent model in device-resident consensus rounds (cmpc.rounds.LPVRounds:
     gather -> LPV scheduling + planes + QP build + solve -> advance -> exchange, all in HBM), at
     N = 30 (nx 9, nu 2, 2 neighbours: the v3 kernel), on lpv_population's 1023 agents.  Timed
@@ -368,7 +371,7 @@ def lpv_rounds(ctx, replicas=341, rounds=20, warmup=2, rescue=True, check=True, 
 
     from cmpc.rounds import LPVRounds
 
-    bp, args, kw = lpv_population(ctx, replicas, rescue, finish)
+    bp, args, kw = lpv_population(ctx, replicas, rescue, finish, riccati)
     N = bp.N
     R = LPVRounds(bp, *args, **kw)
     dev = R.dev
@@ -394,7 +397,7 @@ def lpv_rounds(ctx, replicas=341, rounds=20, warmup=2, rescue=True, check=True, 
                        f"round = gather + LPV build + solve + advance + exchange",
            "agent_qp_per_s": B * rounds / el, "ms_per_round": el / rounds * 1e3,
            "build_solve_ms": sum(a.elapsed_time(b) for a, b in ev) / rounds, "rounds": rounds, "warmup": warmup,
-           "rescue": rescue, "finish": finish, "mean_ipm_iters": float(it.mean()), "max_ipm_iters": int(it.max()),
+           "rescue": rescue, "finish": finish, "riccati": riccati, "mean_ipm_iters": float(it.mean()), "max_ipm_iters": int(it.max()),
            "max_ipm_iters_per_round": it.max(1).tolist(), "max_kkt": float(kk.max()),
            "status_counts": {int(k): int(v) for k, v in zip(*np.unique(st, return_counts=True))}}
     if check:

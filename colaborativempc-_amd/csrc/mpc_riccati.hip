@@ -53,6 +53,13 @@ constexpr int kDdStall = 2;
 // Cfg::F32: an agent leaves fp32 for good after this many iterations without a new best iterate
 // (or at an fp32 factorisation breakdown) — the lane kernel's kF32Stall (lane_body.h)
 constexpr int kRicF32Stall = 2;
+#ifndef RIC_P1
+#define RIC_P1 1
+#endif
+#ifndef RIC_P4
+#define RIC_P4 1
+#endif
+constexpr bool kP1 = RIC_P1, kP4 = RIC_P4;
 constexpr int kRefineMax = 6;    // refinement steps of a double-double iteration's direction
 // ... in a continued (rescue hand-over) solve: 2 — over the 22 lpv_lab rounds the continued
 // agents end with the same statuses as with 6 (278 vs 279 at the rounding floor; oracle
@@ -1091,6 +1098,41 @@ __device__ __forceinline__ bool riccati_factor_dd(const MpcConst& c, const Dims&
     sweep(pp, [&](int k, const double* Ak) {
         const double* Bk = Ak + d.sA;
         // PA = P[:, :nx] A_k (na x nx);  PB = P [B_k; I] (na x nu)
+        if constexpr (kP1 && G::NX != 0) {
+            // fixed dimensions: a lane's entries (l, l + 64) with every read issued before the two
+            // chains, which then run interleaved (same sums; clamped entries are computed, not stored)
+            constexpr int NX = G::NX, NU = G::NU, NA = NX + NU, E1 = NA * (NX + NU);
+            constexpr int QN = (E1 + kWave - 1) / kWave;
+            dd v[QN], pr[QN][NX];
+            double cf[QN][NX];
+#pragma unroll
+            for (int q = 0; q < QN; ++q) {
+                int e = l + q * kWave;
+                e = e < E1 ? e : E1 - 1;
+                const bool isA = e < NA * NX;
+                const int e2 = e - NA * NX;
+                const int i = isA ? e / NX : e2 / NU, j = isA ? e - (e / NX) * NX : e2 - (e2 / NU) * NU;
+                const double* cp = isA ? Ak + j : Bk + j;
+                const int cs = isA ? NX : NU;
+                v[q] = isA ? dd_of(0.0) : ld_dd(P, i * NA + NX + j);
+#pragma unroll
+                for (int s2 = 0; s2 < NX; ++s2) {
+                    pr[q][s2] = ld_dd(P, i * NA + s2);
+                    cf[q][s2] = cp[s2 * cs];
+                }
+            }
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int s2 = 0; s2 < NX; ++s2)
+#pragma unroll
+                for (int q = 0; q < QN; ++q) v[q] = dd_fmad(v[q], pr[q][s2], cf[q][s2]);
+#pragma unroll
+            for (int q = 0; q < QN; ++q) {
+                const int e = l + q * kWave;
+                if (e < NA * NX) st_dd(PA, e, v[q]);
+                else if (e < E1) st_dd(PB, e - NA * NX, v[q]);
+            }
+        } else
         for (int e = l; e < na * (nx + nu); e += kWave) {
             if (e < na * nx) {
                 const int i = e / nx, j = e - i * nx;
@@ -1213,6 +1255,40 @@ __device__ __forceinline__ bool riccati_factor_dd(const MpcConst& c, const Dims&
         }
         wsync();
         // P_k = blkdiag(W_k + A'Pxx A, 2dR) + Hvy'K_k
+        if constexpr (kP4 && G::NX != 0) {
+            // fixed dimensions: per entry (l, then l + 64) every read of the A'Pxx A chain issued
+            // before it (same sums; both entries hoisted at once spilled)
+            constexpr int NX = G::NX, NU = G::NU, NA = NX + NU, E4 = NA * NA;
+            constexpr int QN = (E4 + kWave - 1) / kWave;
+#pragma unroll
+            for (int q = 0; q < QN; ++q) {
+                const int e0 = l + q * kWave;
+                const bool st = e0 < E4 && k > 0;
+                const int e = e0 < E4 ? e0 : E4 - 1;
+                const int i = e / NA, j = e - i * NA;
+                const int ic = i < NX ? i : NX - 1, jc = j < NX ? j : 0;
+                const dd v0 = i < NX ? dd_of(Ak[d.sAB + ic * NX + jc])
+                                     : dd_of((j >= NX) ? 2.0 * c.dR[(i - NX) * NU + (j >= NX ? j - NX : 0)] : 0.0);
+                dd pr[NX];
+                double cf[NX];
+#pragma unroll
+                for (int s2 = 0; s2 < NX; ++s2) {
+                    pr[s2] = ld_dd(PA, s2 * NX + jc);
+                    cf[s2] = Ak[s2 * NX + ic];
+                }
+                __builtin_amdgcn_sched_barrier(0);
+                dd t = v0;   // runs on every lane, kept by the rows i < nx only
+#pragma unroll
+                for (int s2 = 0; s2 < NX; ++s2) t = dd_fmad(t, pr[s2], cf[s2]);
+                dd v = i < NX ? t : v0;
+#pragma unroll
+                for (int a = 0; a < NU; ++a) v = dd_fma(v, ld_dd(Hy, a * NA + i), ld_dd(Kk, a * NA + j));
+                if (st && j <= i) {
+                    st_dd(P, i * NA + j, v);
+                    st_dd(P, j * NA + i, v);
+                }
+            }
+        } else
         for (int e = l; e < na * na && k > 0; e += kWave) {
             const int i = e / na, j = e - i * na;
             if (j > i) continue;
@@ -1446,7 +1522,30 @@ __device__ __forceinline__ void kres_dd(const MpcConst& c, const Dims& d, const 
         wsync();
         sweep(pp, [&](int k, const double* Ak) {
             const double* Bk = Ak + d.sA;
-            if (l < nx) {
+            if constexpr (G::NX != 0) {
+                // fixed dimensions: every read of the step issued before its chain (same sums)
+                constexpr int NX = G::NX, NU = G::NU;
+                const int lx = l < NX ? l : NX - 1;
+                dd x[NX];
+                double ar[NX], br[NU], vk[NU];
+#pragma unroll
+                for (int t = 0; t < NX; ++t) {
+                    ar[t] = Ak[lx * NX + t];
+                    x[t] = ld_dd(Xd, k * NX + t);
+                }
+#pragma unroll
+                for (int i = 0; i < NU; ++i) {
+                    br[i] = Bk[lx * NU + i];
+                    vk[i] = v[k * NU + i];
+                }
+                __builtin_amdgcn_sched_barrier(0);
+                dd acc = dd_of(0.0);
+#pragma unroll
+                for (int t = 0; t < NX; ++t) acc = dd_fmad(acc, x[t], ar[t]);
+#pragma unroll
+                for (int i = 0; i < NU; ++i) acc = dd_fmadd(acc, br[i], vk[i]);
+                if (l < NX) st_dd(Xd, (k + 1) * NX + l, acc);
+            } else if (l < nx) {
                 dd acc = dd_of(0.0);
                 for (int t = 0; t < nx; ++t) acc = dd_fmad(acc, ld_dd(Xd, k * nx + t), Ak[l * nx + t]);
                 for (int i = 0; i < nu; ++i) acc = dd_fmadd(acc, Bk[l * nu + i], v[k * nu + i]);
@@ -1469,7 +1568,55 @@ __device__ __forceinline__ void kres_dd(const MpcConst& c, const Dims& d, const 
             const double* Bk = Ak + d.sA;
             const double* pa = psid + ((N - 1 - k) & 1) * 2 * nx;
             double* pb = psid + ((N - k) & 1) * 2 * nx;
-            if (l < nu) {
+            if constexpr (G::NX != 0) {
+                // fixed dimensions, one instruction stream for both lane groups (the branches ran
+                // one after the other): lanes < NU form out_k, lanes 32.. psi_k.  An out lane runs
+                // the psi lanes' W X_k terms on zeros first: dd_fmad({+0, +0}, {0, 0}, w) is
+                // {+0, +0} exactly, so its sums are the generic path's; every read is issued first.
+                constexpr int NX = G::NX, NU = G::NU;
+                const bool po = l < NU;
+                const int t = l >= 32 && l < 32 + NX ? l - 32 : 0, lu = po ? l : 0;
+                const double* cp = po ? Bk + lu : Ak + t;   // psi_{k+1} coefficients: B_k[:, l] | A_k[:, t]
+                const int cs = po ? NU : NX;
+                dd x[NX], ps[NX];
+                double w[NX], cf[NX], v0[NU], vm[NU], vp[NU], r2[NU], d2[NU];
+#pragma unroll
+                for (int u = 0; u < NX; ++u) {
+                    w[u] = Ak[d.sAB + t * NX + u];
+                    x[u] = po ? dd_of(0.0) : ld_dd(Xd, k * NX + u);
+                    ps[u] = ld_dd(pa, u);
+                    cf[u] = cp[u * cs];
+                }
+#pragma unroll
+                for (int j = 0; j < NU; ++j) {
+                    v0[j] = v[k * NU + j];
+                    vm[j] = k ? -v[(k - 1) * NU + j] : 0.0;
+                    vp[j] = k + 1 < N ? v[(k + 1) * NU + j] : 0.0;
+                    r2[j] = 2.0 * c.R[lu * NU + j];
+                    d2[j] = 2.0 * c.dR[lu * NU + j];
+                }
+                const int rr = c.ms + 2 * (k * NU + lu);
+                const double th0 = th[rr], th1 = th[rr + 1], vl = v[k * NU + lu], rl = rhs[k * NU + lu];
+                __builtin_amdgcn_sched_barrier(0);
+                dd acc = dd_of(0.0);
+#pragma unroll
+                for (int u = 0; u < NX; ++u) acc = dd_fmad(acc, x[u], w[u]);
+#pragma unroll
+                for (int s2 = 0; s2 < NX; ++s2) acc = dd_fmad(acc, ps[s2], cf[s2]);
+                if (po) {
+#pragma unroll
+                    for (int j = 0; j < NU; ++j) {
+                        const dd dk = dd_ts(v0[j], vm[j]);
+                        const dd dn = (k + 1 < N) ? dd_ts(vp[j], -v0[j]) : dd_of(0.0);
+                        acc = dd_fmadd(acc, r2[j], v0[j]);
+                        acc = dd_fmad(acc, dd_sub(dk, dn), d2[j]);
+                    }
+                    acc = dd_fmad(acc, dd_ts(th0, th1), vl);
+                    out[k * NU + l] = dd_sub(dd_of(rl), acc).hi;
+                } else if (k > 0 && l >= 32 && l < 32 + NX) {
+                    st_dd(pb, t, acc);
+                }
+            } else if (l < nu) {
                 dd acc = dd_of(0.0);
                 for (int s2 = 0; s2 < nx; ++s2) acc = dd_fmad(acc, ld_dd(pa, s2), Bk[s2 * nu + l]);
                 for (int j = 0; j < nu; ++j) {
