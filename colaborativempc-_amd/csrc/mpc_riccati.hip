@@ -1148,6 +1148,38 @@ __device__ __forceinline__ bool riccati_factor_dd(const MpcConst& c, const Dims&
         }
         wsync();
         // Hvy = [B'PA + PA_u | -2dR] (nu x na);  Hvv = 2R + 2dR + diag(th_u) + B'PB + PB_u (nu x nu)
+        if constexpr (kP1 && G::NX != 0) {
+            // fixed dimensions (nu na + nu nu <= 64: one entry per lane), every read issued before
+            // the chain (same sums; the Hvy columns j >= nx take their -2dR value at the end)
+            constexpr int NX = G::NX, NU = G::NU, NA = NX + NU, EY = NU * NA, E2 = EY + NU * NU;
+            static_assert(E2 <= kWave, "one Hvy / Hvv entry per lane");
+            const int e = l < E2 ? l : E2 - 1;
+            const bool isY = e < EY;
+            const int cc = isY ? e / NA : (e - EY) / NU;
+            const int j = isY ? e - cc * NA : 0, ee = isY ? 0 : (e - EY) - cc * NU;
+            const int jc = j < NX ? j : 0;
+            const double* ob = isY ? PA + 2 * jc : PB + 2 * ee;   // operand column (dd)
+            const int os = isY ? NX : NU;
+            dd v = isY ? (j < NX ? ld_dd(PA, (NX + cc) * NX + jc) : dd_of(0.0))
+                       : dd_add(dd_ts(2.0 * c.R[cc * NU + ee], 2.0 * c.dR[cc * NU + ee]), ld_dd(PB, (NX + cc) * NU + ee));
+            dd pr[NX];
+            double cf[NX];
+#pragma unroll
+            for (int s2 = 0; s2 < NX; ++s2) {
+                pr[s2] = ld_dd(ob, s2 * os);
+                cf[s2] = Bk[s2 * NU + cc];
+            }
+            const int rr = c.ms + 2 * (k * NU + cc);
+            const double th0 = th[rr], th1 = th[rr + 1];
+            const double dry = -2.0 * c.dR[cc * NU + (j >= NX ? j - NX : 0)];
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int s2 = 0; s2 < NX; ++s2) v = dd_fmad(v, pr[s2], cf[s2]);
+            if (!isY && cc == ee) v = dd_add(v, dd_ts(th0, th1));
+            if (isY && j >= NX) v = dd_of(dry);
+            if (l < EY) st_dd(Hy, l, v);
+            else if (l < E2) st_dd(H, l - EY, v);
+        } else
         for (int e = l; e < nu * na + nu * nu; e += kWave) {
             if (e < nu * na) {
                 const int cc = e / na, j = e - cc * na;
