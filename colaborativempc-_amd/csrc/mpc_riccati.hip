@@ -1288,36 +1288,37 @@ __device__ __forceinline__ bool riccati_factor_dd(const MpcConst& c, const Dims&
         wsync();
         // P_k = blkdiag(W_k + A'Pxx A, 2dR) + Hvy'K_k
         if constexpr (kP4 && G::NX != 0) {
-            // fixed dimensions: per entry (l, then l + 64) every read of the A'Pxx A chain issued
-            // before it (same sums; both entries hoisted at once spilled)
+            // fixed dimensions: a lane's two entries (l, l + 64) as two interleaved chains, their
+            // reads left to the compiler's schedule (hoisting both entries' operands spilled); the
+            // A'Pxx A chain runs on every lane and is kept by the rows i < nx only (same sums)
             constexpr int NX = G::NX, NU = G::NU, NA = NX + NU, E4 = NA * NA;
             constexpr int QN = (E4 + kWave - 1) / kWave;
+            int iq[QN], jq[QN], icq[QN], jcq[QN];
+            dd v0[QN], t[QN];
 #pragma unroll
             for (int q = 0; q < QN; ++q) {
-                const int e0 = l + q * kWave;
-                const bool st = e0 < E4 && k > 0;
-                const int e = e0 < E4 ? e0 : E4 - 1;
-                const int i = e / NA, j = e - i * NA;
-                const int ic = i < NX ? i : NX - 1, jc = j < NX ? j : 0;
-                const dd v0 = i < NX ? dd_of(Ak[d.sAB + ic * NX + jc])
-                                     : dd_of((j >= NX) ? 2.0 * c.dR[(i - NX) * NU + (j >= NX ? j - NX : 0)] : 0.0);
-                dd pr[NX];
-                double cf[NX];
+                int e = l + q * kWave;
+                e = e < E4 ? e : E4 - 1;
+                iq[q] = e / NA;
+                jq[q] = e - iq[q] * NA;
+                icq[q] = iq[q] < NX ? iq[q] : NX - 1;
+                jcq[q] = jq[q] < NX ? jq[q] : 0;
+                v0[q] = iq[q] < NX ? dd_of(Ak[d.sAB + icq[q] * NX + jcq[q]])
+                                   : dd_of((jq[q] >= NX) ? 2.0 * c.dR[(iq[q] - NX) * NU + (jq[q] >= NX ? jq[q] - NX : 0)] : 0.0);
+                t[q] = v0[q];
+            }
 #pragma unroll
-                for (int s2 = 0; s2 < NX; ++s2) {
-                    pr[s2] = ld_dd(PA, s2 * NX + jc);
-                    cf[s2] = Ak[s2 * NX + ic];
-                }
-                __builtin_amdgcn_sched_barrier(0);
-                dd t = v0;   // runs on every lane, kept by the rows i < nx only
+            for (int s2 = 0; s2 < NX; ++s2)
 #pragma unroll
-                for (int s2 = 0; s2 < NX; ++s2) t = dd_fmad(t, pr[s2], cf[s2]);
-                dd v = i < NX ? t : v0;
+                for (int q = 0; q < QN; ++q) t[q] = dd_fmad(t[q], ld_dd(PA, s2 * NX + jcq[q]), Ak[s2 * NX + icq[q]]);
 #pragma unroll
-                for (int a = 0; a < NU; ++a) v = dd_fma(v, ld_dd(Hy, a * NA + i), ld_dd(Kk, a * NA + j));
-                if (st && j <= i) {
-                    st_dd(P, i * NA + j, v);
-                    st_dd(P, j * NA + i, v);
+            for (int q = 0; q < QN; ++q) {
+                dd v = iq[q] < NX ? t[q] : v0[q];
+#pragma unroll
+                for (int a = 0; a < NU; ++a) v = dd_fma(v, ld_dd(Hy, a * NA + iq[q]), ld_dd(Kk, a * NA + jq[q]));
+                if (l + q * kWave < E4 && k > 0 && jq[q] <= iq[q]) {
+                    st_dd(P, iq[q] * NA + jq[q], v);
+                    st_dd(P, jq[q] * NA + iq[q], v);
                 }
             }
         } else
