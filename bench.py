@@ -42,15 +42,23 @@ def main():
                     help="cfg5 only: BASELINE cfg5's fp32 path (the Riccati kernel's fp32 mode: an fp32 Riccati "
                          "factorisation, fp64 iterates / residuals, tol 1e-6), checked against the fp64 solve")
     ap.add_argument("--agents", type=int, default=None, help="agents per GPU (default: the config's)")
+    ap.add_argument("--agents-total", type=int, default=None,
+                    help="strong scaling: this many agents in all, split evenly over the ranks (BASELINE cfg4: "
+                         "--agents-total 4096 on 8 GPUs); default: weak scaling, --agents per GPU")
     ap.add_argument("--horizon", type=int, default=None)
     ap.add_argument("--nb", type=int, default=2)
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="target CPU-baseline sample time")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-ref", action="store_true", help="skip the reference-configuration (N=125) line")
+    ap.add_argument("--no-cfg5", action="store_true",
+                    help="skip the cfg5 sub-object of the default line (BASELINE configs[4]: fp64 and fp32 paths)")
     args = ap.parse_args()
     cfg5 = args.config == "cfg5"
     if args.fp32 and not cfg5:
         raise SystemExit("--fp32 is the cfg5 path (use --config cfg5 --fp32)")
+    if args.agents_total is not None and args.agents is not None:
+        raise SystemExit("--agents (per GPU, weak scaling) and --agents-total (strong scaling) exclude each other")
+    strong = args.agents_total is not None
     args.agents = args.agents or (8192 if cfg5 else 1024)
     args.horizon = args.horizon or (50 if cfg5 else 30)
     dim = 3 if cfg5 else 2
@@ -80,6 +88,10 @@ def main():
     from cmpc import scenarios as S
     from cmpc.rounds import DIRounds
 
+    if strong:
+        if args.agents_total % world:
+            raise SystemExit(f"--agents-total {args.agents_total} is not divisible by {world} ranks")
+        args.agents = args.agents_total // world
     n_total = args.agents * world
     scen = S.make_di(n_total, args.horizon, args.nb, dim)
     ctx = cmpc.Context(local)
@@ -141,7 +153,9 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu:
         cpu, max_err = cpu_baseline(R, args.cpu_seconds, rounds=1 if cfg5 else 4, newton=3 if cfg5 else 0,
                                     label=args.config)
-    ref_line = osqp_line = None
+    ref_line = osqp_line = cfg5_sub = None
+    if rank == 0 and world == 1 and not args.no_cfg5 and not cfg5 and not strong:
+        cfg5_sub = cfg5_line(ctx)
     if rank == 0 and world == 1 and not args.no_ref and not cfg5:
         ref_line = reference_config(ctx)
         ref_line["lpv_rounds"] = lpv_rounds(ctx)
@@ -158,7 +172,7 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": elapsed / args.steps * 1e3,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if strong else "weak",
             "vs_baseline": None,
             "dtype": "f32 factorisation / f64 residuals" if args.fp32 else "f64",
             "data": "synthetic (seeded double-integrator agent population, SURVEY.md §8d)",
@@ -171,7 +185,10 @@ def main():
                               if args.fp32 else
                               "fp64 stage-wise Riccati IPM (BASELINE asks fp32; fp64 >= it)") +
                              "; step = build+solve+advance+all-gather") if cfg5 else
-                            (f"cfg3: {args.agents} agents/GPU, N={N}, 2-D double integrator nx={nx} nu={nu}, "
+                            (f"cfg4: {n_total} agents in all ({args.agents} per GPU over {world}), N={N}, 2-D double "
+                             f"integrator nx={nx} nu={nu}, nb={args.nb}, fp64 condensed IPM, strong scaling; step = "
+                             f"build+solve+advance+all-gather" if strong and n_total == 4096 else
+                             f"cfg3: {args.agents} agents/GPU, N={N}, 2-D double integrator nx={nx} nu={nu}, "
                              f"nb={args.nb}, fp64 condensed IPM; step = build+solve+advance+all-gather"),
                 "agents_total": n_total, "horizon": N, "nx": nx, "nu": nu, "neighbours": args.nb,
                 "parallelism": f"agents sharded over {world} GPU(s), "
@@ -186,7 +203,10 @@ def main():
             "roofline": {
                 "kernel": ("mpc_riccati_kernel<Cfg<2,6,3,6,GR,F32>>" if args.fp32 else
                            "mpc_riccati_kernel<Cfg<2,6,3,6,GR>>") if cfg5 else "mpc_ipm3_kernel<4,4,2,2>",
-                "bound": "mfma",
+                # neither MFMA- nor HBM-bound: one wavefront per agent runs dependent chains (sq_profile:
+                # the wave's instruction-issue, wait and MFMA-busy shares of its cycles, from SQ counters)
+                "bound": "latency",
+                "counters": sq_profile(pmc_kind or "cfg3"),
                 "achieved": achieved_tf,
                 "peak": peak,
                 "peak_note": "fp32 vector (the factorisation's precision)" if args.fp32 else "fp64 vector = matrix",
@@ -201,12 +221,96 @@ def main():
                 "hbm_frac": alg_bytes * args.agents / (kern_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
             },
             "cpu_baseline": cpu,
+            "cfg5": cfg5_sub,
             "reference_config": ref_line,
             "osqp_dropin": osqp_line,
         }
         print(json.dumps(out))
     if world > 1:
         dist.destroy_process_group()
+
+
+def cfg5_line(ctx, steps=5, warmup=2):
+    """BASELINE configs[4] inside the default line, so the driver observes it: 8192 agents, N = 50,
+    3-D double integrator (nx 6, nu 3), nb 2 — the fp64 stage-wise Riccati path and the fp32 path
+    (the Riccati kernel's fp32 mode: fp32 factorisation and Newton recursions, fp64 iterates,
+    tol 1e-6), each timed over `steps` device-resident rounds after `warmup` (the same step as the
+    main line: build + solve + advance + exchange), with the fp32 path's tolerance check against the
+    fp64 solve of the same problems (fp32_vs_fp64: every agent's max |z32 - z64| / max(1, |z64|),
+    bar 1e-3) and its roofline (stage-wise Riccati flops at the measured iterations)."""
+    import torch
+
+    from cmpc import scenarios as S
+    from cmpc.rounds import DIRounds
+
+    scen = S.make_di(8192, 50, 2, 3)
+    out = {"workload": "cfg5: 8192 agents/GPU, N=50, 3-D double integrator nx=6 nu=3, nb=2; step = "
+                       "build+solve+advance+exchange", "steps": steps, "warmup": warmup}
+    for fp32 in (False, True):
+        R = DIRounds(scen, ctx=ctx, fp32=fp32)
+        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+        its = torch.empty((steps, R.B), dtype=torch.int32, device=R.dev)
+        kk = torch.empty((steps, R.B), dtype=torch.float64, device=R.dev)
+        st = torch.empty((steps, R.B), dtype=torch.int32, device=R.dev)
+        for _ in range(warmup):
+            R.step()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for k in range(steps):
+            R.bind_outputs(kk[k], its[k], st[k])
+            R.step(timer=ev[k])
+        torch.cuda.synchronize()
+        el = time.perf_counter() - t0
+        kern = sum(a.elapsed_time(b) for a, b in ev) / steps
+        mean_it = float(its.to(torch.float64).mean())
+        flops = S.riccati_flops(6, 3, 50, mean_it)
+        ach = flops * R.B / (kern * 1e-3) / 1e12
+        peak = FP32_PEAK_TFLOPS if fp32 else FP64_PEAK_TFLOPS
+        kind = "cfg5fp32" if fp32 else "cfg5"
+        traffic, src = pmc_traffic(kind)
+        line = {"value": R.B * steps / el, "unit": "agent-QP/s", "ms_per_step": el / steps * 1e3,
+                "mean_ipm_iters": mean_it, "max_kkt": float(kk.max()),
+                "status_counts": {int(a): int(b) for a, b in zip(*np.unique(st.cpu().numpy(), return_counts=True))},
+                "roofline": {"kernel": f"mpc_riccati_kernel<Cfg<2,6,3,6,GR{',F32' if fp32 else ''}>>",
+                             "bound": "latency", "achieved": ach, "peak": peak, "unit": "TFLOP/s", "frac": ach / peak,
+                             "traffic": traffic, "traffic_source": src, "kernel_ms_per_launch": kern,
+                             "alg_flops_per_qp": flops, "counters": sq_profile(kind)}}
+        if fp32:
+            line["fp32_vs_fp64"] = fp32_vs_fp64(R)
+            line["dtype"] = "f32 factorisation / f64 residuals"
+        else:
+            line["dtype"] = "f64"
+        out["fp32" if fp32 else "fp64"] = line
+        del R
+    out["fp32_over_fp64"] = out["fp32"]["value"] / out["fp64"]["value"]
+    return out
+
+
+def sq_profile(kind):
+    """The solver kernel's wave-time shares from the newest committed SQ counter summary
+    (profiles/sq_{kind}_r*.json, tools/pmc_sq.sh + tools/prof_summary.py sq): instruction issue
+    (active_inst_any, of which VALU), s_waitcnt waits (wait_any), dependency / pipe stalls
+    (wait_inst_any) and MFMA busy — the evidence for the `bound` label.  "stale": whether the kernel
+    sources changed since the counters were taken."""
+    import glob
+
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    from prof_summary import solver_sources_sha
+
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"sq_{kind}_r*.json")))
+    if not files:
+        return None
+    try:
+        with open(files[-1]) as f:
+            rec = json.load(f)
+    except (OSError, ValueError):
+        return None
+    sha = rec.get("sources_sha")
+    out = dict(rec.get("fractions_of_wave_time", {}))
+    out.update({"valu_insts_per_wave": rec.get("per_wave", {}).get("valu_insts"),
+                "source": os.path.relpath(files[-1], ROOT), "commit": rec.get("commit"),
+                "stale": None if sha is None else sha != solver_sources_sha()})
+    return out
 
 
 def reference_config(ctx, reps=10, cpu=True):

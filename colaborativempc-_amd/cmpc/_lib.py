@@ -192,6 +192,7 @@ SIGNATURES = {
     "cmpc_comm_id": (ct.c_int, [ct.c_char_p]),
     "cmpc_comm_init": (ct.c_int, [ct.c_void_p, ct.c_int, ct.c_int, ct.c_char_p]),
     "cmpc_allgather_trajectories": (ct.c_int, [ct.c_void_p, _DP, _DP, ct.c_ulonglong, ct.c_void_p]),
+    "cmpc_comm_sum_i32": (ct.c_int, [ct.c_void_p, _IP, ct.c_ulonglong, ct.c_void_p]),
     "cmpc_comm_destroy": (ct.c_int, [ct.c_void_p]),
     "cmpc_lpv_rounds_create": (ct.c_int, [ct.c_void_p, ct.POINTER(cmpc_lpv_params), ct.POINTER(cmpc_track),
                                           ct.POINTER(cmpc_lpv_rounds_dims), ct.POINTER(cmpc_lpv_rounds_init),

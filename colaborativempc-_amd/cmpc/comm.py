@@ -44,6 +44,16 @@ class Comm:
             self.ctx.h, ct.cast(traj_local.data_ptr(), L._DP), ct.cast(traj_all.data_ptr(), L._DP),
             traj_local.numel(), ct.c_void_p(s.cuda_stream)))
 
+    def sum_i32(self, buf, stream=None):
+        """buf (contiguous CUDA int32 tensor) <- its sum over every rank, in place (cmpc_comm_sum_i32)."""
+        import torch
+
+        if not (isinstance(buf, torch.Tensor) and buf.is_cuda and buf.dtype == torch.int32 and buf.is_contiguous()):
+            raise ValueError("buf must be a contiguous CUDA int32 tensor")
+        s = stream if stream is not None else torch.cuda.current_stream(buf.device)
+        self.ctx.check(self.ctx.lib.cmpc_comm_sum_i32(self.ctx.h, ct.cast(buf.data_ptr(), L._IP), buf.numel(),
+                                                      ct.c_void_p(s.cuda_stream)))
+
     def close(self):
         if getattr(self, "ctx", None) is not None:
             self.ctx.lib.cmpc_comm_destroy(self.ctx.h)

@@ -277,6 +277,12 @@ class LPVRounds:
         """x0 <- xPred[1], Last_xPredicted <- xPred[1:], uPred, u_old <- u_0, the exchanged X, Y; an agent
         without a finite solution keeps its state and trajectory; infeasible agents are counted."""
         self.n_infeasible.zero_()
+        if self.last_rows == self.N + 1:
+            # first round: Last_xPredicted goes from N + 1 rows per agent to N dense rows.  An agent the
+            # advance leaves alone (no finite solution) must find its own previous rows in its dense
+            # slot, not bytes of the (N + 1)-row layout: compact the layout first (rows 0..N-1)
+            dense = self.x_last[:, :self.N, :].contiguous()
+            self.x_last.view(-1)[:dense.numel()].copy_(dense.view(-1))
         self.ctx.check(self.ctx.lib.cmpc_lpv_advance_dev(self.ctx.h, ct.byref(self.rdims), _tptr(self.z),
                                                          _tptr(self.x0), _tptr(self.x_last), _tptr(self.u_last),
                                                          _tptr(self.u_old), _tptr(self.traj_local),
@@ -301,13 +307,32 @@ class LPVRounds:
         self.advance()
         self.exchange()
         if halt:
-            bad = self.infeasible()
+            bad = self.infeasible_all()
             if bad:
                 raise InfeasibleRound(bad)
 
     def infeasible(self):
         """Infeasible agents of this rank in the latest round (synchronises)."""
         return int(self.n_infeasible.item())
+
+    def infeasible_all(self):
+        """Infeasible agents of every rank in the latest round (synchronises; collective when
+        sharded).  The reference's loop quits for every agent at once (LPV_HP_N_main.py:102-111):
+        each rank takes the halt decision on the node's count, so no rank breaks out of the loop
+        while the others wait for it in the next round's all-gather."""
+        if self.world == 1:
+            return self.infeasible()
+        if self.comm is not None:   # libcmpc's RCCL communicator (cmpc_comm_sum_i32)
+            cnt = self.n_infeasible.clone()
+            self.comm.sum_i32(cnt, self.torch.cuda.current_stream(self.dev))
+            return int(cnt.item())
+        import torch.distributed as dist
+
+        cnt = self.n_infeasible.clone()
+        if dist.get_backend(self.group) == "gloo":   # gloo reduces host tensors
+            cnt = cnt.cpu()
+        dist.all_reduce(cnt, op=dist.ReduceOp.SUM, group=self.group)
+        return int(cnt.item())
 
 
 class InfeasibleRound(RuntimeError):

@@ -62,8 +62,8 @@ def solve_mpc(p, ctx=None, tol=None, max_iter=None, fp32=False, riccati=False, g
     """Solve a batch of structured agent-QPs on the GPU (host arrays in/out).
     ``fp32``: the fp32 path (BASELINE cfg5): fp32 Riccati factorisation and Newton recursions with
     fp64 iterates — the Riccati kernel's fp32 mode where it is instantiated (nx, nu, mc = 6, 3, 6),
-    with ``lane`` (or where only it is instantiated) the lane-per-agent kernel, else the fp32
-    workgroup-per-agent solver;
+    with ``lane`` (or where only it is instantiated) the lane-per-agent kernel; other dimensions
+    raise CmpcError (CMPC_ERR_UNSUPPORTED);
     ``lane``: the lane-per-agent stage-wise kernel (fp64, or fp32 with ``fp32``);
     ``riccati``: force the stage-wise Riccati solver (the default when N*nu > 64);
     ``generic``: force the runtime-dimension condensed kernel;

@@ -181,6 +181,17 @@ int cmpc_allgather_trajectories(cmpc_ctx* ctx, const double* traj_local, double*
     return CMPC_OK;
 }
 
+int cmpc_comm_sum_i32(cmpc_ctx* ctx, int* buf, unsigned long long count, void* stream) {
+    if (!ctx) return CMPC_ERR_ARG;
+    if (count && !buf) return fail(ctx, CMPC_ERR_ARG, "null buffer");
+    if (!ctx->comm || !count) return CMPC_OK;  // one rank: the local count is the node's
+    int rc = set_device(ctx);
+    if (rc != CMPC_OK) return rc;
+    const ncclResult_t r = ncclAllReduce(buf, buf, (size_t)count, ncclInt32, ncclSum, ctx->comm, (hipStream_t)stream);
+    if (r != ncclSuccess) return fail(ctx, CMPC_ERR_DEVICE, std::string("ncclAllReduce: ") + ncclGetErrorString(r));
+    return CMPC_OK;
+}
+
 int cmpc_comm_destroy(cmpc_ctx* ctx) {
     if (!ctx) return CMPC_ERR_ARG;
     if (ctx->comm) {
@@ -432,7 +443,7 @@ int cmpc_di_solve_dev(cmpc_ctx* ctx, const cmpc_di_params* prm, const cmpc_di_di
     if (dims->batch == 0) return CMPC_OK;
     const int flags = opts ? opts->flags : 0;
     hipStream_t s = (hipStream_t)stream;
-    if (!c.wg && !c.lane && !c.riccati && !c.rescue && !(flags & CMPC_FLAG_GENERIC)) {  // rescue needs materialised rows
+    if (!c.lane && !c.riccati && !c.rescue && !(flags & CMPC_FLAG_GENERIC)) {  // rescue needs materialised rows
         cmpc::MpcPtrs p{in->A, in->B, in->x0, in->u_prev, nullptr, nullptr, nullptr, out->z, out->kkt, out->iters,
                         out->status, opts ? (unsigned long long*)opts->stamps : nullptr, nullptr};
         p.fuse = cmpc::DiFuse{nbr, lane, traj_all, dc, 1};

@@ -22,7 +22,6 @@ struct MpcConst {
     int npad;   // n rounded up to 16 (MFMA tile)
     int ldk;    // leading dimension of the LDS Hessian (odd)
     int max_iter;
-    int wg;       // 0: one-wave kernels; 2: workgroup kernel in fp32 (CMPC_FLAG_FP32)
     int riccati;  // 1: stage-wise Riccati kernel (fp64, N*nu > 64 or CMPC_FLAG_RICCATI)
     int rescue;   // 1: CMPC_FLAG_RESCUE on a condensed solve (Riccati re-solve of broken-down agents)
     int lpv;      // 1: data made by lpv_build.hip with Q diagonal (the v3 kernel's LS layout applies)
@@ -109,9 +108,6 @@ __host__ __device__ inline int stop_status(int stop, double best_m, double tol) 
     return stop == kStopMaxIter ? CMPC_MAX_ITER_REACHED : CMPC_UNSOLVED;
 }
 
-// Long-horizon workgroup-per-agent kernel (mpc_ipm_wg.hip), fp32 or fp64, N*nu <= 256.
-size_t mpc_wg_lds_bytes(const MpcConst& c, bool fp32);
-hipError_t mpc_wg_launch(const MpcConst& c, const MpcPtrs& p, int batch, hipStream_t s, bool fp32);
 constexpr size_t kMaxLdsBytes = 160 * 1024;
 
 // Rescue hand-over (CMPC_FLAG_RESCUE).  A condensed kernel whose factorisation breaks down leaves

@@ -180,7 +180,8 @@ __host__ __device__ inline void lane_agent(const MpcConst& c, const MpcPtrs& P, 
     double* ws = P.ws;
     const int j = b % kLaneAP;  // lane within the wavefront's agents
 #if defined(__HIP_DEVICE_COMPILE__)
-    // one buffer resource over the launch's scratch (mpc_lane_launch keeps it below 2 GiB)
+    // one buffer resource over the launch's scratch (mpc_lane_launch splits batches whose scratch
+    // would reach 2 GiB into sub-launches, so the 32-bit offsets never wrap)
     const __amdgpu_buffer_rsrc_t rs =
         __builtin_amdgcn_make_buffer_rsrc(ws, 0, (int)(L.total * S * 8 < 0x7fffffffull ? L.total * S * 8 : 0x7fffffffull),
                                           0x00020000);

@@ -693,10 +693,6 @@ int mpc_prepare(const cmpc_mpc_dims* d, const cmpc_mpc_weights* wt, const cmpc_o
         *msg = "CMPC_FLAG_LANE: no lane-per-agent kernel for these dimensions (nx,nu,mc,ns = 6,3,6,3 or 4,2,6,3)";
         return CMPC_ERR_UNSUPPORTED;
     }
-    if (fp32 && !lane_ok && d->N * d->nu > CMPC_MAX_NCOND_WG) {
-        *msg = "N*nu > 256: exceeds the fp32 workgroup-per-agent solver";
-        return CMPC_ERR_UNSUPPORTED;
-    }
     c->nx = d->nx;
     c->nu = d->nu;
     c->N = d->N;
@@ -711,10 +707,16 @@ int mpc_prepare(const cmpc_mpc_dims* d, const cmpc_mpc_weights* wt, const cmpc_o
     c->tol = (o && o->tol > 0) ? o->tol : 1e-9;
     c->max_iter = (o && o->max_iter > 0) ? o->max_iter : 60;
     // fp32: the stage-wise Riccati kernel's fp32 mode where it is instantiated (BASELINE cfg5), unless
-    // CMPC_FLAG_LANE asks for the lane-per-agent kernel; else the lane kernel; else the workgroup kernel
+    // CMPC_FLAG_LANE asks for the lane-per-agent kernel; else the lane kernel where it is instantiated;
+    // other dimensions have no fp32 path (the round-1 workgroup-per-agent fp32 solver, which missed
+    // the 1e-3 bar, is retired)
     c->f32 = (fp32 && !lane_req && mpc_riccati_f32_supported(*c)) ? 1 : 0;
     c->lane = (fp32 && lane_ok && !c->f32) ? 2 : (lane_req ? 1 : 0);
-    c->wg = (fp32 && !c->lane && !c->f32) ? 2 : 0;
+    if (fp32 && !c->f32 && !c->lane) {
+        *msg = "CMPC_FLAG_FP32: no fp32 path for these dimensions (nx,nu,mc = 6,3,6 on the Riccati kernel; "
+               "nx,nu,mc,ns = 6,3,6,3 or 4,2,6,3 on the lane kernel)";
+        return CMPC_ERR_UNSUPPORTED;
+    }
     c->riccati = (c->f32 || (!fp32 && !c->lane && (c->n > CMPC_MAX_NCOND || (o && (o->flags & CMPC_FLAG_RICCATI)))))
                      ? 1 : 0;
     double qs = 1.0;
@@ -732,10 +734,6 @@ int mpc_prepare(const cmpc_mpc_dims* d, const cmpc_mpc_weights* wt, const cmpc_o
         qs = fmax(qs, 2.0 * wt->Qs[j]);
     }
     c->qs_max = qs;
-    if (c->wg && mpc_wg_lds_bytes(*c, true) > kMaxLdsBytes) {
-        *msg = "problem does not fit the fp32 workgroup solver's 160 KB of LDS";
-        return CMPC_ERR_UNSUPPORTED;
-    }
     if (c->riccati && mpc_riccati_lds_bytes(*c) > kMaxLdsBytes) {
         *msg = "the per-agent rows of this horizon do not fit the Riccati solver's 160 KB of LDS";
         return CMPC_ERR_UNSUPPORTED;
@@ -775,7 +773,6 @@ hipError_t mpc_launch(const MpcConst& c_in, const MpcPtrs& p, int batch, hipStre
     MpcConst c = c_in;
     c.ws_stride = p.ws ? mpc_ws_doubles(c) : 0;
     if (c.lane) return mpc_lane_launch(c, p, batch, s);
-    if (c.wg) return mpc_wg_launch(c, p, batch, s, c.wg == 2);
     if (c.riccati) return mpc_riccati_launch(c, p, batch, s);
     hipError_t e;
     if (flags & CMPC_FLAG_GENERIC || !mpc3_try_launch(c, p, batch, s, &e)) {

@@ -101,6 +101,38 @@ hipError_t mpc_lane_launch(const MpcConst& c, const MpcPtrs& p, int batch, hipSt
     if (batch == 0) return hipSuccess;
     if (!p.ws) return hipErrorInvalidValue;
     const LaneLayout L = lane_layout(c);
+    // The kernel addresses the launch's scratch through one buffer resource with 32-bit offsets
+    // (lane_body.h): a batch whose scratch reaches 2 GiB (cfg5 N = 50: ~19.7k agents; N = 125: ~8k)
+    // runs as consecutive sub-launches, each with its own agents' pointers and the scratch reused
+    // from its base (an agent's results depend on its own data only).  The launch order indexes the
+    // whole batch, so the sub-launches run in agent order.
+    const size_t per = L.total * sizeof(double);
+    if (per * (size_t)batch >= 0x7fffffffull) {
+        const int chunk = (int)((0x7fffffffull / per) / kLaneAP * kLaneAP);
+        if (chunk < kLaneAP) return hipErrorInvalidValue;
+        const int N = c.N, nx = c.nx, nu = c.nu, mc = c.mc;
+        const size_t nz = (size_t)(nx + c.ns) * (N + 1) + 2 * (size_t)c.n;
+        for (int b0 = 0; b0 < batch; b0 += chunk) {
+            const size_t o = (size_t)b0;
+            MpcPtrs q = p;
+            q.A = p.A + o * N * nx * nx;
+            q.B = p.B + o * N * nx * nu;
+            q.x0 = p.x0 + o * nx;
+            q.up = p.up + o * nu;
+            q.p = p.p + o * (N + 1) * nx;
+            q.C = p.C + o * N * mc * nx;
+            q.h = p.h + o * N * mc;
+            q.z = p.z + o * nz;
+            if (p.kkt) q.kkt = p.kkt + o;
+            if (p.iters) q.iters = p.iters + o;
+            if (p.status) q.status = p.status + o;
+            q.stamps = nullptr;
+            q.order = nullptr;
+            hipError_t e = mpc_lane_launch(c, q, batch - b0 < chunk ? batch - b0 : chunk, s);
+            if (e != hipSuccess) return e;
+        }
+        return hipSuccess;
+    }
     const size_t S = (size_t)batch;
     const int N = c.N, nx = c.nx, nu = c.nu, mc = c.mc;
     hipError_t e;

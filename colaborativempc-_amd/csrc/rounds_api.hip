@@ -20,7 +20,7 @@ struct cmpc_lpv_rounds {
     char* mem = nullptr;
     double *x0 = nullptr, *x_last = nullptr, *u_last = nullptr, *u_old = nullptr, *traj_all = nullptr,
            *traj_local = nullptr, *pose = nullptr, *x_agents = nullptr, *z = nullptr, *planes = nullptr,
-           *kkt = nullptr;
+           *kkt = nullptr, *x_dense = nullptr;
     int *nbr = nullptr, *iters = nullptr, *status = nullptr, *infeasible = nullptr;
 };
 
@@ -75,7 +75,7 @@ int cmpc_lpv_rounds_create(cmpc_ctx* ctx, const cmpc_lpv_params* prm, const cmpc
 
     const size_t B = d.batch, N = d.N, nb = d.nb, T = d.n_total, row = (N + 1) * 2;
     const size_t cnt[] = {B * 9, B * (N + 1) * 9, B * N * 2, B * 2, T * row, B * row, B * row,
-                          B * row * (nb ? nb : 1), B * nz_lpv(d.N), B * N * 3 * (nb ? nb : 1), B};
+                          B * row * (nb ? nb : 1), B * nz_lpv(d.N), B * N * 3 * (nb ? nb : 1), B, B * N * 9};
     size_t bytes = 0;
     for (size_t c : cnt) bytes += ((8 * c + 255) & ~size_t(255));
     bytes += 4 * ((B * (nb ? nb : 1) + 63) & ~size_t(63)) + 3 * 4 * ((B + 63) & ~size_t(63)) + 256;
@@ -90,8 +90,8 @@ int cmpc_lpv_rounds_create(cmpc_ctx* ctx, const cmpc_lpv_params* prm, const cmpc
         return p;
     };
     double** dp[] = {&h->x0, &h->x_last, &h->u_last, &h->u_old, &h->traj_all, &h->traj_local, &h->pose,
-                     &h->x_agents, &h->z, &h->planes, &h->kkt};
-    for (int i = 0; i < 11; ++i) *dp[i] = reinterpret_cast<double*>(take(8 * cnt[i]));
+                     &h->x_agents, &h->z, &h->planes, &h->kkt, &h->x_dense};
+    for (int i = 0; i < 12; ++i) *dp[i] = reinterpret_cast<double*>(take(8 * cnt[i]));
     h->nbr = reinterpret_cast<int*>(take(4 * B * (nb ? nb : 1)));
     h->iters = reinterpret_cast<int*>(take(4 * B));
     h->status = reinterpret_cast<int*>(take(4 * B));
@@ -144,6 +144,15 @@ int cmpc_lpv_rounds_step(cmpc_lpv_rounds* h, int rounds, int* rounds_done, int* 
         const cmpc_lpv_out dout{h->z, nb ? h->planes : nullptr, h->kkt, h->iters, h->status};
         if ((rc = cmpc_solve_lpv_batch_dev(ctx, &h->prm, &h->track, &ld, &din, &dout, &h->opts, s)) != CMPC_OK) return rc;
         HIP_TRY(hipMemsetAsync(h->infeasible, 0, sizeof(int), s));
+        if (h->last_rows == h->d.N + 1) {
+            // first round: Last_xPredicted goes from N + 1 rows per agent to N dense ones.  The advance
+            // rewrites each agent's dense slot from its solution, but an agent it does not advance
+            // (no finite solution) must find its own previous rows there, not bytes of the
+            // (N + 1)-row layout: compact the layout first (rows 0..N-1 of each agent)
+            const size_t w = 8 * (size_t)h->d.N * 9;
+            HIP_TRY(hipMemcpy2DAsync(h->x_dense, w, h->x_last, w + 72, w, h->d.batch, hipMemcpyDeviceToDevice, s));
+            HIP_TRY(hipMemcpyAsync(h->x_last, h->x_dense, w * h->d.batch, hipMemcpyDeviceToDevice, s));
+        }
         if ((rc = cmpc_lpv_advance_dev(ctx, &rd, h->z, h->x0, h->x_last, h->u_last, h->u_old, h->traj_local, h->status,
                                        h->infeasible, s)) != CMPC_OK)
             return rc;
@@ -155,6 +164,11 @@ int cmpc_lpv_rounds_step(cmpc_lpv_rounds* h, int rounds, int* rounds_done, int* 
             if ((rc = cmpc_allgather_trajectories(ctx, h->traj_local, h->traj_all, row * h->d.batch, s)) != CMPC_OK)
                 return rc;
         }
+        // the node's infeasible count, not this rank's: the reference's loop quits for every agent
+        // at once (LPV_HP_N_main.py:102-111), so every rank must take the same halt decision (a
+        // rank that broke alone would leave the others waiting in the next round's all-gather).
+        // The host exchange runs one round per step: its caller combines the counts it returns.
+        if (sharded && !host_x && (rc = cmpc_comm_sum_i32(ctx, h->infeasible, 1, s)) != CMPC_OK) return rc;
         ++done;
         if (halt || r + 1 == rounds) {  // the reference stops the experiment at an infeasible agent
             HIP_TRY(hipMemcpyAsync(&bad, h->infeasible, sizeof(int), hipMemcpyDeviceToHost, s));

@@ -66,7 +66,6 @@ extern "C" {
 #define CMPC_MAX_NCOND 64      /* condensed one-wavefront-per-agent solvers (fp64); beyond it the
                                   stage-wise Riccati solver runs any horizon whose rows fit LDS
                                   (N = 125, nb <= 4 at nx = 9) */
-#define CMPC_MAX_NCOND_WG 256  /* fp32 workgroup-per-agent solver (CMPC_FLAG_FP32) */
 
 typedef struct cmpc_ctx cmpc_ctx;
 
@@ -75,8 +74,8 @@ typedef struct cmpc_ctx cmpc_ctx;
                                 fp32 with fp64 iterates / residuals and a per-agent fp64 finish (opts.tol
                                 ~1e-6) — on the stage-wise Riccati kernel where it has an fp32 instantiation
                                 (nx,nu,mc = 6,3,6), on the lane-per-agent kernel with CMPC_FLAG_LANE or where
-                                only that one is instantiated (nx,nu,mc,ns = 6,3,6,3 or 4,2,6,3); elsewhere the
-                                fp32 workgroup-per-agent condensed solver (N*nu <= 256, opts.tol ~1e-5) */
+                                only that one is instantiated (nx,nu,mc,ns = 6,3,6,3 or 4,2,6,3); other
+                                dimensions: CMPC_ERR_UNSUPPORTED */
 #define CMPC_FLAG_RICCATI 16 /* force the stage-wise Riccati solver (fp64; the default when N*nu > 64) */
 #define CMPC_FLAG_RESCUE 32 /* condensed solves (fp64): an agent whose factorisation breaks down short of
                                1e3 tol (status CMPC_UNSOLVED) continues from its last iterate on the
@@ -103,7 +102,11 @@ typedef struct {
                          (cmpc.rounds.DIRounds(lpt=True)).  The lane-per-agent solver (CMPC_FLAG_FP32 /
                          LANE) packs its wavefronts in this order, so each holds agents of similar
                          iteration counts.  Honoured by cmpc_solve_mpc_batch_dev; NULL:
-                         identity.  Entries are clamped into range; a non-permutation leaves agents unsolved. */
+                         identity.  Entries are clamped into range.  A non-permutation is undefined
+                         behaviour: a missing agent is left unsolved, and a duplicated one is solved by
+                         two workgroups (lanes) at once into the same scratch and outputs (a data race).
+                         The library does not check it (the device array is read by the kernels only);
+                         cmpc.rounds.DIRounds builds it by argsort, always a permutation. */
 } cmpc_opts;
 
 int cmpc_abi_version(void);
@@ -319,7 +322,10 @@ int cmpc_lpv_advance_dev(cmpc_ctx* ctx, const cmpc_di_dims* dims, const double* 
  * Failure semantics (LPV_Planner.py:243-249, LPV_HP_N_main.py:102-111): an agent is
  * infeasible when its status is not in {1, 2, -2}; the reference quits the experiment there.
  * cmpc_lpv_rounds_step counts infeasible agents per round on the device and stops after the
- * first round that has any (rounds_done < rounds); an agent whose solution is not finite
+ * first round that has any (rounds_done < rounds).  Sharded over RCCL, the count is the
+ * node's (cmpc_comm_sum_i32 over the ranks), so every rank stops in the same round; with
+ * CMPC_ROUNDS_HOST_EXCHANGE (one round per step) *infeasible is this rank's count and the
+ * host combines them as it exchanges positions.  An agent whose solution is not finite
  * (track lookup failed, the reference raises) keeps its previous state and trajectory, so no
  * NaN reaches a neighbour.
  * ---------------------------------------------------------------------- */
@@ -447,6 +453,12 @@ int cmpc_ocd_converged_dev(cmpc_ctx* ctx, int batch, int per, double atol, doubl
  *                   rank's traj_local (count doubles, DEVICE) in rank order; stream-ordered
  *                   (hip_stream as void*, 0 = default).  For the position exchange of a
  *                   round, count = local agents * (N+1) * 2.
+ *   cmpc_comm_sum_i32: buf (count int32, DEVICE) <- its sum over every rank of the
+ *                   communicator, in place, stream-ordered (one RCCL all-reduce).  The
+ *                   rounds use it for the halt decision: the reference's loop stops for
+ *                   every agent at once when one is infeasible (LPV_HP_N_main.py:102-111),
+ *                   so every rank must see the node's infeasible count, not its own.
+ *                   Without a communicator (one rank) it leaves buf unchanged.
  *   cmpc_comm_destroy: leaves the communicator (cmpc_destroy does it too).
  * ---------------------------------------------------------------------- */
 #define CMPC_COMM_ID_BYTES 128
@@ -454,6 +466,7 @@ int cmpc_comm_id(unsigned char id[CMPC_COMM_ID_BYTES]);
 int cmpc_comm_init(cmpc_ctx* ctx, int nranks, int rank, const unsigned char id[CMPC_COMM_ID_BYTES]);
 int cmpc_allgather_trajectories(cmpc_ctx* ctx, const double* traj_local, double* traj_all, unsigned long long count,
                                 void* hip_stream);
+int cmpc_comm_sum_i32(cmpc_ctx* ctx, int* buf, unsigned long long count, void* hip_stream);
 int cmpc_comm_destroy(cmpc_ctx* ctx);
 
 /* Device self-test of the f64 MFMA fragment mapping used by the solver

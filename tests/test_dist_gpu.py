@@ -87,6 +87,27 @@ def test_two_rank_lpv_rounds_match_single_process(tmp_path, gpu_ctx):
         assert np.array_equal(d["zs"], zs[:, r * half:(r + 1) * half]), f"rank {r}: solutions differ"
 
 
+def test_two_rank_lpv_rounds_halt_together(tmp_path, gpu_ctx):
+    """An infeasible agent on rank 0 only: the reference quits the whole loop in that round
+    (LPV_HP_N_main.py:102-111), so BOTH ranks must raise InfeasibleRound in round 0 with the
+    node's count (1) — a rank halting alone would leave the other waiting in the next round's
+    all-gather (the processes would hang until the timeout)."""
+    port = _free_port()
+    procs = []
+    for r in range(2):
+        env = dict(os.environ, RANK=str(r), WORLD_SIZE="2", LOCAL_RANK="0", MASTER_ADDR="127.0.0.1",
+                   MASTER_PORT=str(port), CMPC_DIST_BACKEND="gloo")
+        procs.append(subprocess.Popen([sys.executable, os.path.join(ROOT, "tools", "dist_rounds.py"), "lpv_halt",
+                                       str(tmp_path / f"halt{r}.npz"), "4", "3"], env=env,
+                                      stdout=subprocess.PIPE, stderr=subprocess.STDOUT))
+    for p in procs:
+        out, _ = p.communicate(timeout=240)
+        assert p.returncode == 0, out.decode()[-3000:]
+    for r in range(2):
+        d = np.load(tmp_path / f"halt{r}.npz")
+        assert bool(d["raised"]) and int(d["count"]) == 1 and int(d["done"]) == 0, (r, dict(d))
+
+
 def test_c_abi_rccl_allgather_single_rank(gpu_ctx):
     """cmpc_comm_init / cmpc_allgather_trajectories (the C-ABI exchange a MATLAB / C host uses
     instead of torch.distributed), one rank: the gather is the identity, and rounds driven
@@ -105,6 +126,10 @@ def test_c_abi_rccl_allgather_single_rank(gpu_ctx):
         comm.allgather(loc, out)
         torch.cuda.synchronize()
         assert torch.equal(out, loc)
+        cnt = torch.tensor([3, 0], dtype=torch.int32, device="cuda")
+        comm.sum_i32(cnt)   # one rank: the sum over ranks is the rank's own
+        torch.cuda.synchronize()
+        assert cnt.tolist() == [3, 0]
         with pytest.raises(ValueError):
             comm.allgather(loc, torch.zeros(65, 31, 2, dtype=torch.float64, device="cuda"))
         sc = S.make_di(256, 30, 2, 2)
@@ -139,3 +164,23 @@ def test_bench_two_ranks_on_one_device_emit_one_line():
     assert out["n_gpus"] == 2 and out["config"]["agents_total"] == 2048 and out["steps"] == 5
     assert out["value"] > 0 and out["unsolved"] == 0 and out["max_kkt"] < 1e-6
     assert "gloo" in out["config"]["parallelism"]
+
+
+def test_bench_two_ranks_strong_scaling_cfg4():
+    """bench.py --agents-total (strong scaling, BASELINE cfg4's 4096 agents split over the ranks):
+    two ranks of 2048 on device 0 (exchange over gloo), one JSON line for the whole population,
+    "scaling": "strong", the workload named cfg4."""
+    import json
+
+    env = dict(os.environ, CMPC_DIST_BACKEND="gloo", CMPC_DEVICE="0")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.join(ROOT, "bench.py"),
+           "--gpus", "2", "--agents-total", "4096", "--steps", "3", "--warmup", "1", "--no-cpu", "--no-ref"]
+    p = subprocess.run(cmd, env=env, cwd=ROOT, capture_output=True, text=True, timeout=240)
+    assert p.returncode == 0, (p.stdout[-2000:], p.stderr[-3000:])
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, p.stdout[-2000:]
+    out = json.loads(lines[0])
+    assert out["scaling"] == "strong" and out["config"]["agents_total"] == 4096
+    assert out["config"]["workload"].startswith("cfg4")
+    assert out["value"] > 0 and out["unsolved"] == 0 and out["max_kkt"] < 1e-6

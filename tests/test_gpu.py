@@ -633,6 +633,25 @@ def test_cfg5_fp32_path_small_batches(gpu_ctx, lane):
         np.testing.assert_array_equal(iq, it[sl])
 
 
+def test_lane_kernel_batch_past_2gib_of_scratch(gpu_ctx):
+    """The lane kernel addresses its scratch with 32-bit buffer offsets: a cfg5 batch of 20480
+    agents (~2.2 GB of scratch) runs as sub-launches below 2 GiB each.  64 distinct cfg5 problems
+    tiled 320 times: every copy returns the bits of the 64-agent solve (nothing silently dropped
+    past the 2 GiB mark)."""
+    import cmpc
+
+    P = _cfg5_problem(64, rounds=1)
+    reps = 320
+    z, _, it, st = cmpc.solve_mpc(P, gpu_ctx, fp32=True, lane=True)
+    Q = {k: (np.tile(v, (reps,) + (1,) * (v.ndim - 1)) if isinstance(v, np.ndarray) and v.ndim and v.shape[0] == 64
+             else v) for k, v in P.items()}
+    zq, _, iq, sq = cmpc.solve_mpc(Q, gpu_ctx, fp32=True, lane=True)
+    assert zq.shape[0] == 64 * reps
+    np.testing.assert_array_equal(zq, np.tile(z, (reps, 1)))
+    np.testing.assert_array_equal(iq, np.tile(it, reps))
+    np.testing.assert_array_equal(sq, np.tile(st, reps))
+
+
 def test_lane_kernel_fp64_vs_c_restatement(gpu_ctx):
     """The lane-per-agent kernel in fp64 (CMPC_FLAG_LANE) runs the C restatement's Riccati method
     (oracle newton 1): same statuses, z within 1e-6 wherever both solve (the kernel's fused sweeps
@@ -651,21 +670,23 @@ def test_lane_kernel_fp64_vs_c_restatement(gpu_ctx):
     assert np.abs(z[both] - zc[both]).max() < Z_TOL
 
 
-def test_fp32_flag_off_lane_dims_uses_workgroup_solver(gpu_ctx):
-    """Dimensions the lane kernel is not instantiated for (nb = 3: 7 rows per stage) keep the fp32
-    workgroup-per-agent condensed solver: finite answers near the fp64 optimum (its bar: 5e-3)."""
+def test_fp32_flag_without_fp32_path_is_refused(gpu_ctx):
+    """Dimensions with neither the Riccati kernel's fp32 instantiation (nx, nu, mc = 6, 3, 6) nor the
+    lane kernel's (6, 3, 6, 3 / 4, 2, 6, 3) — here nb = 3, 7 rows per stage — have no fp32 path:
+    CMPC_FLAG_FP32 is refused with CMPC_ERR_UNSUPPORTED (the round-1 fp32 workgroup solver, which
+    missed the 1e-3 bar, is retired), while the same problems solve in fp64."""
     import cmpc
+    from cmpc import _lib as L
     from cmpc import scenarios as S
-    from oracle import cmpc_oracle as CO
     from oracle import synth
 
     sc = S.make_di(16, 20, 3, 2)
     P = synth.structured(sc.shared, sc.params, sc.A, sc.B, sc.x0, sc.u_prev, sc.lane, sc.nbr, sc.traj, np.arange(16))
-    z, kkt, it, st = cmpc.solve_mpc(P, gpu_ctx, fp32=True, tol=1e-5)
-    zc, _, _, _ = CO.solve_batch(P)
-    err = np.abs(z - zc) / np.maximum(1.0, np.abs(zc))
-    print(f"wg fp32: status {np.unique(st, return_counts=True)}, max rel err {err.max():.2e}")
-    assert np.isfinite(z).all() and err.max() < 5e-3
+    with pytest.raises(cmpc.CmpcError) as ei:
+        cmpc.solve_mpc(P, gpu_ctx, fp32=True)
+    assert ei.value.code == L.CMPC_ERR_UNSUPPORTED
+    _, _, _, st = cmpc.solve_mpc(P, gpu_ctx)
+    assert (st == cmpc.CMPC_SOLVED).all()
 
 
 def test_ocd_dual_update_and_convergence_match_reference(gpu_ctx):

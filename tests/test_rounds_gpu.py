@@ -115,9 +115,13 @@ def test_infeasible_agent_halts_the_loop_and_is_not_propagated(gpu_ctx):
     assert ei.value.count == 1
     R = LPVRounds(bp, *args, **kw)
     traj0 = R.traj_all.cpu().numpy().copy()
+    N = R.N
     for _ in range(2):
         R.step(halt=False)
         torch.cuda.synchronize()
+        # the infeasible agent keeps its previous prediction in its dense N-row slot (rows 0..N-1)
+        xl = R.x_last.cpu().numpy().reshape(-1)[: R.B * N * 9].reshape(R.B, N, 9)
+        assert np.array_equal(xl[0], args[1][0, :N], equal_nan=True)
         st = R.status.cpu().numpy()
         assert st[0] == cmpc.CMPC_UNSOLVED and st[1] == cmpc.CMPC_SOLVED
         assert R.infeasible() == 1

@@ -6,7 +6,8 @@ and the backend from the environment (CMPC_DIST_BACKEND, default gloo: on a one-
 rank shares device 0, and RCCL refuses two ranks on one device).
 
 Usage: python tools/dist_rounds.py OUT.npz N_AGENTS HORIZON ROUNDS SAMPLE
-       python tools/dist_rounds.py lpv OUT.npz REPS ROUNDS   (LPVRounds, ring neighbours across ranks)"""
+       python tools/dist_rounds.py lpv OUT.npz REPS ROUNDS   (LPVRounds, ring neighbours across ranks)
+       python tools/dist_rounds.py lpv_halt OUT.npz REPS ROUNDS   (same, one infeasible agent on rank 0)"""
 import os
 import sys
 
@@ -45,11 +46,14 @@ def run(n_agents, horizon, rounds, sample, rank=0, world=1, group=None):
     return np.stack(trajs), prob, z0
 
 
-def run_lpv(reps, rounds, rank=0, world=1, group=None):
+def run_lpv(reps, rounds, rank=0, world=1, group=None, offtrack=False):
     """Device-resident LPV rounds (cmpc.rounds.LPVRounds) of `reps` copies of the reference's
     3-agent N = 30 Highway run (tests/golden/lpv_n30_a3, step 0), ring neighbours (i+1, i+2 mod
     n: the same positions as each copy's own other two agents, but crossing the rank boundary).
-    Returns (traj_all per round, this rank's z per round)."""
+    Returns (traj_all per round, this rank's z per round).  ``offtrack``: agent 0 (rank 0's) gets a
+    previous prediction off the track (NaN s in one row: infeasible, status -10); every rank's
+    LPVRounds.step must then raise InfeasibleRound in the first round with the node's count.
+    Returns (raised, count, rounds completed) instead."""
     import types
 
     import torch
@@ -71,10 +75,22 @@ def run_lpv(reps, rounds, rank=0, world=1, group=None):
     ctx = cmpc.Context(0)
     bp = cmpc.PlannerLPVBatch(Q, 1e7 * np.eye(3), 0.0 * np.eye(2), 50.0 * np.eye(2), N, dt, track, 5.0, model, lim,
                               ctx=ctx)
-    R = LPVRounds(bp, np.tile(d["x0"][sel], (reps, 1)), np.tile(np.stack([d[f"x_last_{j}"] for j in sel]), (reps, 1, 1)),
+    x_last = np.tile(np.stack([d[f"x_last_{j}"] for j in sel]), (reps, 1, 1))
+    if offtrack:
+        x_last[0, 3, 6] = np.nan
+    R = LPVRounds(bp, np.tile(d["x0"][sel], (reps, 1)), x_last,
                   np.tile(np.stack([d[f"u_last_{j}"] for j in sel]), (reps, 1, 1)), nbr,
                   u_old=np.tile(d["u_old"][sel], (reps, 1)), traj=np.tile(d["pose"][sel], (reps, 1, 1)),
                   rank=rank, world=world, group=group)
+    if offtrack:
+        from cmpc.rounds import InfeasibleRound
+
+        for r in range(rounds):
+            try:
+                R.step()
+            except InfeasibleRound as e:
+                return True, e.count, r
+        return False, 0, rounds
     trajs, zs = [], []
     for _ in range(rounds):
         R.step()
@@ -92,6 +108,11 @@ def main():
     torch.cuda.set_device(0)
     dist.init_process_group(os.environ.get("CMPC_DIST_BACKEND", "gloo"), rank=rank, world_size=world)
     try:
+        if sys.argv[1] == "lpv_halt":   # dist_rounds.py lpv_halt OUT.npz REPS ROUNDS
+            out, reps, rounds = sys.argv[2], int(sys.argv[3]), int(sys.argv[4])
+            raised, count, done = run_lpv(reps, rounds, rank, world, offtrack=True)
+            np.savez(out, raised=raised, count=count, done=done)
+            return
         if sys.argv[1] == "lpv":   # dist_rounds.py lpv OUT.npz REPS ROUNDS
             out, reps, rounds = sys.argv[2], int(sys.argv[3]), int(sys.argv[4])
             trajs, zs = run_lpv(reps, rounds, rank, world)

@@ -5,6 +5,7 @@
       launches (dispatches warmup .. warmup+steps-1) is the number bench.py's
       roofline.kernel_ms_per_launch must agree with.
   python tools/prof_summary.py pmc <counter_collection.csv (FETCH pass)> <(WRITE pass)> <out.json> [commit]
+  python tools/prof_summary.py sq <out.json> <commit> <pass1.csv> [pass2.csv ...]   (tools/pmc_sq.sh passes)
   SOLVER=<kernel name substring> selects the solver kernel (default mpc_ipm; cfg5: mpc_riccati,
   the fp32 path: mpc_lane_kernel).
       HBM bytes per launch of the solver kernel from FETCH_SIZE / WRITE_SIZE (kB), with the
@@ -83,8 +84,58 @@ def pmc(fetch_csv, write_csv, out, commit=None):
     print(json.dumps(res))
 
 
+def _pmc_all(path):
+    """{counter: [per-dispatch values of the solver kernel]} of one --pmc pass."""
+    vals = {}
+    for r in _rows(path):
+        if SOLVER not in r.get("Kernel_Name", ""):
+            continue
+        d = int(r.get("Dispatch_Id", r.get("Correlation_Id", 0)))
+        c = vals.setdefault(r["Counter_Name"], {})
+        c[d] = c.get(d, 0.0) + float(r["Counter_Value"])
+    return {k: [v[d] for d in sorted(v)] for k, v in vals.items()}
+
+
+def sq(out, commit, *csvs):
+    """Instruction-mix / wave-state summary of the solver kernel from SQ (and GRBM) counter passes
+    (tools/pmc_sq.sh: one pass per counter group).  Per-launch means over the dispatches after the
+    first; SQ_WAVE_CYCLES / SQ_WAIT_* / SQ_ACTIVE_INST_* count quad-cycles, SQ_VALU_MFMA_BUSY_CYCLES
+    and SQ_BUSY_CYCLES cycles (MI355X_MICROARCH.md, PMC units).  Fractions of the kernel's wave time:
+    active (an instruction issued), waiting (s_waitcnt: LDS / memory latency), issue-stalled
+    (dependency / pipe hazards), VALU active, MFMA busy."""
+    per = {}
+    for path in csvs:
+        for k, v in _pmc_all(path).items():
+            per[k] = v
+    mean = {k: (sum(v[1:]) / len(v[1:]) if len(v) > 1 else v[0]) for k, v in per.items() if v}
+    g = mean.get
+    wc = g("SQ_WAVE_CYCLES")
+    res = {"counters_per_launch": mean, "kernel_filter": SOLVER, "commit": commit, "sources_sha": solver_sources_sha()}
+    if wc:
+        res["fractions_of_wave_time"] = {
+            "active_inst_any": g("SQ_ACTIVE_INST_ANY", 0.0) / wc,
+            "active_valu": g("SQ_ACTIVE_INST_VALU", 0.0) / wc,
+            "active_lds": g("SQ_ACTIVE_INST_LDS", 0.0) / wc,
+            "active_salu": g("SQ_ACTIVE_INST_SCA", 0.0) / wc,
+            "wait_any": g("SQ_WAIT_ANY", 0.0) / wc,
+            "wait_inst_any": g("SQ_WAIT_INST_ANY", 0.0) / wc,
+            "mfma_busy": g("SQ_VALU_MFMA_BUSY_CYCLES", 0.0) / (4.0 * wc),
+        }
+        waves = g("SQ_WAVES") or 1.0
+        res["per_wave"] = {"cycles": 4.0 * wc / waves, "valu_insts": g("SQ_INSTS_VALU", 0.0) / waves,
+                           "fma_f64_insts": g("SQ_INSTS_VALU_FMA_F64", 0.0) / waves,
+                           "mfma_insts": g("SQ_INSTS_MFMA", 0.0) / waves, "lds_insts": g("SQ_INSTS_LDS", 0.0) / waves,
+                           "salu_insts": g("SQ_INSTS_SALU", 0.0) / waves}
+        if g("SQ_LDS_IDX_ACTIVE"):
+            res["lds_bank_conflict_frac"] = g("SQ_LDS_BANK_CONFLICT", 0.0) / g("SQ_LDS_IDX_ACTIVE")
+    json.dump(res, open(out, "w"), indent=1)
+    print(json.dumps({k: v for k, v in res.items() if k != "counters_per_launch"}))
+
+
 if __name__ == "__main__":
     if sys.argv[1] == "trace":
         trace(sys.argv[2], int(sys.argv[3]), int(sys.argv[4]), sys.argv[5])
+    elif sys.argv[1] == "sq":   # prof_summary.py sq OUT.json COMMIT pass1.csv pass2.csv ...
+        sq(sys.argv[2], sys.argv[3], *sys.argv[4:])
     else:
         pmc(sys.argv[2], sys.argv[3], sys.argv[4], sys.argv[5] if len(sys.argv) > 5 else None)
