@@ -39,7 +39,7 @@ __host__ __device__ constexpr int slk(int r) { return r == 0 ? -1 : (r == 1 ? 0 
 __host__ __device__ constexpr double sgn(int r) { return r < 4 ? 1.0 : -1.0; }
 
 struct Lds3 {
-    int cst, A, B, C, H, Pq, x0, up, W, Gb, Yb, X, dX, yb, U, dU, rd, gU, vb, thin, bU, Ld, red, stamps, total;
+    int cst, A, B, C, H, Pq, x0, up, W, Gb, Yb, X, dX, yb, U, dU, rd, vb, thin, bU, Ld, red, stamps, Phi, total;
 };
 
 // LS (the reference's own agent, nx 9 / nu 2, built by lpv_build.hip): the model's structure is
@@ -53,6 +53,20 @@ struct Lds3 {
 constexpr int kLsW = 5;  // LS stage weights: w(vx,vx), w(ey,ey), w(X,X), w(X,Y), w(Y,Y)
 template <int NB>
 __host__ __device__ constexpr int ls_cw() { return 4 + 2 * NB; }
+
+// Segmented (parallel-in-time) forward simulation: the horizon's N stages split into four
+// segments [a_q, a_{q+1}), one per row of 16 lanes.  Each row runs its segment's recursion from a
+// zero state (row 0 from x_0); a two-step chain then carries the true state across the segment
+// starts, x_{a_{q+1}} = x^loc_{a_{q+1}} + Phi_{a_{q+1}} x_{a_q}, and one parallel pass adds
+// Phi_k x_{a_q} to every stage of segments 1..3.  Phi_k = A_{k-1} .. A_{a_q}, the transition from
+// the segment start, depends on A only: built once per solve (phi_build).  The serial chain drops
+// from N stage steps to ceil(N / 4) + 2.  For the small-state instantiations (NX <= 4: the LDS image
+// has room for Phi) with T >= 2 tiles and NU <= 2, i.e. N > 8: every segment is non-empty.
+__host__ __device__ constexpr int seg_a(int q, int N) { return (q * N + 3) / 4; }
+template <int T, int NX, int NU, bool LS>
+__host__ __device__ constexpr bool seg_on() {
+    return !LS && NX <= 4 && NU <= 2 && T >= 2;
+}
 
 template <int T, int NX, int NU, int NB, bool LS = false>
 __host__ __device__ inline Lds3 lds3_layout(int N) {
@@ -86,13 +100,15 @@ __host__ __device__ inline Lds3 lds3_layout(int N) {
     L.U = take(NP);
     L.dU = take(NP);
     L.rd = take(NP);
-    L.gU = take(NP);
     L.vb = take(NP);
     L.thin = take(NP);
     L.bU = take(NP);
     L.Ld = take(T * 16 * 17);
     L.red = take(16);
     L.stamps = take(kStampSlots);
+    // segmented forward simulation (kSeg): the transitions Phi_k of stages (a_1, N] (fwd3seg); 352
+    // doubles at N = 30, NX = 4
+    L.Phi = take(seg_on<T, NX, NU, LS>() ? (N - seg_a(1, N)) * NX * NX : 0);
     L.total = o;
     return L;
 }
@@ -164,6 +180,133 @@ __device__ __forceinline__ void fwd3(int l, int N, const double* A, const double
     }
     if (k < N) step(k, a0, b0);
     if (k + 1 < N) step(k + 1, a1, b1);
+}
+
+// Phi_k for k in (a_1, N] (see seg_a): rows 1..3 build their segment's transitions in parallel, lane
+// s of the row holding row s of Phi (Phi_{a_q} = I, Phi_{k+1} = A_k Phi_k); stored at slot k - a_1 - 1.
+template <int NX>
+__device__ __forceinline__ void phi_build(int l, int N, const double* A, double* Phi) {
+    const int q = l >> 4, s = (l & 15) < NX ? (l & 15) : 0;
+    const int a1 = seg_a(1, N), a = seg_a(q, N), e = seg_a(q + 1, N);
+    double ph[NX];
+#pragma unroll
+    for (int t = 0; t < NX; ++t) ph[t] = (s == t) ? 1.0 : 0.0;
+    for (int i = 0; i < a1; ++i) {  // a_1 = the longest segment
+        const int k = a + i;
+        const bool valid = q >= 1 && k < e;
+        const int kc = valid ? k : a1;
+        double ar[NX], nw[NX];
+#pragma unroll
+        for (int t = 0; t < NX; ++t) ar[t] = A[(kc * NX + s) * NX + t];
+        static_for<0, NX>([&](auto c_c) __attribute__((always_inline)) {
+            constexpr int cc = decltype(c_c)::value;
+            double v = 0.0;
+            static_for<0, NX>([&](auto t_c) __attribute__((always_inline)) {
+                constexpr int tt = decltype(t_c)::value;
+                v = fma(ar[tt], bcast16<tt>(ph[cc]), v);
+            });
+            nw[cc] = v;
+        });
+#pragma unroll
+        for (int c = 0; c < NX; ++c) ph[c] = valid ? nw[c] : ph[c];
+        if (valid && (l & 15) < NX) {
+#pragma unroll
+            for (int c = 0; c < NX; ++c) Phi[((k - a1) * NX + s) * NX + c] = ph[c];
+        }
+    }
+}
+
+// x += Phi x_a (the correction of a stage state, and the segment-start chain: same operation order)
+template <int NX>
+__device__ __forceinline__ double phi_apply(const double* phr, const double* xa, double v) {
+#pragma unroll
+    for (int t = 0; t < NX; ++t) v = fma(phr[t], xa[t], v);
+    return v;
+}
+
+// fwd3 (x_0 = x0 or 0, x_{k+1} = A_k x_k + B_k u_k) by segments (seg_a, phi_build); X, U, A, B as fwd3.
+template <int NX, int NU>
+__device__ __forceinline__ void fwd3seg(int l, int N, const double* A, const double* B, const double* x0,
+                                        const double* U, double* X, const double* Phi) {
+    static_assert(NX <= 16, "row broadcast");
+    const int q = l >> 4, s = (l & 15) < NX ? (l & 15) : 0;
+    const int a1 = seg_a(1, N), a = seg_a(q, N), e = seg_a(q + 1, N);
+    // each row its segment, from x^loc_{a_q} = 0 (row 0: x_0); B_k u_k is formed beside the chain. A
+    // finished row repeats its last stage without changing its state (clamped fetch, select, equal store)
+    double xr = (q == 0 && x0) ? x0[s] : 0.0;
+    if (q == 0) X[s] = xr;
+    auto fetch = [&](int i, double* av) __attribute__((always_inline)) {
+        const int k = a + i < e ? a + i : e - 1;
+#pragma unroll
+        for (int t = 0; t < NX; ++t) av[t] = A[(k * NX + s) * NX + t];
+#pragma unroll
+        for (int j = 0; j < NU; ++j) {
+            av[NX + j] = B[(k * NX + s) * NU + j];
+            av[NX + NU + j] = U[k * NU + j];
+        }
+    };
+    auto step = [&](int i, const double* av) __attribute__((always_inline)) {
+        const int k = a + i < e ? a + i : e - 1;
+        double v0 = 0.0, v1 = 0.0;
+#pragma unroll
+        for (int j = 0; j < NU; ++j) v0 = fma(av[NX + j], av[NX + NU + j], v0);
+        static_for<0, NX>([&](auto t) __attribute__((always_inline)) {
+            constexpr int tt = decltype(t)::value;
+            if constexpr (tt & 1) v1 = fma(av[tt], bcast16<tt>(xr), v1);
+            else v0 = fma(av[tt], bcast16<tt>(xr), v0);
+        });
+        xr = (a + i < e) ? v0 + v1 : xr;
+        X[(k + 1) * NX + s] = xr;
+    };
+    // two register sets, one stage ahead (the rows' chains are ceil(N / 4) steps long)
+    double p0[NX + 2 * NU], p1[NX + 2 * NU];
+    fetch(0, p0);
+    int i = 0;
+    for (; i + 1 < a1; i += 2) {
+        fetch(i + 1, p1);
+        __builtin_amdgcn_sched_barrier(0);
+        step(i, p0);
+        fetch(i + 2, p0);
+        __builtin_amdgcn_sched_barrier(0);
+        step(i + 1, p1);
+    }
+    if (i < a1) step(i, p0);
+    wsync();
+    // segment starts: x_{a_1} is exact (segment 0 began at x_0); x_{a_{q+1}} = x^loc + Phi x_{a_q}
+    // (every row runs the chain; row q keeps x_{a_q} for its own stages)
+    double xq[NX];
+    {
+        double xa[NX], ph[NX];
+        double v = X[a1 * NX + s];
+#pragma unroll
+        for (int qq = 2; qq < 5; ++qq) {
+            static_for<0, NX>([&](auto t) __attribute__((always_inline)) {
+                constexpr int tt = decltype(t)::value;
+                xa[tt] = bcast16<tt>(v);
+            });
+#pragma unroll
+            for (int t = 0; t < NX; ++t) xq[t] = (q == qq - 1) ? xa[t] : xq[t];
+            if (qq == 4) break;
+            const int aq = seg_a(qq, N);
+#pragma unroll
+            for (int t = 0; t < NX; ++t) ph[t] = Phi[((aq - a1 - 1) * NX + s) * NX + t];
+            v = phi_apply<NX>(ph, xa, X[aq * NX + s]);
+        }
+    }
+    // row q >= 1 corrects its segment's stages (a_q, a_{q+1}]: x_k = x^loc_k + Phi_k x_{a_q}; at most
+    // 2 x 16 entries per row (segments of <= 8 stages, NX <= 4)
+    if (q >= 1) {
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const int j = (l & 15) + 16 * h, k = a + 1 + j / NX, r = j % NX;
+            if (k <= e) {
+                double ph[NX];
+#pragma unroll
+                for (int t = 0; t < NX; ++t) ph[t] = Phi[((k - a1 - 1) * NX + r) * NX + t];
+                X[k * NX + r] = phi_apply<NX>(ph, xq, X[k * NX + r]);
+            }
+        }
+    }
 }
 
 // The adjoint's serial part only: psi_N = y_N, psi_k = y_k + A_k' psi_{k+1} for k = N-1 .. 1,
@@ -373,7 +516,18 @@ __global__ __launch_bounds__(64, 1) void mpc_ipm3_kernel(const MpcConst c, const
             if ((lo ? r < MC : r < NI) && isfinite(wv(r))) actm |= 1u << r;
     }
 #define ACT(r) ((actm >> (r)) & 1u)
-    fwd3<NX, NU, LS>(l, N, sA, sB, sx0, U, X);
+    constexpr bool kSeg = seg_on<T, NX, NU, LS>();
+    double* sPhi = sm + L.Phi;
+    // x_{k+1} = A_k x_k + B_k u_k, by segments where the instantiation has them
+    auto fwd = [&](const double* x0v, const double* Uv, double* Xv) __attribute__((always_inline)) {
+        if constexpr (kSeg) fwd3seg<NX, NU>(l, N, sA, sB, x0v, Uv, Xv, sPhi);
+        else fwd3<NX, NU, LS>(l, N, sA, sB, x0v, Uv, Xv);
+    };
+    if constexpr (kSeg) {
+        phi_build<NX>(l, N, sA, sPhi);
+        wsync();
+    }
+    fwd(sx0, U, X);
     wsync();
 
     // value of row r at (Xv, Uv[, sig]) for this lane's rows
@@ -1130,7 +1284,7 @@ __global__ __launch_bounds__(64, 1) void mpc_ipm3_kernel(const MpcConst c, const
             for (int i = l; i < NP; i += 64) dU[i] = (i < n) ? vb[i] : 0.0;
             wsync();
             STAMP(10);
-            fwd3<NX, NU, LS>(l, N, sA, sB, nullptr, dU, dX);
+            fwd(nullptr, dU, dX);
             wsync();
             STAMP(11);
 #pragma unroll
@@ -1224,7 +1378,7 @@ __global__ __launch_bounds__(64, 1) void mpc_ipm3_kernel(const MpcConst c, const
     wsync();
 
     // ---- output in the reference layout ----
-    fwd3<NX, NU, LS>(l, N, sA, sB, sx0, U, X);
+    fwd(sx0, U, X);
     wsync();
     constexpr int NXE = NX + NS;
     const size_t nz = (size_t)NXE * (N + 1) + 2 * (size_t)n;
