@@ -32,7 +32,6 @@ struct MpcConst {
     unsigned long long ws_stride;  // doubles of MpcPtrs::ws per agent (set by mpc_launch; 0: no scratch)
     double tol;
     double qs_max;  // max(1, 2*max(Qs)) — slack residual scale
-    double Q[CMPC_MAX_NX * CMPC_MAX_NX];
     double R[CMPC_MAX_NU * CMPC_MAX_NU];
     double dR[CMPC_MAX_NU * CMPC_MAX_NU];
     double Qs[CMPC_MAX_NS];
@@ -40,7 +39,15 @@ struct MpcConst {
     double u_lb[CMPC_MAX_NU];
     int row_slack[CMPC_MAX_MC];
     int row_sign[CMPC_MAX_MC];
+    // last: a kernel that copies the struct to LDS (mpc_riccati.hip) copies only its first nx * nx
+    // entries (mpc_const_used_doubles), 864 B less at nx = 6
+    double Q[CMPC_MAX_NX * CMPC_MAX_NX];
 };
+
+// doubles of an MpcConst up to the last Q entry an nx x nx problem reads
+__host__ __device__ inline int mpc_const_used_doubles(const MpcConst& c) {
+    return (int)((offsetof(MpcConst, Q) + sizeof(double) * (size_t)c.nx * c.nx + 7) / 8);
+}
 
 struct DiConst {
     int N, nb, nx, nu, ns, dim, self_offset;

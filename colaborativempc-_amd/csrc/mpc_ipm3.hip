@@ -577,7 +577,9 @@ __global__ __launch_bounds__(64, 1) void mpc_ipm3_kernel(const MpcConst c, const
     double best_m = INFINITY, best_kkt = INFINITY, bsg[NS] = {0.0, 0.0, 0.0};
     int best_it = 0, stop = kStopMaxIter, it;
     double kkt = INFINITY;
-    double Dsig[NS] = {1.0, 1.0, 1.0}, rsig[NS] = {0.0, 0.0, 0.0}, dsg[NS] = {0.0, 0.0, 0.0};
+    // iDs: 1 / D_sigma of the stage's slack groups (one division each per iteration; the W build, rho~
+    // and the slack directions multiply by it)
+    double iDs[NS] = {1.0, 1.0, 1.0}, rsig[NS] = {0.0, 0.0, 0.0}, dsg[NS] = {0.0, 0.0, 0.0};
     v4d acc[NT];
     double alpha_prev = 1;  // step of the previous iteration (kShortStep guard)
     for (it = 1; it <= c.max_iter; ++it) {
@@ -713,21 +715,21 @@ __global__ __launch_bounds__(64, 1) void mpc_ipm3_kernel(const MpcConst c, const
 #pragma unroll
             for (int r = 0; r < MC; ++r)
                 if (slk(r) == j) v += th[r];
-            Dsig[j] = v;
+            iDs[j] = 1.0 / v;
         }
         if (own) {
             if (lo) {
                 // W_{k+1} = 2Q + sum_r th'_r c_r c_r' + sum_{pairs in a slack group} phi (a_r - a_r')(a_r - a_r')'
                 double thp[MC];
 #pragma unroll
-                for (int r = 0; r < MC; ++r) thp[r] = slk(r) < 0 ? th[r] : Qs2[slk(r)] * th[r] / Dsig[slk(r)];
+                for (int r = 0; r < MC; ++r) thp[r] = slk(r) < 0 ? th[r] : Qs2[slk(r)] * th[r] * iDs[slk(r)];
                 if constexpr (LS) {
                     // block diagonal (Q diagonal, rows on vx / ey / (X, Y)): the five entries that are
                     // not 2Q's, accumulated in the dense build's order
                     const double* cr = sC + k * CW;
                     double wvx = fma(thp[1] * cr[1], cr[1], fma(thp[0] * cr[0], cr[0], Q2[0]));
                     double wey = fma(thp[3] * cr[3], cr[3], fma(thp[2] * cr[2], cr[2], Q2[3 * NX + 3]));
-                    const double phi23 = th[2] * th[3] / Dsig[1], d23 = cr[2] - cr[3];
+                    const double phi23 = th[2] * th[3] * iDs[1], d23 = cr[2] - cr[3];
                     wey = fma(phi23 * d23, d23, wey);
                     double wxx = Q2[7 * NX + 7], wxy = Q2[7 * NX + 8], wyy = Q2[8 * NX + 8];
 #pragma unroll
@@ -741,7 +743,7 @@ __global__ __launch_bounds__(64, 1) void mpc_ipm3_kernel(const MpcConst c, const
                     for (int q = 0; q < NB; ++q)
 #pragma unroll
                         for (int q2 = q + 1; q2 < NB; ++q2) {  // plane rows share slack 2, sign -1
-                            const double phi = th[4 + q] * th[4 + q2] / Dsig[2];
+                            const double phi = th[4 + q] * th[4 + q2] * iDs[2];
                             const double dx = cr[4 + 2 * q2] - cr[4 + 2 * q], dy = cr[5 + 2 * q2] - cr[5 + 2 * q];
                             wxx = fma(phi * dx, dx, wxx);
                             wxy = fma(phi * dx, dy, wxy);
@@ -788,7 +790,7 @@ __global__ __launch_bounds__(64, 1) void mpc_ipm3_kernel(const MpcConst c, const
 #pragma unroll
                             for (int r2 = r + 1; r2 < MC; ++r2) {
                                 if (slk(r2) != slk(r)) continue;
-                                const double phi = th[r] * th[r2] / Dsig[slk(r)];
+                                const double phi = th[r] * th[r2] * iDs[slk(r)];
                                 const double ds = sgn(r) * Ck_(r * NX + s) - sgn(r2) * Ck_(r2 * NX + s);
                                 const double du = sgn(r) * Ck_(r * NX + u) - sgn(r2) * Ck_(r2 * NX + u);
                                 v = fma(phi * ds, du, v);
@@ -1187,7 +1189,7 @@ __global__ __launch_bounds__(64, 1) void mpc_ipm3_kernel(const MpcConst c, const
                             if (r2 == r || slk(r2) != j) continue;
                             v += th[r2] * rho[r] - th[r] * sgn(r) * sgn(r2) * rho[r2];
                         }
-                        v /= Dsig[j];
+                        v *= iDs[j];
                     }
                     if constexpr (LS) {  // the row's nonzeros (same accumulation order)
                         const double* cr = sC + k * CW;
@@ -1298,7 +1300,7 @@ __global__ __launch_bounds__(64, 1) void mpc_ipm3_kernel(const MpcConst c, const
 #pragma unroll
                 for (int r = 0; r < MC; ++r)
                     if (slk(r) == j) v += sgn(r) * (rho[r] + th[r] * gdu[r]);
-                dsg[j] = (lo && own) ? -v / Dsig[j] : 0.0;
+                dsg[j] = (lo && own) ? -v * iDs[j] : 0.0;
             }
             // dt_r = -rp - G dU - s dsig ;  dl_r = rho + th (G dU + s dsig)
             auto sdr = [&](int r) -> double { return (lo && slk(r) >= 0) ? sgn(r) * dsg[slk(r)] : 0.0; };

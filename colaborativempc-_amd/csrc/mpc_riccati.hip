@@ -193,7 +193,10 @@ __host__ __device__ inline RLds r_layout_ex(const MpcConst& c, bool gr) {
     L.Kd = take(2 * c.nu * d.na);
     L.psid = take(4 * nx);
     L.stamps = take(kStampSlots);
-    L.cst = take((int)((sizeof(MpcConst) + 7) / 8));
+    // the weights' LDS copy, up to the last Q entry in use: at BASELINE cfg5 the whole struct made the
+    // image 41.3 KB, over the 40 KB that lets four waves share a CU (three did: a quarter of the
+    // SIMDs idle); without Q's unused tail it is 40.4 KB
+    L.cst = take(mpc_const_used_doubles(c));
     L.total = o;
     return L;
 }
@@ -1689,7 +1692,7 @@ __global__ __launch_bounds__(kWave) void mpc_riccati_kernel(const MpcConst c_arg
     {
         const unsigned long long* src = reinterpret_cast<const unsigned long long*>(&c_arg);
         unsigned long long* dst = reinterpret_cast<unsigned long long*>(sm + L.cst);
-        for (int i = l; i < (int)(sizeof(MpcConst) / 8); i += kWave) dst[i] = src[i];
+        for (int i = l; i < mpc_const_used_doubles(c_arg); i += kWave) dst[i] = src[i];
         wsync();
     }
     const MpcConst& c = *reinterpret_cast<const MpcConst*>(sm + L.cst);
