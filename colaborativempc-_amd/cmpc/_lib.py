@@ -59,6 +59,13 @@ class cmpc_mpc_weights(ct.Structure):
                 ("row_slack", _IP), ("row_sign", _IP)]
 
 
+CMPC_SOLVER_CONDENSED_V3, CMPC_SOLVER_CONDENSED, CMPC_SOLVER_RICCATI, CMPC_SOLVER_LANE = 1, 2, 3, 4
+
+
+class cmpc_plan_info(ct.Structure):
+    _fields_ = [(k, ct.c_int) for k in ("solver", "lds_bytes", "wg_per_cu", "agents_per_wg")]
+
+
 class cmpc_mpc_data(ct.Structure):
     _fields_ = [(k, _DP) for k in ("A", "B", "x0", "u_prev", "qlin", "C", "h")]
 
@@ -193,6 +200,8 @@ SIGNATURES = {
     "cmpc_comm_init": (ct.c_int, [ct.c_void_p, ct.c_int, ct.c_int, ct.c_char_p]),
     "cmpc_allgather_trajectories": (ct.c_int, [ct.c_void_p, _DP, _DP, ct.c_ulonglong, ct.c_void_p]),
     "cmpc_comm_sum_i32": (ct.c_int, [ct.c_void_p, _IP, ct.c_ulonglong, ct.c_void_p]),
+    "cmpc_plan_mpc": (ct.c_int, [ct.POINTER(cmpc_mpc_dims), ct.POINTER(cmpc_mpc_weights), ct.POINTER(cmpc_opts),
+                                 ct.POINTER(cmpc_plan_info)]),
     "cmpc_comm_destroy": (ct.c_int, [ct.c_void_p]),
     "cmpc_lpv_rounds_create": (ct.c_int, [ct.c_void_p, ct.POINTER(cmpc_lpv_params), ct.POINTER(cmpc_track),
                                           ct.POINTER(cmpc_lpv_rounds_dims), ct.POINTER(cmpc_lpv_rounds_init),

@@ -57,6 +57,23 @@ def _flags(fp32=False, riccati=False, generic=False, rescue=False, lane=False):
         (L.CMPC_FLAG_LANE if lane else 0)
 
 
+def plan(shared, batch=1, fp32=False, riccati=False, generic=False, lane=False):
+    """Which solver cmpc_solve_mpc_batch would run for this problem shape, and its occupancy
+    (cmpc_plan_mpc, host only): dict(solver=name, lds_bytes, wg_per_cu, agents_per_wg)."""
+    w, keep = _weights(shared)
+    d = _dims(shared, batch)
+    o = L.opts(None, None, _flags(fp32, riccati, generic, False, lane))
+    info = L.cmpc_plan_info()
+    rc = L.load().cmpc_plan_mpc(ct.byref(d), ct.byref(w), ct.byref(o), ct.byref(info))
+    if rc != L.CMPC_OK:
+        raise L.CmpcError(rc, "cmpc_plan_mpc")
+    names = {L.CMPC_SOLVER_CONDENSED_V3: "condensed_v3", L.CMPC_SOLVER_CONDENSED: "condensed",
+             L.CMPC_SOLVER_RICCATI: "riccati", L.CMPC_SOLVER_LANE: "lane"}
+    del keep
+    return dict(solver=names[info.solver], lds_bytes=info.lds_bytes, wg_per_cu=info.wg_per_cu,
+                agents_per_wg=info.agents_per_wg)
+
+
 def solve_mpc(p, ctx=None, tol=None, max_iter=None, fp32=False, riccati=False, generic=False, rescue=False,
               stamps=None, lane=False):
     """Solve a batch of structured agent-QPs on the GPU (host arrays in/out).

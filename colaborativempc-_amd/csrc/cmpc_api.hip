@@ -228,6 +228,34 @@ int cmpc_solve_mpc_batch_dev(cmpc_ctx* ctx, const cmpc_mpc_dims* dims, const cmp
     return CMPC_OK;
 }
 
+int cmpc_plan_mpc(const cmpc_mpc_dims* dims, const cmpc_mpc_weights* w, const cmpc_opts* opts, cmpc_plan_info* out) {
+    if (!dims || !w || !out) return CMPC_ERR_ARG;
+    cmpc::MpcConst c;
+    const char* msg = nullptr;
+    const int rc = cmpc::mpc_prepare(dims, w, opts, &c, &msg);
+    if (rc != CMPC_OK) return rc;
+    // the choice of mpc_launch: lane, Riccati, the specialised condensed kernel, the generic one
+    size_t lds;
+    out->agents_per_wg = 1;
+    if (c.lane) {
+        out->solver = CMPC_SOLVER_LANE;
+        lds = cmpc::mpc_lane_lds_bytes(c);
+        out->agents_per_wg = 32;
+    } else if (c.riccati) {
+        out->solver = CMPC_SOLVER_RICCATI;
+        lds = cmpc::mpc_riccati_lds_bytes(c);
+    } else if (!(opts && (opts->flags & CMPC_FLAG_GENERIC)) && (lds = cmpc::mpc3_lds_bytes(c)) != 0) {
+        out->solver = CMPC_SOLVER_CONDENSED_V3;
+    } else {
+        out->solver = CMPC_SOLVER_CONDENSED;
+        lds = cmpc::mpc_lds_bytes(c);
+    }
+    out->lds_bytes = (int)lds;
+    const size_t wg = lds ? cmpc::kMaxLdsBytes / lds : 4;
+    out->wg_per_cu = (int)(wg < 4 ? wg : 4);
+    return CMPC_OK;
+}
+
 int cmpc_solve_mpc_batch(cmpc_ctx* ctx, const cmpc_mpc_dims* d, const cmpc_mpc_weights* w,
                          const cmpc_mpc_data* in, const cmpc_mpc_out* out, const cmpc_opts* opts) {
     if (!ctx) return CMPC_ERR_ARG;

@@ -166,6 +166,9 @@ size_t mpc_lds_bytes(const MpcConst& c);
 hipError_t mpc_launch(const MpcConst& c, const MpcPtrs& p, int batch, hipStream_t s, int flags = 0);
 // v3 kernels of mpc_ipm3.hip (PlannerLPV row pattern, N <= 32); false when none covers the problem.
 bool mpc3_try_launch(const MpcConst& c, const MpcPtrs& p, int batch, hipStream_t s, hipError_t* err);
+// LDS bytes of the v3 instantiation mpc3_try_launch would run for c (0: none covers it)
+size_t mpc3_lds_bytes(const MpcConst& c);
+size_t mpc_lane_lds_bytes(const MpcConst& c);
 
 // LPV reference-semantics builder (scheduling + planes + weights + rows).
 struct LpvConst {

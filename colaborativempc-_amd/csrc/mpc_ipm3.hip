@@ -1452,6 +1452,42 @@ static hipError_t launch3_t(const MpcConst& c, const MpcPtrs& p, int batch, hipS
         return true;                                                        \
     }
 #if CMPC_V3_SET == 1
+// host: the LDS image of the instantiation mpc3_try_launch picks (the same coverage rules)
+size_t mpc3_lds_bytes(const MpcConst& c) {
+    if (c.ns != 3 || c.N > 32 || c.mc < 4 || c.n > 64) return 0;
+    for (int r = 0; r < c.mc; ++r)
+        if (c.row_slack[r] != slk(r) || c.row_sign[r] != (int)sgn(r)) return 0;
+    const int nb = c.mc - 4, T = c.npad / 16;
+    auto lay = [&](auto nx_c, auto nu_c, auto nb_c, auto ls_c) -> size_t {
+        constexpr int NX_ = decltype(nx_c)::value, NU_ = decltype(nu_c)::value, NB_ = decltype(nb_c)::value;
+        constexpr bool LS_ = decltype(ls_c)::value;
+        int o;
+        switch (T) {
+            case 1: o = lds3_layout<1, NX_, NU_, NB_, LS_>(c.N).total; break;
+            case 2: o = lds3_layout<2, NX_, NU_, NB_, LS_>(c.N).total; break;
+            case 3: o = lds3_layout<3, NX_, NU_, NB_, LS_>(c.N).total; break;
+            default: o = lds3_layout<4, NX_, NU_, NB_, LS_>(c.N).total; break;
+        }
+        return sizeof(double) * (size_t)o;
+    };
+    using std::integral_constant;
+#define LAY(NX_, NU_, NB_, LS_) \
+    lay(integral_constant<int, NX_>{}, integral_constant<int, NU_>{}, integral_constant<int, NB_>{}, \
+        integral_constant<bool, LS_>{})
+    if (c.nx == 4 && c.nu == 2 && nb <= 2)
+        return nb == 2 ? LAY(4, 2, 2, false) : (nb == 1 ? LAY(4, 2, 1, false) : LAY(4, 2, 0, false));
+    if (c.nx == 9 && c.nu == 2 && nb <= 3) {
+        if (c.lpv)
+            return nb == 3 ? LAY(9, 2, 3, true)
+                           : (nb == 2 ? LAY(9, 2, 2, true) : (nb == 1 ? LAY(9, 2, 1, true) : LAY(9, 2, 0, true)));
+        return nb == 3 ? LAY(9, 2, 3, false)
+                       : (nb == 2 ? LAY(9, 2, 2, false) : (nb == 1 ? LAY(9, 2, 1, false) : LAY(9, 2, 0, false)));
+    }
+    if (c.nx == 6 && c.nu == 3 && nb == 2) return LAY(6, 3, 2, false);
+#undef LAY
+    return 0;
+}
+
 bool mpc3_try_set2(const MpcConst& c, const MpcPtrs& p, int batch, hipStream_t s, hipError_t* err, int nb);
 bool mpc3_try_set3(const MpcConst& c, const MpcPtrs& p, int batch, hipStream_t s, hipError_t* err, int nb);
 bool mpc3_try_set4(const MpcConst& c, const MpcPtrs& p, int batch, hipStream_t s, hipError_t* err, int nb);

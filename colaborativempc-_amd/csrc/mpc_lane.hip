@@ -97,6 +97,12 @@ bool mpc_lane_supported(const MpcConst& c) {
     return (c.nx == 6 && c.nu == 3 && c.mc == 6 && c.ns == 3) || (c.nx == 4 && c.nu == 2 && c.mc == 6 && c.ns == 3);
 }
 
+size_t mpc_lane_lds_bytes(const MpcConst& c) {
+    if (c.nx == 6 && c.nu == 3 && c.mc == 6 && c.ns == 3) return 2 * (size_t)IMap<6, 3, 6, 3>::bytes;
+    if (c.nx == 4 && c.nu == 2 && c.mc == 6 && c.ns == 3) return 2 * (size_t)IMap<4, 2, 6, 3>::bytes;
+    return 0;
+}
+
 hipError_t mpc_lane_launch(const MpcConst& c, const MpcPtrs& p, int batch, hipStream_t s) {
     if (batch == 0) return hipSuccess;
     if (!p.ws) return hipErrorInvalidValue;

@@ -42,7 +42,8 @@
 extern "C" {
 #endif
 
-#define CMPC_ABI_VERSION 3   /* 2: cmpc_lpv_advance_dev status / infeasible, cmpc_lpv_rounds_*; 3: cmpc_opts.order */
+#define CMPC_ABI_VERSION 4   /* 2: cmpc_lpv_advance_dev status / infeasible, cmpc_lpv_rounds_*; 3: cmpc_opts.order;
+                                4: cmpc_comm_sum_i32, cmpc_plan_mpc */
 
 /* API error codes */
 #define CMPC_OK 0
@@ -169,6 +170,24 @@ int cmpc_solve_mpc_batch(cmpc_ctx* ctx, const cmpc_mpc_dims* dims, const cmpc_mp
 int cmpc_solve_mpc_batch_dev(cmpc_ctx* ctx, const cmpc_mpc_dims* dims, const cmpc_mpc_weights* w,
                              const cmpc_mpc_data* dev_in, const cmpc_mpc_out* dev_out,
                              const cmpc_opts* opts, void* hip_stream);
+
+/* The solver a structured batch would run, and how many of its workgroups share a CU — host only
+ * (no context, no device).  Every solver uses more than 256 VGPRs + AGPRs per lane, so one
+ * wavefront per SIMD (4 workgroups per CU at most); the LDS image then decides: wg_per_cu =
+ * min(4, 160 KB / lds_bytes).  The lane-per-agent solver packs 32 agents per workgroup.  Errors as
+ * cmpc_solve_mpc_batch (CMPC_ERR_UNSUPPORTED, CMPC_ERR_ARG). */
+#define CMPC_SOLVER_CONDENSED_V3 1 /* specialised condensed kernel (mpc_ipm3: PlannerLPV row pattern) */
+#define CMPC_SOLVER_CONDENSED 2    /* generic condensed kernel */
+#define CMPC_SOLVER_RICCATI 3      /* stage-wise Riccati kernel (long horizons, fp32 path) */
+#define CMPC_SOLVER_LANE 4         /* lane-per-agent stage-wise kernel */
+typedef struct {
+    int solver;        /* CMPC_SOLVER_* */
+    int lds_bytes;     /* dynamic LDS per workgroup */
+    int wg_per_cu;     /* workgroups resident per CU */
+    int agents_per_wg; /* 1, or 32 (lane solver) */
+} cmpc_plan_info;
+int cmpc_plan_mpc(const cmpc_mpc_dims* dims, const cmpc_mpc_weights* w, const cmpc_opts* opts,
+                  cmpc_plan_info* out);
 
 /* ------------------------------------------------------------------------
  * Reference-semantics LPV batch: one call = PlannerLPV.solve for every agent

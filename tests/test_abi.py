@@ -33,7 +33,27 @@ def test_library_exports_every_declared_symbol():
 
 
 def test_abi_version():
-    assert L.load().cmpc_abi_version() == 3
+    assert L.load().cmpc_abi_version() == 4
+
+
+def test_plan_occupancy_of_the_bench_configs():
+    """cmpc_plan_mpc (host only): the solver each BASELINE shape runs and how many of its workgroups
+    share a CU.  Guards the occupancy the bench numbers rest on: the cfg3 condensed kernel and the
+    cfg5 Riccati kernel (fp64 and the fp32 mode) must keep four one-wave workgroups per CU — one per
+    SIMD (round 3's cfg5 image grew to 41.3 KB, over the 40 KB for four, and ran three)."""
+    from cmpc import scenarios as S
+    from cmpc.solver import plan
+
+    p3 = plan(S.di_shared(2, 30, 2), 1024)
+    assert p3["solver"] == "condensed_v3" and p3["wg_per_cu"] == 4 and p3["lds_bytes"] <= 40 * 1024, p3
+    for fp32 in (False, True):
+        p5 = plan(S.di_shared(3, 50, 2), 8192, fp32=fp32)
+        assert p5["solver"] == "riccati" and p5["wg_per_cu"] == 4 and p5["lds_bytes"] <= 40 * 1024, p5
+    pl = plan(S.di_shared(3, 50, 2), 8192, fp32=True, lane=True)
+    assert pl["solver"] == "lane" and pl["agents_per_wg"] == 32
+    assert plan(S.di_shared(2, 30, 2), 1024, generic=True)["solver"] == "condensed"
+    with pytest.raises(cmpc.CmpcError):   # no fp32 path for nb = 3 at these dimensions
+        plan(S.di_shared(2, 20, 3), 16, fp32=True)
 
 
 def test_no_cpu_fallback_without_device():
