@@ -39,7 +39,7 @@ __host__ __device__ constexpr int slk(int r) { return r == 0 ? -1 : (r == 1 ? 0 
 __host__ __device__ constexpr double sgn(int r) { return r < 4 ? 1.0 : -1.0; }
 
 struct Lds3 {
-    int cst, A, B, C, H, Pq, x0, up, W, Gb, Yb, X, dX, yb, U, dU, rd, vb, thin, bU, Ld, red, stamps, Phi, total;
+    int cst, A, B, C, H, Pq, x0, up, W, Gb, Yb, X, dX, yb, U, dU, rd, vb, thin, bU, Ld, red, stamps, Phi, Pst, total;
 };
 
 // LS (the reference's own agent, nx 9 / nu 2, built by lpv_build.hip): the model's structure is
@@ -63,6 +63,8 @@ __host__ __device__ constexpr int ls_cw() { return 4 + 2 * NB; }
 // from N stage steps to ceil(N / 4) + 2.  For the small-state instantiations (NX <= 4: the LDS image
 // has room for Phi) with T >= 2 tiles and NU <= 2, i.e. N > 8: every segment is non-empty.
 __host__ __device__ constexpr int seg_a(int q, int N) { return (q * N + 3) / 4; }
+// ... and of the adjoint over the stages k = 1..N: [b_q, b_{q+1}), b_0 = 1, b_4 = N + 1
+__host__ __device__ constexpr int seg_b(int q, int N) { return 1 + (q * N + 3) / 4; }
 template <int T, int NX, int NU, bool LS>
 __host__ __device__ constexpr bool seg_on() {
     return !LS && NX <= 4 && NU <= 2 && T >= 2;
@@ -86,29 +88,34 @@ __host__ __device__ inline Lds3 lds3_layout(int N) {
     L.Pq = take((N + 1) * NX);
     L.x0 = take(NX);
     L.up = take(NU);
-    // the Cholesky panel scratch ((T-1) x 16 x 17) aliases W after the K build; Gb extends W only
-    // where W is smaller than that (short horizons, small NX): at NX = 9 the extra 12 KB it used to
-    // take halved the agents per CU (90 KB -> 78 KB: two agents per CU instead of one)
+    // the Cholesky panel scratch ((T-1) x 16 x 17) aliases W | dX | yb after the K build (the stage
+    // weights are consumed by then, and the residuals' adjoints are done while the passes' have not
+    // begun); Gb extends them only where they are smaller than that (short horizons, small NX).  At
+    // NX = 9 the extra 12 KB it used to take halved the agents per CU (90 KB -> 78 KB); at cfg3 the
+    // dX | yb alias makes room for the segmented recursions' transitions within 40 KB.
     const int wsz = LS ? N * kLsW : N * NX * NX;
     L.W = take(wsz);
-    const int sp_need = (T - 1) * 16 * 17 - wsz;
+    L.dX = take((N + 1) * NX);
+    L.yb = take((N + 1) * NX);
+    const int sp_need = (T - 1) * 16 * 17 - (L.yb + (((N + 1) * NX + 1) & ~1) - L.W);
     L.Gb = take(sp_need > 0 ? sp_need : 0);
     L.Yb = L.Gb;
     L.X = take((N + 1) * NX);
-    L.dX = take((N + 1) * NX);
-    L.yb = take((N + 1) * NX);
     L.U = take(NP);
     L.dU = take(NP);
     L.rd = take(NP);
     L.vb = take(NP);
     L.thin = take(NP);
-    L.bU = take(NP);
+    // the best iterate's U lives in a register where the segmented recursions need the room (NP <= 64)
+    L.bU = take(seg_on<T, NX, NU, LS>() ? 0 : NP);
     L.Ld = take(T * 16 * 17);
     L.red = take(16);
     L.stamps = take(kStampSlots);
     // segmented forward simulation (kSeg): the transitions Phi_k of stages (a_1, N] (fwd3seg); 352
     // doubles at N = 30, NX = 4
     L.Phi = take(seg_on<T, NX, NU, LS>() ? (N - seg_a(1, N)) * NX * NX : 0);
+    // ... and the transposed transitions Psi'_k of the segmented adjoint (psi3seg): 352 doubles at N = 30
+    L.Pst = take(seg_on<T, NX, NU, LS>() ? (seg_b(3, N) - 1) * NX * NX : 0);
     L.total = o;
     return L;
 }
@@ -309,6 +316,116 @@ __device__ __forceinline__ void fwd3seg(int l, int N, const double* A, const dou
     }
 }
 
+// Psi'_k (transposed) for k in [1, b_3): x_{b_{q+1}} = Psi_k x_k, the transition of stages k ..
+// b_{q+1} - 1 of segment q (seg_b); rows 0..2 build their segment's in parallel from the top
+// (Psi'_k = A_k' Psi'_{k+1}), lane s holding row s; stored at slot k - 1.
+template <int NX>
+__device__ __forceinline__ void psi_build(int l, int N, const double* A, double* Pst) {
+    const int q = l >> 4, s = (l & 15) < NX ? (l & 15) : 0;
+    const int b = seg_b(q, N), e = seg_b(q + 1, N), len = seg_b(1, N) - 1;
+    double tr[NX];
+#pragma unroll
+    for (int c = 0; c < NX; ++c) tr[c] = (s == c) ? 1.0 : 0.0;
+    for (int i = 0; i < len; ++i) {
+        const int k = e - 1 - i;
+        const bool valid = q <= 2 && k >= b;
+        const int kc = valid ? k : 1;
+        double at[NX], nw[NX];
+#pragma unroll
+        for (int t = 0; t < NX; ++t) at[t] = A[(kc * NX + t) * NX + s];
+        static_for<0, NX>([&](auto c_c) __attribute__((always_inline)) {
+            constexpr int cc = decltype(c_c)::value;
+            double v = 0.0;
+            static_for<0, NX>([&](auto t_c) __attribute__((always_inline)) {
+                constexpr int tt = decltype(t_c)::value;
+                v = fma(at[tt], bcast16<tt>(tr[cc]), v);
+            });
+            nw[cc] = v;
+        });
+#pragma unroll
+        for (int c = 0; c < NX; ++c) tr[c] = valid ? nw[c] : tr[c];
+        if (valid && (l & 15) < NX) {
+#pragma unroll
+            for (int c = 0; c < NX; ++c) Pst[((k - 1) * NX + s) * NX + c] = tr[c];
+        }
+    }
+}
+
+// psi3 (psi_N = y_N, psi_k = y_k + A_k' psi_{k+1}, k = N-1 .. 1, over y in place) by segments: each row
+// runs its segment from psi^loc = 0 above it (the top one from psi_N = y_N), a two-step chain carries
+// psi down the segment tops, each row corrects its stages, psi_k = psi^loc_k + Psi'_k psi_{b_{q+1}}.
+template <int NX>
+__device__ __forceinline__ void psi3seg(int l, int N, const double* A, double* y, const double* Pst) {
+    const int q = l >> 4, j = l & 15, s = j < NX ? j : 0;
+    const int b = seg_b(q, N), e = seg_b(q + 1, N), len = seg_b(1, N) - 1;
+    double pr = 0.0;  // psi^loc_{k+1}: zero above the segment
+    auto fetch = [&](int i, double* av) __attribute__((always_inline)) {
+        const int k = e - 1 - i >= b ? e - 1 - i : b;
+        const int ka = k < N ? k : N - 1;  // psi_N = y_N: A_N does not exist (pr = 0 there)
+#pragma unroll
+        for (int t = 0; t < NX; ++t) av[t] = A[(ka * NX + t) * NX + s];
+        av[NX] = y[k * NX + s];
+    };
+    auto step = [&](int i, const double* av) __attribute__((always_inline)) {
+        const int k = e - 1 - i >= b ? e - 1 - i : b;
+        double p0 = av[NX], p1 = 0.0;
+        static_for<0, NX>([&](auto t) __attribute__((always_inline)) {
+            constexpr int tt = decltype(t)::value;
+            if constexpr (tt & 1) p1 = fma(av[tt], bcast16<tt>(pr), p1);
+            else p0 = fma(av[tt], bcast16<tt>(pr), p0);
+        });
+        pr = (e - 1 - i >= b) ? p0 + p1 : pr;
+        y[k * NX + s] = pr;
+    };
+    double a0[NX + 1], a1[NX + 1];
+    fetch(0, a0);
+    int i = 0;
+    for (; i + 1 < len; i += 2) {
+        fetch(i + 1, a1);
+        __builtin_amdgcn_sched_barrier(0);
+        step(i, a0);
+        fetch(i + 2, a0);
+        __builtin_amdgcn_sched_barrier(0);
+        step(i + 1, a1);
+    }
+    if (i < len) step(i, a0);
+    wsync();
+    // segment tops, from above: psi_{b_3} is exact (the top segment began at psi_N); row q keeps
+    // psi_{b_{q+1}} for its stages
+    double pq[NX];
+    {
+        double xa[NX], ph[NX];
+        double v = y[seg_b(3, N) * NX + s];
+#pragma unroll
+        for (int qq = 2; qq >= 0; --qq) {
+            static_for<0, NX>([&](auto t) __attribute__((always_inline)) {
+                constexpr int tt = decltype(t)::value;
+                xa[tt] = bcast16<tt>(v);
+            });
+#pragma unroll
+            for (int t = 0; t < NX; ++t) pq[t] = (q == qq) ? xa[t] : pq[t];
+            if (qq == 0) break;
+            const int bb = seg_b(qq, N);
+#pragma unroll
+            for (int t = 0; t < NX; ++t) ph[t] = Pst[((bb - 1) * NX + s) * NX + t];
+            v = phi_apply<NX>(ph, xa, y[bb * NX + s]);
+        }
+    }
+    // rows 0..2 correct their stages [b_q, b_{q+1}): at most 8 stages x NX entries, 2 per lane
+    if (q <= 2) {
+#pragma unroll
+        for (int h = 0; h < (8 * NX + 15) / 16; ++h) {
+            const int idx = j + 16 * h, k = b + idx / NX, r = idx % NX;
+            if (k < e) {
+                double ph[NX];
+#pragma unroll
+                for (int t = 0; t < NX; ++t) ph[t] = Pst[((k - 1) * NX + r) * NX + t];
+                y[k * NX + r] = phi_apply<NX>(ph, pq, y[k * NX + r]);
+            }
+        }
+    }
+}
+
 // The adjoint's serial part only: psi_N = y_N, psi_k = y_k + A_k' psi_{k+1} for k = N-1 .. 1,
 // written over y in place (rows 0,1 of the wave on y0, rows 2,3 on y1; y_k is fetched before
 // psi_k overwrites it).  The products o_k = B_k' psi_{k+1} are independent of one another and
@@ -490,7 +607,7 @@ __global__ __launch_bounds__(64, 1) void mpc_ipm3_kernel(const MpcConst c, const
             dU[i] = 0.0;
             vb[i] = 0.0;
             thin[i] = 0.0;
-            bU[i] = 0.0;
+            if constexpr (!seg_on<T, NX, NU, LS>()) bU[i] = 0.0;
         }
     }
     // ---- rows owned by this lane: stage k+1 rows (lanes 0..31) or input rows of u_k (32..63) ----
@@ -518,16 +635,20 @@ __global__ __launch_bounds__(64, 1) void mpc_ipm3_kernel(const MpcConst c, const
 #define ACT(r) ((actm >> (r)) & 1u)
     constexpr bool kSeg = seg_on<T, NX, NU, LS>();
     double* sPhi = sm + L.Phi;
-    // x_{k+1} = A_k x_k + B_k u_k, by segments where the instantiation has them
-    auto fwd = [&](const double* x0v, const double* Uv, double* Xv) __attribute__((always_inline)) {
-        if constexpr (kSeg) fwd3seg<NX, NU>(l, N, sA, sB, x0v, Uv, Xv, sPhi);
-        else fwd3<NX, NU, LS>(l, N, sA, sB, x0v, Uv, Xv);
+    // x_{k+1} = A_k x_k + B_k u_k, by segments where the instantiation has them.  The lane index is
+    // an argument: inside the iteration loop it is the loop's own (opaque) copy, so the segment
+    // bounds derived from it are recomputed there instead of hoisted and held across the loop
+    auto fwd = [&](int lv, const double* x0v, const double* Uv, double* Xv) __attribute__((always_inline)) {
+        if constexpr (kSeg) fwd3seg<NX, NU>(lv, N, sA, sB, x0v, Uv, Xv, sPhi);
+        else fwd3<NX, NU, LS>(lv, N, sA, sB, x0v, Uv, Xv);
     };
+    double* sPst = sm + L.Pst;
     if constexpr (kSeg) {
         phi_build<NX>(l, N, sA, sPhi);
+        psi_build<NX>(l, N, sA, sPst);
         wsync();
     }
-    fwd(sx0, U, X);
+    fwd(l, sx0, U, X);
     wsync();
 
     // value of row r at (Xv, Uv[, sig]) for this lane's rows
@@ -575,6 +696,7 @@ __global__ __launch_bounds__(64, 1) void mpc_ipm3_kernel(const MpcConst c, const
     // best iterate by merit max(res, 1e4 mu) (< tol <=> converged), returned when the method
     // stops short of convergence (iteration cap, factorisation breakdown, stagnation)
     double best_m = INFINITY, best_kkt = INFINITY, bsg[NS] = {0.0, 0.0, 0.0};
+    double bu_r = 0.0;  // best iterate's U[l] (segmented instantiations; else the LDS image bU)
     int best_it = 0, stop = kStopMaxIter, it;
     double kkt = INFINITY;
     // iDs: 1 / D_sigma of the stage's slack groups (one division each per iteration; the W build, rho~
@@ -629,7 +751,9 @@ __global__ __launch_bounds__(64, 1) void mpc_ipm3_kernel(const MpcConst c, const
         if (l < NX) dX[l] = yb[l];
         wsync();
         STAMP(0);
-        psi3<NX, LS>(l, N, sA, yb, dX);  // psi over yb (-> gradient) and over dX (-> rd)
+        // psi over yb (-> gradient) and over dX (-> rd): two 30-stage chains side by side on the rows of
+        // the wave (segmenting both on the quads of the rows measured slower: 3.7k -> 3.9k clk)
+        psi3<NX, LS>(l, N, sA, yb, dX);
         wsync();
         STAMP(1);
         double gs_l = 1.0, nrd_l = 0.0, nrs_l = 0.0, nrp_l = 0.0, mu_l = 0.0;
@@ -689,7 +813,9 @@ __global__ __launch_bounds__(64, 1) void mpc_ipm3_kernel(const MpcConst c, const
             best_m = merit;
             best_kkt = kkt;
             best_it = it;
-            for (int i = l; i < NP; i += 64) bU[i] = U[i];
+            if constexpr (seg_on<T, NX, NU, LS>()) bu_r = l < NP ? U[l] : 0.0;  // NP <= 64: one per lane
+            else
+                for (int i = l; i < NP; i += 64) bU[i] = U[i];
 #pragma unroll
             for (int j = 0; j < NS; ++j) bsg[j] = sg[j];
         }
@@ -1210,7 +1336,8 @@ __global__ __launch_bounds__(64, 1) void mpc_ipm3_kernel(const MpcConst c, const
             if (l < NX) yb[l] = 0.0;
             wsync();
             STAMP(8);
-            psi3<NX, LS>(l, N, sA, yb, yb);
+            if constexpr (kSeg) psi3seg<NX>(l, N, sA, yb, sPst);
+            else psi3<NX, LS>(l, N, sA, yb, yb);
             wsync();
             STAMP(9);
             if (!lo && own) {
@@ -1286,7 +1413,7 @@ __global__ __launch_bounds__(64, 1) void mpc_ipm3_kernel(const MpcConst c, const
             for (int i = l; i < NP; i += 64) dU[i] = (i < n) ? vb[i] : 0.0;
             wsync();
             STAMP(10);
-            fwd(nullptr, dU, dX);
+            fwd(l, nullptr, dU, dX);
             wsync();
             STAMP(11);
 #pragma unroll
@@ -1370,7 +1497,11 @@ __global__ __launch_bounds__(64, 1) void mpc_ipm3_kernel(const MpcConst c, const
     int status = CMPC_SOLVED;
     if (stop != kStopConverged) {
         if (best_it > 0) {  // restore the best iterate
-            for (int i = l; i < NP; i += 64) U[i] = bU[i];
+            if constexpr (seg_on<T, NX, NU, LS>()) {
+                if (l < NP) U[l] = bu_r;
+            } else {
+                for (int i = l; i < NP; i += 64) U[i] = bU[i];
+            }
 #pragma unroll
             for (int j = 0; j < NS; ++j) sg[j] = bsg[j];
             kkt = best_kkt;
@@ -1380,7 +1511,7 @@ __global__ __launch_bounds__(64, 1) void mpc_ipm3_kernel(const MpcConst c, const
     wsync();
 
     // ---- output in the reference layout ----
-    fwd(sx0, U, X);
+    fwd(l, sx0, U, X);
     wsync();
     constexpr int NXE = NX + NS;
     const size_t nz = (size_t)NXE * (N + 1) + 2 * (size_t)n;
