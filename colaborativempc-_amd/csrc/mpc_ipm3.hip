@@ -106,8 +106,7 @@ __host__ __device__ inline Lds3 lds3_layout(int N) {
     L.rd = take(NP);
     L.vb = take(NP);
     L.thin = take(NP);
-    // the best iterate's U lives in a register where the segmented recursions need the room (NP <= 64)
-    L.bU = take(seg_on<T, NX, NU, LS>() ? 0 : NP);
+    L.bU = take(NP);
     L.Ld = take(T * 16 * 17);
     L.red = take(16);
     L.stamps = take(kStampSlots);
@@ -607,7 +606,7 @@ __global__ __launch_bounds__(64, 1) void mpc_ipm3_kernel(const MpcConst c, const
             dU[i] = 0.0;
             vb[i] = 0.0;
             thin[i] = 0.0;
-            if constexpr (!seg_on<T, NX, NU, LS>()) bU[i] = 0.0;
+            bU[i] = 0.0;
         }
     }
     // ---- rows owned by this lane: stage k+1 rows (lanes 0..31) or input rows of u_k (32..63) ----
@@ -696,7 +695,6 @@ __global__ __launch_bounds__(64, 1) void mpc_ipm3_kernel(const MpcConst c, const
     // best iterate by merit max(res, 1e4 mu) (< tol <=> converged), returned when the method
     // stops short of convergence (iteration cap, factorisation breakdown, stagnation)
     double best_m = INFINITY, best_kkt = INFINITY, bsg[NS] = {0.0, 0.0, 0.0};
-    double bu_r = 0.0;  // best iterate's U[l] (segmented instantiations; else the LDS image bU)
     int best_it = 0, stop = kStopMaxIter, it;
     double kkt = INFINITY;
     // iDs: 1 / D_sigma of the stage's slack groups (one division each per iteration; the W build, rho~
@@ -813,9 +811,7 @@ __global__ __launch_bounds__(64, 1) void mpc_ipm3_kernel(const MpcConst c, const
             best_m = merit;
             best_kkt = kkt;
             best_it = it;
-            if constexpr (seg_on<T, NX, NU, LS>()) bu_r = l < NP ? U[l] : 0.0;  // NP <= 64: one per lane
-            else
-                for (int i = l; i < NP; i += 64) bU[i] = U[i];
+            for (int i = l; i < NP; i += 64) bU[i] = U[i];
 #pragma unroll
             for (int j = 0; j < NS; ++j) bsg[j] = sg[j];
         }
@@ -829,20 +825,26 @@ __global__ __launch_bounds__(64, 1) void mpc_ipm3_kernel(const MpcConst c, const
         }
 
         // ================= Newton matrix K = Gamma' W Gamma + Hc + diag =================
-        // 1 / t_r once per iteration (theta and both passes' rho use it)
+        // theta = lam / t through 1 / t_r, and 1 / D_sigma.  The passes need 1 / t_r, theta and 1 / D_sigma
+        // again: they recompute them after the factorisation, bit for bit, rather than hold 15 doubles
+        // in registers across the K build and the Cholesky (held, they made the T = 4 instantiation
+        // spill to scratch).  `oz` is an opaque zero that keeps the compiler from merging the two.
         double tin[RX];
+        auto theta = [&](double oz) __attribute__((always_inline)) {
 #pragma unroll
-        for (int r = 0; r < RX; ++r) tin[r] = ACT(r) ? 1.0 / t[r] : 0.0;
+            for (int r = 0; r < RX; ++r) tin[r] = ACT(r) ? 1.0 / (t[r] + oz) : 0.0;
 #pragma unroll
-        for (int r = 0; r < RX; ++r) th[r] = lam[r] * tin[r];
+            for (int r = 0; r < RX; ++r) th[r] = lam[r] * tin[r];
 #pragma unroll
-        for (int j = 0; j < NS; ++j) {
-            double v = Qs2[j];
+            for (int j = 0; j < NS; ++j) {
+                double v = Qs2[j];
 #pragma unroll
-            for (int r = 0; r < MC; ++r)
-                if (slk(r) == j) v += th[r];
-            iDs[j] = 1.0 / v;
-        }
+                for (int r = 0; r < MC; ++r)
+                    if (slk(r) == j) v += th[r];
+                iDs[j] = 1.0 / v;
+            }
+        };
+        theta(0.0);
         if (own) {
             if (lo) {
                 // W_{k+1} = 2Q + sum_r th'_r c_r c_r' + sum_{pairs in a slack group} phi (a_r - a_r')(a_r - a_r')'
@@ -1281,6 +1283,11 @@ __global__ __launch_bounds__(64, 1) void mpc_ipm3_kernel(const MpcConst c, const
         const double* Lme = Ld + ((l >> 4) < T ? (l >> 4) : 0) * 272;
 
         // ================= predictor / corrector =================
+        {
+            int ozi;
+            asm volatile("v_mov_b32 %0, 0" : "=v"(ozi));
+            theta((double)ozi);
+        }
         double sig_c = 0.0, alpha = 0.0;
         for (int pass = 0; pass < 2; ++pass) {
             // pass 1: Mehrotra's second-order term dt_aff * dl_aff from the predictor still in (rho, gdu, dsg)
@@ -1497,11 +1504,7 @@ __global__ __launch_bounds__(64, 1) void mpc_ipm3_kernel(const MpcConst c, const
     int status = CMPC_SOLVED;
     if (stop != kStopConverged) {
         if (best_it > 0) {  // restore the best iterate
-            if constexpr (seg_on<T, NX, NU, LS>()) {
-                if (l < NP) U[l] = bu_r;
-            } else {
-                for (int i = l; i < NP; i += 64) U[i] = bU[i];
-            }
+            for (int i = l; i < NP; i += 64) U[i] = bU[i];
 #pragma unroll
             for (int j = 0; j < NS; ++j) sg[j] = bsg[j];
             kkt = best_kkt;

@@ -11,6 +11,8 @@ from conftest import KKT_TOL, LPV_CASES, assert_matches_optimum, golden, lpv_qps
 pytestmark = pytest.mark.gpu
 
 Z_TOL = 1e-6
+# agents at the rounding floor (status 2 on either side, KKT <= 1e-6 on both) against the C restatement
+FLOOR_ZTOL = 1e-5   # measured 1.4e-6 on the rescue round (tests below)
 
 
 def _gains():
@@ -205,14 +207,21 @@ def test_rescue_pass_resolves_factorisation_breakdowns(gpu_ctx, finish):
                      u_prev=R.u_old.cpu().numpy(), qlin=b["qlin"], C=b["C"], h=b["h"])
             zc, kc, ic, sc = CO.solve_batch_rescue(P, nthreads=8, finish=finish)
             both = (sc == 1) & (st1 == 1)
+            floor = ~both
             err = np.abs(zc - z1).max(1)
             print(f"round {rnd}: {int(bad.sum())} broken down (status -10), {int(changed.sum())} continued; "
-                  f"{int(both.sum())} of {R.B} solved by both, max |dz| {err[both].max():.1e}; GPU status 2 "
-                  f"{int((st1 == 2).sum())}; C statuses {dict(zip(*[a.tolist() for a in np.unique(sc, return_counts=True)]))}")
-            # agents at the rounding floor (status 2, KKT <= 1e-6 asserted above) are not compared;
-            # without CMPC_FLAG_FINISH a breakdown already at the floor stays there (~8 % of this
-            # round on both sides), with it they are finished
-            assert both.mean() >= (0.95 if finish else 0.85) and err[both].max() < 1e-6
+                  f"{int(both.sum())} of {R.B} solved by both, max |dz| {err[both].max():.1e}; at the rounding floor "
+                  f"on either side {int(floor.sum())}, max |dz| {err[floor].max() if floor.any() else 0:.1e}, "
+                  f"max C kkt {kc[floor].max() if floor.any() else 0:.1e}; GPU status 2 {int((st1 == 2).sum())}; C "
+                  f"statuses {dict(zip(*[a.tolist() for a in np.unique(sc, return_counts=True)]))}")
+            # every agent is compared: where both sides converge, to 1e-6; where either stops at the
+            # rounding floor (status 2: merit below 1e3 tol, KKT <= 1e-6 on both sides), to the floor's
+            # accuracy (measured: 1.4e-6).  Without CMPC_FLAG_FINISH a breakdown already at the floor stays
+            # there (~10 % of this round on either side); with it they are finished (~5 % left)
+            assert np.isin(sc, (1, 2)).all() and (kc <= 1e-6).all(), (np.unique(sc), kc.max())
+            assert err[both].max() < 1e-6
+            assert floor.mean() <= (0.07 if finish else 0.12), floor.mean()
+            assert not floor.any() or err[floor].max() < FLOOR_ZTOL, err[floor].max()
             return
         R.advance()
         R.exchange()
