@@ -12,6 +12,10 @@ namespace cmpc {
 // Stage k (0..N) of agent b: p_k -> pk[nx]; for k >= 1 also the rows of stage k (C_{k-1} ->
 // Ck[mc*nx], h_{k-1} -> hk[mc], mc = 4 + nb).  own: the agent's exchanged trajectory
 // ((N+1) x 2), nbr: its nb neighbour indices into traj_all.
+// COMPACT (the v3 kernel's DS images, 2-D double integrator): Ck receives only the planes'
+// coefficients [a_x, a_y] per neighbour (2 nb values); the other rows' coefficients are the
+// constants -1 / +1 on v_x and +1 / -1 on p_y.  Same arithmetic, same bits.
+template <bool COMPACT = false>
 __device__ __forceinline__ void di_stage_rows(const DiConst& c, const int* nbr, double lane, const double* traj_all,
                                               const double* own, int k, double* pk, double* Ck, double* hk) {
 #pragma clang fp contract(off)
@@ -22,14 +26,16 @@ __device__ __forceinline__ void di_stage_rows(const DiConst& c, const int* nbr, 
     pk[ipy] = -lane * c.q_lane;
     if (k == 0) return;
     const int h1 = k - 1;
-    for (int i = 0; i < mc * nx; ++i) Ck[i] = 0.0;
-    Ck[0 * nx + ivx] = -1.0;
+    if (!COMPACT) {
+        for (int i = 0; i < mc * nx; ++i) Ck[i] = 0.0;
+        Ck[0 * nx + ivx] = -1.0;
+        Ck[1 * nx + ivx] = 1.0;
+        Ck[2 * nx + ipy] = 1.0;
+        Ck[3 * nx + ipy] = -1.0;
+    }
     hk[0] = -c.min_vel;
-    Ck[1 * nx + ivx] = 1.0;
     hk[1] = c.max_vel;
-    Ck[2 * nx + ipy] = 1.0;
     hk[2] = c.hw + lane;
-    Ck[3 * nx + ipy] = -1.0;
     hk[3] = c.hw - lane;
     double px = 0.0, py = 0.0;
     for (int i = 0; i < nb; ++i) {
@@ -42,7 +48,7 @@ __device__ __forceinline__ void di_stage_rows(const DiConst& c, const int* nbr, 
         const double bb = -0.5 * (ax * (ex + nx_) + ay * (ey + ny_));
         const double qx = own[k * 2] - nt[k * 2], qy = own[k * 2 + 1] - nt[k * 2 + 1];
         const double wgt = (2.0 * c.min_dist - sqrt(qx * qx + qy * qy)) / nb;
-        double* cr = Ck + (4 + i) * nx;
+        double* cr = COMPACT ? Ck + 2 * i : Ck + (4 + i) * nx;
         cr[0] = ax;
         cr[1] = ay;
         hk[4 + i] = -c.min_dist / 2 - bb;

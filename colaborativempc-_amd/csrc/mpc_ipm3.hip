@@ -54,6 +54,18 @@ constexpr int kLsW = 5;  // LS stage weights: w(vx,vx), w(ey,ey), w(X,X), w(X,Y)
 template <int NB>
 __host__ __device__ constexpr int ls_cw() { return 4 + 2 * NB; }
 
+// DS (the synthetic 2-D double integrator's fused round, x = [p_x p_y v_x v_y], rows built by
+// di_rows.h inside the launch): rows 0..3 are -v_x, v_x, p_y, -p_y (constant coefficients), the planes
+// a_x p_x + a_y p_y, Q diagonal.  The images shrink to the planes' coefficients (N x 2 nb) and the
+// six entries of W_k that are not exactly zero (w_xx, w_xy, w_yx, w_yy on (p_x, p_y), w_vx, w_vy);
+// every product and sum is the dense form's, in its order, without the exact zeros: same bits.
+// Bit equality with the dense instantiation also needs the same fma contraction in both: the
+// backend's cross-statement contraction (-ffp-contract=fast) decides per use count of a product and
+// so differs between the two instantiations; this file is built with -ffp-contract=on (Makefile).
+constexpr int kDsW = 6;
+template <int NB>
+__host__ __device__ constexpr int ds_cw() { return NB > 0 ? 2 * NB : 2; }
+
 // Segmented (parallel-in-time) forward simulation: the horizon's N stages split into four
 // segments [a_q, a_{q+1}), one per row of 16 lanes.  Each row runs its segment's recursion from a
 // zero state (row 0 from x_0); a two-step chain then carries the true state across the segment
@@ -70,7 +82,7 @@ __host__ __device__ constexpr bool seg_on() {
     return !LS && NX <= 4 && NU <= 2 && T >= 2;
 }
 
-template <int T, int NX, int NU, int NB, bool LS = false>
+template <int T, int NX, int NU, int NB, bool LS = false, bool DS = false>
 __host__ __device__ inline Lds3 lds3_layout(int N) {
     constexpr int NP = 16 * T, MC = 4 + NB;
     Lds3 L;
@@ -83,7 +95,7 @@ __host__ __device__ inline Lds3 lds3_layout(int N) {
     L.cst = take(NX * NX + 2 * NU * NU + 3 + 2 * NU);
     L.A = take(LS ? N * NX * 3 : N * NX * NX);
     L.B = take(LS ? N * 3 * NU : N * NX * NU);
-    L.C = take(LS ? N * ls_cw<NB>() : N * MC * NX);
+    L.C = take(LS ? N * ls_cw<NB>() : (DS ? N * ds_cw<NB>() : N * MC * NX));
     L.H = take(N * MC);
     L.Pq = take((N + 1) * NX);
     L.x0 = take(NX);
@@ -93,7 +105,7 @@ __host__ __device__ inline Lds3 lds3_layout(int N) {
     // begun); Gb extends them only where they are smaller than that (short horizons, small NX).  At
     // NX = 9 the extra 12 KB it used to take halved the agents per CU (90 KB -> 78 KB); at cfg3 the
     // dX | yb alias makes room for the segmented recursions' transitions within 40 KB.
-    const int wsz = LS ? N * kLsW : N * NX * NX;
+    const int wsz = LS ? N * kLsW : (DS ? N * kDsW : N * NX * NX);
     L.W = take(wsz);
     L.dX = take((N + 1) * NX);
     L.yb = take((N + 1) * NX);
@@ -499,16 +511,18 @@ __device__ __forceinline__ double bpsi3(const double* B, const double* psi, int 
 
 }  // namespace
 
-template <int T, int NX, int NU, int NB, bool LS = false>
+template <int T, int NX, int NU, int NB, bool LS = false, bool DS = false>
 __global__ __launch_bounds__(64, 1) void mpc_ipm3_kernel(const MpcConst c, const MpcPtrs P) {
     constexpr int MC = 4 + NB, NS = 3, NT = T * (T + 1) / 2, NP = 16 * T, NXP = (NX + 3) & ~3;
     constexpr int NI = 2 * NU, RX = MC > NI ? MC : NI;
     constexpr int CW = ls_cw<NB>();  // LS: row coefficients per stage
     static_assert(!LS || (NX == 9 && NU == 2), "LS: the reference's agent model");
+    static_assert(!DS || (NX == 4 && NU == 2 && !LS), "DS: the 2-D double integrator");
+    constexpr int CWD = ds_cw<NB>();  // DS: plane coefficients per stage
     extern __shared__ __attribute__((aligned(16))) double sm[];
     const int l0 = threadIdx.x, b = blockIdx.x, N = c.N, n = N * NU, ms = N * MC;
     const int l = l0;
-    const Lds3 L = lds3_layout<T, NX, NU, NB, LS>(N);
+    const Lds3 L = lds3_layout<T, NX, NU, NB, LS, DS>(N);
     double* Q2 = sm + L.cst;          // 2Q
     double* R2 = Q2 + NX * NX;        // 2R
     double* dR2 = R2 + NU * NU;       // 2dR
@@ -582,7 +596,10 @@ __global__ __launch_bounds__(64, 1) void mpc_ipm3_kernel(const MpcConst c, const
             const double ln = F.lane[b];
             for (int kk = l; kk <= N; kk += 64) {
                 const int h1 = kk > 0 ? kk - 1 : 0;
-                di_stage_rows(F.c, nbr, ln, F.traj_all, own, kk, sP + kk * NX, sC + h1 * MC * NX, sH + h1 * MC);
+                if constexpr (DS)
+                    di_stage_rows<true>(F.c, nbr, ln, F.traj_all, own, kk, sP + kk * NX, sC + h1 * CWD, sH + h1 * MC);
+                else
+                    di_stage_rows(F.c, nbr, ln, F.traj_all, own, kk, sP + kk * NX, sC + h1 * MC * NX, sH + h1 * MC);
             }
         } else {
             for (int i = l; i < N * MC * NX; i += 64) sC[i] = gC[i];
@@ -659,6 +676,13 @@ __global__ __launch_bounds__(64, 1) void mpc_ipm3_kernel(const MpcConst c, const
             if (r < 2) v = cr[r] * xk[0];
             else if (r < 4) v = cr[r] * xk[3];
             else v = fma(cr[4 + 2 * (r - 4) + 1], xk[8], cr[4 + 2 * (r - 4)] * xk[7]);
+        } else if constexpr (DS) {  // the dense chain's nonzero terms, from the same +0 start
+            if (r < 2) v = fma(r == 0 ? -1.0 : 1.0, xk[2], 0.0);
+            else if (r < 4) v = fma(r == 2 ? 1.0 : -1.0, xk[1], 0.0);
+            else {
+                const double* cr = sC + k * CWD + 2 * (r - 4);
+                v = fma(cr[1], xk[1], fma(cr[0], xk[0], 0.0));
+            }
         } else {
             const double* cr = sC + (k * MC + r) * NX;
 #pragma unroll
@@ -736,6 +760,22 @@ __global__ __launch_bounds__(64, 1) void mpc_ipm3_kernel(const MpcConst c, const
                     }
                     dX[(k + 1) * NX + s2] = v;
                 });
+            } else if constexpr (DS) {
+                const double* cr = sC + k * CWD;
+                const double* y = yb + (k + 1) * NX;
+                double v0 = y[0], v1 = y[1], v2 = y[2];
+                v1 = fma(lam[3], -1.0, fma(lam[2], 1.0, v1));
+                v2 = fma(lam[1], 1.0, fma(lam[0], -1.0, v2));
+#pragma unroll
+                for (int q = 0; q < NB; ++q) {
+                    v0 = fma(lam[4 + q], cr[2 * q], v0);
+                    v1 = fma(lam[4 + q], cr[2 * q + 1], v1);
+                }
+                double* d = dX + (k + 1) * NX;
+                d[0] = v0;
+                d[1] = v1;
+                d[2] = v2;
+                d[3] = y[3];
             } else {
 #pragma unroll
                 for (int s = 0; s < NX; ++s) {
@@ -883,6 +923,47 @@ __global__ __launch_bounds__(64, 1) void mpc_ipm3_kernel(const MpcConst c, const
                     wk[2] = wxx;
                     wk[3] = wxy;
                     wk[4] = wyy;
+                } else if constexpr (DS) {
+                    // the dense build's entries that are not exact zeros, term by term in its order
+                    // (rows r, then the slack pairs: (2, 3) in group 1, the plane pairs in group 2)
+                    const double* cr = sC + k * CWD;
+                    double wxx = Q2[0], wxy = Q2[1], wyx = Q2[NX], wyy = Q2[NX + 1];
+                    double wvx = Q2[2 * NX + 2];
+                    wvx = fma(thp[0] * -1.0, -1.0, wvx);
+                    wvx = fma(thp[1] * 1.0, 1.0, wvx);
+                    wyy = fma(thp[2] * 1.0, 1.0, wyy);
+                    wyy = fma(thp[3] * -1.0, -1.0, wyy);
+#pragma unroll
+                    for (int q = 0; q < NB; ++q) {
+                        const double ax = cr[2 * q], ay = cr[2 * q + 1], tq = thp[4 + q];
+                        wxx = fma(tq * ax, ax, wxx);
+                        wxy = fma(tq * ax, ay, wxy);
+                        wyx = fma(tq * ay, ax, wyx);
+                        wyy = fma(tq * ay, ay, wyy);
+                    }
+                    {  // rows 2, 3 (slack 1, signs +1): a_2 - a_3 = 2 on p_y
+                        const double phi = th[2] * th[3] * iDs[1], ds = 1.0 * 1.0 - 1.0 * -1.0;
+                        wyy = fma(phi * ds, ds, wyy);
+                    }
+#pragma unroll
+                    for (int q = 0; q < NB; ++q)
+#pragma unroll
+                        for (int q2 = q + 1; q2 < NB; ++q2) {  // plane rows: slack 2, signs -1
+                            const double phi = th[4 + q] * th[4 + q2] * iDs[2];
+                            const double dx = -1.0 * cr[2 * q] - -1.0 * cr[2 * q2];
+                            const double dy = -1.0 * cr[2 * q + 1] - -1.0 * cr[2 * q2 + 1];
+                            wxx = fma(phi * dx, dx, wxx);
+                            wxy = fma(phi * dx, dy, wxy);
+                            wyx = fma(phi * dy, dx, wyx);
+                            wyy = fma(phi * dy, dy, wyy);
+                        }
+                    double* wk = sW + k * kDsW;
+                    wk[0] = wxx;
+                    wk[1] = wxy;
+                    wk[2] = wyx;
+                    wk[3] = wyy;
+                    wk[4] = wvx;
+                    wk[5] = Q2[3 * NX + 3];
                 } else {
                 // the stage's rows and 2Q into registers in one batch of LDS reads (read inside the
                 // loops below they were issued one dependent wait at a time)
@@ -1041,11 +1122,12 @@ __global__ __launch_bounds__(64, 1) void mpc_ipm3_kernel(const MpcConst c, const
             auto stage = [&](auto tau_c, int kk, const double* av, auto pf) __attribute__((always_inline)) {
                 constexpr int tau = decltype(tau_c)::value;
                 const double* Ak = sA + kk * NX * NX;
-                const double* Wk = sW + kk * NX * NX;
-                double wk[PA];
-                if constexpr (kPf) {
+                const double* Wk = sW + kk * (DS ? kDsW : NX * NX);
+                constexpr int PW = DS ? kDsW : PA;
+                double wk[PW];
+                if constexpr (kPf || DS) {
 #pragma unroll
-                    for (int i = 0; i < PA; ++i) wk[i] = Wk[i];
+                    for (int i = 0; i < PW; ++i) wk[i] = Wk[i];
                 }
                 pf();
                 __builtin_amdgcn_sched_barrier(0);
@@ -1072,7 +1154,12 @@ __global__ __launch_bounds__(64, 1) void mpc_ipm3_kernel(const MpcConst c, const
                 static_for<0, NXP>([&](auto s_c) __attribute__((always_inline)) {
                     constexpr int s = decltype(s_c)::value;
                     double y = 0.0;
-                    if constexpr (s < NX) {
+                    if constexpr (DS && s < NX) {  // W_k's nonzero entries (kDsW order), the dense chain's terms
+                        if constexpr (s == 0) y = fma(wk[1], g[1], fma(wk[0], g[0], 0.0));
+                        else if constexpr (s == 1) y = fma(wk[3], g[1], fma(wk[2], g[0], 0.0));
+                        else y = fma(wk[s + 2], g[s], 0.0);
+                        gf[s] = g[s];
+                    } else if constexpr (s < NX) {
 #pragma unroll
                         for (int u = 0; u < NX; ++u) y = fma(W_(s * NX + u), g[u], y);
                         gf[s] = g[s];
@@ -1332,6 +1419,14 @@ __global__ __launch_bounds__(64, 1) void mpc_ipm3_kernel(const MpcConst c, const
                             ybv[7] = fma(v, cr[4 + 2 * (r - 4)], ybv[7]);
                             ybv[8] = fma(v, cr[5 + 2 * (r - 4)], ybv[8]);
                         }
+                    } else if constexpr (DS) {  // -v_x, v_x, p_y, -p_y, planes on (p_x, p_y)
+                        if (r < 2) ybv[2] = fma(v, r == 0 ? -1.0 : 1.0, ybv[2]);
+                        else if (r < 4) ybv[1] = fma(v, r == 2 ? 1.0 : -1.0, ybv[1]);
+                        else {
+                            const double* cr = sC + k * CWD + 2 * (r - 4);
+                            ybv[0] = fma(v, cr[0], ybv[0]);
+                            ybv[1] = fma(v, cr[1], ybv[1]);
+                        }
                     } else {
 #pragma unroll
                         for (int s = 0; s < NX; ++s) ybv[s] = fma(v, sC[(k * MC + r) * NX + s], ybv[s]);
@@ -1549,27 +1644,35 @@ __global__ __launch_bounds__(64, 1) void mpc_ipm3_kernel(const MpcConst c, const
 #undef ACT
 }
 
-template <int T, int NX, int NU, int NB, bool LS>
+template <int T, int NX, int NU, int NB, bool LS, bool DS>
 static hipError_t launch3(const MpcConst& c, const MpcPtrs& p, int batch, hipStream_t s) {
-    const size_t lds = sizeof(double) * (size_t)lds3_layout<T, NX, NU, NB, LS>(c.N).total;
-    hipError_t e = hipFuncSetAttribute((const void*)mpc_ipm3_kernel<T, NX, NU, NB, LS>,
+    const size_t lds = sizeof(double) * (size_t)lds3_layout<T, NX, NU, NB, LS, DS>(c.N).total;
+    hipError_t e = hipFuncSetAttribute((const void*)mpc_ipm3_kernel<T, NX, NU, NB, LS, DS>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL((mpc_ipm3_kernel<T, NX, NU, NB, LS>), dim3(batch), dim3(64), lds, s, c, p);
+    hipLaunchKernelGGL((mpc_ipm3_kernel<T, NX, NU, NB, LS, DS>), dim3(batch), dim3(64), lds, s, c, p);
     return hipGetLastError();
 }
 
-template <int NX, int NU, int NB, bool LS = false>
+template <int NX, int NU, int NB, bool LS = false, bool DS = false>
 static hipError_t launch3_t(const MpcConst& c, const MpcPtrs& p, int batch, hipStream_t s) {
     switch (c.npad / 16) {
-        case 1: return launch3<1, NX, NU, NB, LS>(c, p, batch, s);
-        case 2: return launch3<2, NX, NU, NB, LS>(c, p, batch, s);
-        case 3: return launch3<3, NX, NU, NB, LS>(c, p, batch, s);
-        default: return launch3<4, NX, NU, NB, LS>(c, p, batch, s);
+        case 1: return launch3<1, NX, NU, NB, LS, DS>(c, p, batch, s);
+        case 2: return launch3<2, NX, NU, NB, LS, DS>(c, p, batch, s);
+        case 3: return launch3<3, NX, NU, NB, LS, DS>(c, p, batch, s);
+        default: return launch3<4, NX, NU, NB, LS, DS>(c, p, batch, s);
     }
 }
 
-// This file is compiled once per instantiation set (CMPC_V3_SET = 1, 2, 3; see the Makefile) so
+// Q diagonal (the DS images keep only W_k's diagonal outside the (p_x, p_y) block)
+static bool q_diagonal(const MpcConst& c) {
+    for (int s = 0; s < c.nx; ++s)
+        for (int u = 0; u < c.nx; ++u)
+            if (s != u && c.Q[s * c.nx + u] != 0.0) return false;
+    return true;
+}
+
+// This file is compiled once per instantiation set (CMPC_V3_SET = 1 .. 5; see the Makefile) so
 // the instantiations build in parallel.  Set 1 also holds the dispatcher.
 #ifndef CMPC_V3_SET
 #define CMPC_V3_SET 1
@@ -1584,6 +1687,12 @@ static hipError_t launch3_t(const MpcConst& c, const MpcPtrs& p, int batch, hipS
     if (c.lpv && c.nx == 9 && c.nu == 2 && nb == NB_ && !p.fuse.on) {       \
         *err = launch3_t<9, 2, NB_, true>(c, p, batch, s);                  \
         return true;                                                        \
+    }
+// the fused double-integrator round with a diagonal Q (DS images; the dense form gives the same bits)
+#define CASE_DS(NB_)                                                                   \
+    if (p.fuse.on && c.nx == 4 && c.nu == 2 && nb == NB_ && q_diagonal(c)) {           \
+        *err = launch3_t<4, 2, NB_, false, true>(c, p, batch, s);                      \
+        return true;                                                                   \
     }
 #if CMPC_V3_SET == 1
 // host: the LDS image of the instantiation mpc3_try_launch picks (the same coverage rules)
@@ -1623,6 +1732,7 @@ size_t mpc3_lds_bytes(const MpcConst& c) {
 }
 
 bool mpc3_try_set2(const MpcConst& c, const MpcPtrs& p, int batch, hipStream_t s, hipError_t* err, int nb);
+bool mpc3_try_set5(const MpcConst& c, const MpcPtrs& p, int batch, hipStream_t s, hipError_t* err, int nb);
 bool mpc3_try_set3(const MpcConst& c, const MpcPtrs& p, int batch, hipStream_t s, hipError_t* err, int nb);
 bool mpc3_try_set4(const MpcConst& c, const MpcPtrs& p, int batch, hipStream_t s, hipError_t* err, int nb);
 
@@ -1634,6 +1744,7 @@ bool mpc3_try_launch(const MpcConst& c, const MpcPtrs& p, int batch, hipStream_t
     for (int r = 0; r < c.mc; ++r)
         if (c.row_slack[r] != slk(r) || c.row_sign[r] != (int)sgn(r)) return false;
     const int nb = c.mc - 4;
+    if (mpc3_try_set5(c, p, batch, s, err, nb)) return true;
     CASE(4, 2, 2)
     CASE(4, 2, 1)
     CASE(4, 2, 0)
@@ -1655,6 +1766,13 @@ bool mpc3_try_set3(const MpcConst& c, const MpcPtrs& p, int batch, hipStream_t s
     CASE(6, 3, 2)
     return false;
 }
+#elif CMPC_V3_SET == 5
+bool mpc3_try_set5(const MpcConst& c, const MpcPtrs& p, int batch, hipStream_t s, hipError_t* err, int nb) {
+    CASE_DS(2)
+    CASE_DS(1)
+    CASE_DS(0)
+    return false;
+}
 #else
 bool mpc3_try_set4(const MpcConst& c, const MpcPtrs& p, int batch, hipStream_t s, hipError_t* err, int nb) {
     CASE_LS(3)
@@ -1664,5 +1782,6 @@ bool mpc3_try_set4(const MpcConst& c, const MpcPtrs& p, int batch, hipStream_t s
 #endif
 #undef CASE
 #undef CASE_LS
+#undef CASE_DS
 
 }  // namespace cmpc

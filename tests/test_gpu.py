@@ -12,7 +12,11 @@ pytestmark = pytest.mark.gpu
 
 Z_TOL = 1e-6
 # agents at the rounding floor (status 2 on either side, KKT <= 1e-6 on both) against the C restatement
-FLOOR_ZTOL = 1e-5   # measured 1.4e-6 on the rescue round (tests below)
+# rescue round, agents at the rounding floor on either side (status 2: stopped at merit < 1e3 tol, KKT
+# <= 1e-6 asserted on both sides): z there is fixed only to about cond * KKT, so two builds that round
+# alike to the ulp can land 1e-6 .. 1e-4 apart (measured 1.4e-6, then 4.5e-5 on the same round after a
+# change of fma contraction in the v3 kernel); the solved agents are compared to 1e-6
+FLOOR_ZTOL = 1e-4
 
 
 def _gains():
@@ -212,11 +216,11 @@ def test_rescue_pass_resolves_factorisation_breakdowns(gpu_ctx, finish):
             print(f"round {rnd}: {int(bad.sum())} broken down (status -10), {int(changed.sum())} continued; "
                   f"{int(both.sum())} of {R.B} solved by both, max |dz| {err[both].max():.1e}; at the rounding floor "
                   f"on either side {int(floor.sum())}, max |dz| {err[floor].max() if floor.any() else 0:.1e}, "
-                  f"max C kkt {kc[floor].max() if floor.any() else 0:.1e}; GPU status 2 {int((st1 == 2).sum())}; C "
+                  f"median {np.median(err[floor]) if floor.any() else 0:.1e}, max C kkt {kc[floor].max() if floor.any() else 0:.1e}; GPU status 2 {int((st1 == 2).sum())}; C "
                   f"statuses {dict(zip(*[a.tolist() for a in np.unique(sc, return_counts=True)]))}")
             # every agent is compared: where both sides converge, to 1e-6; where either stops at the
             # rounding floor (status 2: merit below 1e3 tol, KKT <= 1e-6 on both sides), to the floor's
-            # accuracy (measured: 1.4e-6).  Without CMPC_FLAG_FINISH a breakdown already at the floor stays
+            # accuracy (FLOOR_ZTOL).  Without CMPC_FLAG_FINISH a breakdown already at the floor stays
             # there (~10 % of this round on either side); with it they are finished (~5 % left)
             assert np.isin(sc, (1, 2)).all() and (kc <= 1e-6).all(), (np.unique(sc), kc.max())
             assert err[both].max() < 1e-6
