@@ -1,5 +1,7 @@
 """Diagnostic: per-section shader-clock breakdown of the v3 solver kernel.
-Usage: python tools/stamps.py [agents] [N]          cfg3 round-0 problem (double integrator)
+Usage: python tools/stamps.py [agents] [N]          cfg3 round-0 problem (double integrator), solved by
+                                                    the fused round (rows built in the launch: the
+                                                    bench's path); --unfused: build() + solve()
        python tools/stamps.py --lpv [round]         bench.py's lpv_rounds population (nx 9) at that
                                                     round (default 6: the slowest of the line)"""
 import os
@@ -21,6 +23,9 @@ NAMES = {14: "setup", 0: "residual: Q X, C'lam", 1: "residual: 2 adjoints", 2: "
          3: "W_k build", 4: "K: Gamma rec + MFMA", 5: "K: diag adds", 6: "chol: 16x16 factors",
          7: "chol: panel + SYRK", 8: "solve: rho, C'rho", 9: "solve: adjoint", 10: "solve: tri-solves",
          11: "solve: fwd sim", 12: "solve: rows, step", 13: "update"}
+UNFUSED = "--unfused" in sys.argv
+if UNFUSED:
+    sys.argv.remove("--unfused")
 LPV = len(sys.argv) > 1 and sys.argv[1] == "--lpv"
 if LPV:
     import bench
@@ -44,6 +49,8 @@ else:
     sc = S.make_di(n, N, 2, 2)
     R = DIRounds(sc)
     R.build()
+    if not UNFUSED:
+        R.solve = R.build_solve
 st = torch.zeros((n, SLOTS), dtype=torch.int64, device="cuda")
 R.opts = L.opts(stamps=st.data_ptr())
 for _ in range(3):
