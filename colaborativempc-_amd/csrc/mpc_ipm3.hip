@@ -1240,14 +1240,20 @@ __global__ __launch_bounds__(64, 1) void mpc_ipm3_kernel(const MpcConst c, const
 #pragma unroll
             for (int cc = 0; cc < 16; ++cc) rw[cc] = S0[(l & 15) * 17 + cc];
             {
-                const int i = l & 15;
+                // pivot chain: lane j+1's next diagonal entry is its own update fma(-l, l, d) (the
+                // broadcast of its own l is l itself: same bits), so the chain between pivots is
+                // rsq + Newton -> l -> fma -> one broadcast.  l = rw[j] y on every lane: on lane j,
+                // rw[j] is the pivot itself (= djj), above the diagonal the values are never read
+                // (the store below writes zeros there)
+                double dn = 0.0;
                 static_for<0, 16>([&](auto jc) __attribute__((always_inline)) {
                     constexpr int j = decltype(jc)::value;
-                    const double djj = bcast16<j>(rw[j]);
+                    const double djj = bcast16<j>(j == 0 ? rw[0] : dn);
                     if (!(djj > 0.0)) chol_ok = false;
                     const double y = rsqrt_d(djj);
-                    const double lj = (i > j) ? rw[j] * y : ((i == j) ? djj * y : rw[j]);
+                    const double lj = rw[j] * y;
                     rw[j] = lj;
+                    if constexpr (j + 1 < 16) dn = fma(-lj, lj, rw[j + 1]);
                     static_for<j + 1, 16>([&](auto cc) __attribute__((always_inline)) {
                         constexpr int c2 = decltype(cc)::value;
                         rw[c2] = fma(-lj, bcast16<c2>(lj), rw[c2]);
