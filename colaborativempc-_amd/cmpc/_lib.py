@@ -43,6 +43,7 @@ CMPC_FLAG_RICCATI = 16
 CMPC_FLAG_RESCUE = 32   # Riccati continuation of agents whose condensed factorisation broke down
 CMPC_FLAG_FINISH = 64   # ... also of breakdowns already at the rounding floor (status 2)
 CMPC_FLAG_LANE = 128    # lane-per-agent stage-wise kernel, fp64
+CMPC_FLAG_POLISH = 256  # with RESCUE: active-set polish of breakdowns at the rounding floor (OSQP polish=True)
 
 
 class cmpc_opts(ct.Structure):

@@ -67,17 +67,21 @@ def track_of(map_obj):
 
 class PlannerLPVBatch:
     """All agents of one control step in one GPU call (same gains / map / horizon).
-    ``riccati``: force the stage-wise Riccati solver (the default only when N*nu > 64)."""
+    ``riccati``: force the stage-wise Riccati solver (the default only when N*nu > 64);
+    ``polish``: CMPC_FLAG_POLISH (default on, as the reference's OSQP polish=True)."""
 
     def __init__(self, Q, Qs, R, dR, N, dt, map, wq=0, model_param=None, sys_lim=None, ctx=None,
-                 tol=None, max_iter=None, riccati=False):
+                 tol=None, max_iter=None, riccati=False, polish=True):
         self.N, self.dt, self.map = int(N), float(dt), map
         self.ctx = ctx or L.default_context()
         self.prm = lpv_params(Q, Qs, R, dR, dt, wq, model_param, sys_lim)
         self.track, self._track_keep = track_of(map)
         # rescue pass on: an agent whose condensed factorisation breaks down (theta ~ 1e18 on
-        # saturated rows) is re-solved by the Riccati kernel instead of returning its best iterate
-        self.opts = L.opts(tol, max_iter, L.CMPC_FLAG_RICCATI if riccati else L.CMPC_FLAG_RESCUE)
+        # saturated rows) is re-solved by the Riccati kernel instead of returning its best iterate;
+        # polish on (OSQP's polish=True, LPV_Planner.py:233): a breakdown at the rounding floor has its
+        # active set solved exactly
+        self.opts = L.opts(tol, max_iter, L.CMPC_FLAG_RICCATI if riccati else
+                           L.CMPC_FLAG_RESCUE | (L.CMPC_FLAG_POLISH if polish else 0))
 
     def solve(self, x0, x_last, u_last, u_old, x_agents, pose):
         """x0 (B,9); x_last (B,N or N+1,9); u_last (B,N,2); u_old (B,2);

@@ -135,7 +135,7 @@ def osqp_solve_qp_batch(qps, ctx=None, tol=None, max_iter=None, structured=True)
         batch = St.stack([recs[i] for i in idx])
         # CMPC_FLAG_RESCUE, as PlannerLPV / PlannerLPVBatch: a condensed factorisation breakdown
         # continues on the stage-wise kernel instead of returning CMPC_UNSOLVED (OSQP's -10)
-        z, kkt, it, st = solve_mpc(batch, ctx, tol=tol, max_iter=max_iter, rescue=True)
+        z, kkt, it, st = solve_mpc(batch, ctx, tol=tol, max_iter=max_iter, rescue=True, polish=True)
         for a, i in enumerate(idx):
             P, q, G, h, A, b = qps[i][:6]
             x = z[a]

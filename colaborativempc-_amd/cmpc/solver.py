@@ -51,10 +51,10 @@ def check_shapes(p, batch):
 FP32_TOL = 1e-6   # default tolerance of the fp32 path (BASELINE cfg5; lane kernel, mixed precision)
 
 
-def _flags(fp32=False, riccati=False, generic=False, rescue=False, lane=False):
+def _flags(fp32=False, riccati=False, generic=False, rescue=False, lane=False, polish=False):
     return (L.CMPC_FLAG_FP32 if fp32 else 0) | (L.CMPC_FLAG_RICCATI if riccati else 0) | \
         (L.CMPC_FLAG_GENERIC if generic else 0) | (L.CMPC_FLAG_RESCUE if rescue else 0) | \
-        (L.CMPC_FLAG_LANE if lane else 0)
+        (L.CMPC_FLAG_LANE if lane else 0) | (L.CMPC_FLAG_POLISH if polish else 0)
 
 
 def plan(shared, batch=1, fp32=False, riccati=False, generic=False, lane=False):
@@ -75,7 +75,7 @@ def plan(shared, batch=1, fp32=False, riccati=False, generic=False, lane=False):
 
 
 def solve_mpc(p, ctx=None, tol=None, max_iter=None, fp32=False, riccati=False, generic=False, rescue=False,
-              stamps=None, lane=False):
+              stamps=None, lane=False, polish=False):
     """Solve a batch of structured agent-QPs on the GPU (host arrays in/out).
     ``fp32``: the fp32 path (BASELINE cfg5): fp32 Riccati factorisation and Newton recursions with
     fp64 iterates — the Riccati kernel's fp32 mode where it is instantiated (nx, nu, mc = 6, 3, 6),
@@ -86,6 +86,8 @@ def solve_mpc(p, ctx=None, tol=None, max_iter=None, fp32=False, riccati=False, g
     ``generic``: force the runtime-dimension condensed kernel;
     ``rescue``: CMPC_FLAG_RESCUE (a condensed solve whose factorisation breaks down continues on
     the stage-wise Riccati kernel; PlannerLPV's default);
+    ``polish``: CMPC_FLAG_POLISH with ``rescue`` (OSQP's polish=True for a breakdown at the rounding
+    floor: the active set taken as exact, the equality-constrained QP solved; PlannerLPV's default);
     ``stamps``: optional device address of a batch x 16 uint64 buffer (per-section clock counts).
 
     Returns (z (B,nz), kkt (B,), iters (B,), status (B,))."""
@@ -100,7 +102,8 @@ def solve_mpc(p, ctx=None, tol=None, max_iter=None, fp32=False, riccati=False, g
     iters = np.zeros(batch, np.int32)
     status = np.zeros(batch, np.int32)
     out = L.cmpc_mpc_out(L.dptr(z), L.dptr(kkt), L.iptr(iters), L.iptr(status))
-    o = L.opts(tol or (FP32_TOL if fp32 else None), max_iter, _flags(fp32, riccati, generic, rescue, lane), stamps)
+    o = L.opts(tol or (FP32_TOL if fp32 else None), max_iter, _flags(fp32, riccati, generic, rescue, lane, polish),
+               stamps)
     ctx.check(ctx.lib.cmpc_solve_mpc_batch(ctx.h, ct.byref(_dims(p, batch)), ct.byref(w), ct.byref(data),
                                            ct.byref(out), ct.byref(o)))
     del keep, arrs

@@ -29,6 +29,7 @@ struct MpcConst {
     int lane;     // lane-per-agent kernel (mpc_lane.hip): 1 fp64 (CMPC_FLAG_LANE), 2 mixed fp32 (CMPC_FLAG_FP32 | LANE,
                   // or CMPC_FLAG_FP32 on dimensions without an fp32 Riccati instantiation)
     int f32;      // 1: CMPC_FLAG_FP32 on the stage-wise Riccati kernel (Cfg::F32; riccati = 1 as well)
+    int polish;   // 1: CMPC_FLAG_POLISH (with rescue): active-set polish of breakdowns at the rounding floor
     unsigned long long ws_stride;  // doubles of MpcPtrs::ws per agent (set by mpc_launch; 0: no scratch)
     double tol;
     double qs_max;  // max(1, 2*max(Qs)) — slack residual scale
@@ -143,6 +144,9 @@ __host__ __device__ inline bool hand_over(int stop, double best_m, const MpcCons
     return stop == kStopBreakdown && (c.finish || !(best_m < 1e3 * c.tol));
 }
 
+// Active-set polish (mpc_polish.hip): agents whose rescue image carries flag 2.
+size_t mpc_polish_lds_bytes(const MpcConst& c);
+hipError_t mpc_polish_launch(const MpcConst& c, const MpcPtrs& p, int batch, hipStream_t s);
 // Stage-wise Riccati kernel (mpc_riccati.hip): any horizon whose per-agent rows fit LDS.
 size_t mpc_riccati_lds_bytes(const MpcConst& c);
 bool mpc_riccati_f32_supported(const MpcConst& c);  // Cfg::F32 instantiations (BASELINE cfg5 dimensions)

@@ -632,6 +632,19 @@ __global__ __launch_bounds__(kWave) void mpc_ipm_kernel(const MpcConst c, const 
     if (it > c.max_iter) it = c.max_iter;
     bar();
     int status = CMPC_SOLVED;
+    // polish (CMPC_FLAG_POLISH): a stall or max-iteration exit at the rounding floor leaves its last iterate
+    // in the rescue image too (a breakdown wrote it above)
+    if (c.polish && P.ws && stop != kStopConverged && stop != kStopBreakdown && stop != kStopNonFinite &&
+        best_m < 1e3 * c.tol) {
+        double* hd = P.ws + (size_t)b * c.ws_stride;
+        const size_t ht = hand_t(c);
+        for (int i = l; i < n; i += kWave) hd[2 + i] = U[i];
+        for (int i = l; i < N * ns; i += kWave) hd[2 + n + i] = sig[i];
+        for (int r = l; r < m; r += kWave) {
+            hd[ht + r] = t[r];
+            hd[ht + m + r] = lam[r];
+        }
+    }
     if (stop != kStopConverged) {
         if (best_it > 0) {  // restore the best iterate
             for (int i = l; i < n; i += kWave) U[i] = bU[i];
@@ -661,7 +674,14 @@ __global__ __launch_bounds__(kWave) void mpc_ipm_kernel(const MpcConst c, const 
         if (P.iters) P.iters[b] = it;
         if (P.status) P.status[b] = status;
         // rescue hand-over flag: set only by a breakdown (the iterate was written there)
-        if (c.rescue && P.ws) P.ws[(size_t)b * c.ws_stride] = hand_over(stop, best_m, c) ? 1.0 : 0.0;
+        if (c.rescue && P.ws) {  // rescue image flag: 1 handed over (a breakdown), 2 polish (a
+            // breakdown at the rounding floor with CMPC_FLAG_POLISH; slot 1 then holds its best merit)
+            double* hd = P.ws + (size_t)b * c.ws_stride;
+            const bool ho = hand_over(stop, best_m, c);
+            const bool pol = !ho && c.polish && stop != kStopConverged && stop != kStopNonFinite && best_m < 1e3 * c.tol;
+            hd[0] = ho ? 1.0 : (pol ? 2.0 : 0.0);
+            if (pol) hd[1] = best_m;
+        }
     }
 }
 
@@ -743,6 +763,8 @@ int mpc_prepare(const cmpc_mpc_dims* d, const cmpc_mpc_weights* wt, const cmpc_o
                  mpc_riccati_lds_bytes(*c) <= kMaxLdsBytes)
                     ? 1 : 0;
     c->finish = (c->rescue && (o->flags & CMPC_FLAG_FINISH)) ? 1 : 0;
+    c->polish = 0;
+    c->polish = (c->rescue && (o->flags & CMPC_FLAG_POLISH) && mpc_polish_lds_bytes(*c) <= kMaxLdsBytes) ? 1 : 0;
     for (int i = 0; i < d->nu; ++i) {
         c->u_ub[i] = wt->u_ub[i];
         c->u_lb[i] = wt->u_lb[i];
@@ -791,7 +813,11 @@ hipError_t mpc_launch(const MpcConst& c_in, const MpcPtrs& p, int batch, hipStre
     MpcConst cr = c;
     cr.riccati = 1;
     if ((e = mpc_riccati_launch(cr, p, batch, s)) != hipSuccess) return e;
-    return mpc_riccati_launch(cr, p, batch, s);
+    if ((e = mpc_riccati_launch(cr, p, batch, s)) != hipSuccess) return e;
+    // polish (CMPC_FLAG_POLISH): the breakdowns at the rounding floor (rescue image flag 2); the fused
+    // double-integrator round keeps its rows in LDS only, so it has none to polish against
+    if (!c.polish || p.fuse.on) return hipSuccess;
+    return mpc_polish_launch(c, p, batch, s);
 }
 
 // ---- f64 MFMA fragment-map self test: D(16x16) = A(16x4) * B(4x16) ----

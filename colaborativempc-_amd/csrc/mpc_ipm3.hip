@@ -642,6 +642,29 @@ __global__ __launch_bounds__(64, 1) void mpc_ipm3_kernel(const MpcConst c, const
         return lo ? h : wi;
     };
     double sg[NS] = {0.0, 0.0, 0.0};
+    // the rescue image (hand_doubles, internal.h): [flag, -, U, sigma, t, lambda] in the oracle's row order
+    auto write_image = [&]() __attribute__((always_inline)) {
+        double* hd = P.ws + (size_t)b * c.ws_stride;
+        const int m = c.m, ht = (int)hand_t(c);
+        for (int i = l; i < n; i += 64) hd[2 + i] = U[i];
+        if (own) {
+            if (lo) {
+#pragma unroll
+                for (int j = 0; j < NS; ++j) hd[2 + n + k * NS + j] = sg[j];
+#pragma unroll
+                for (int r = 0; r < MC; ++r) {
+                    hd[ht + k * MC + r] = t[r];
+                    hd[ht + m + k * MC + r] = lam[r];
+                }
+            } else {
+#pragma unroll
+                for (int r = 0; r < NI; ++r) {  // input rows of u_k: ms + (k nu + i) 2 + (lb ? 1 : 0)
+                    hd[ht + ms + k * NI + r] = t[r];
+                    hd[ht + m + ms + k * NI + r] = lam[r];
+                }
+            }
+        }
+    };
     wsync();
     if (own) {
 #pragma unroll
@@ -1323,27 +1346,8 @@ __global__ __launch_bounds__(64, 1) void mpc_ipm3_kernel(const MpcConst c, const
         if (!chol_ok) {
             stop = kStopBreakdown;
             if (c.rescue && P.ws) {  // hand the iterate to the Riccati rescue (hand_doubles, internal.h)
-                double* hd = P.ws + (size_t)b * c.ws_stride;
-                const int m = c.m, ht = (int)hand_t(c);
-                if (l == 0) hd[1] = it - 1;
-                for (int i = l; i < n; i += 64) hd[2 + i] = U[i];
-                if (own) {
-                    if (lo) {
-#pragma unroll
-                        for (int j = 0; j < NS; ++j) hd[2 + n + k * NS + j] = sg[j];
-#pragma unroll
-                        for (int r = 0; r < MC; ++r) {
-                            hd[ht + k * MC + r] = t[r];
-                            hd[ht + m + k * MC + r] = lam[r];
-                        }
-                    } else {
-#pragma unroll
-                        for (int r = 0; r < NI; ++r) {  // input rows of u_k: ms + (k nu + i) 2 + (lb ? 1 : 0)
-                            hd[ht + ms + k * NI + r] = t[r];
-                            hd[ht + m + ms + k * NI + r] = lam[r];
-                        }
-                    }
-                }
+                write_image();
+                if (l == 0) P.ws[(size_t)b * c.ws_stride + 1] = it - 1;
             }
             break;
         }
@@ -1603,6 +1607,11 @@ __global__ __launch_bounds__(64, 1) void mpc_ipm3_kernel(const MpcConst c, const
     if (it > c.max_iter) it = c.max_iter;
     wsync();
     int status = CMPC_SOLVED;
+    // polish (CMPC_FLAG_POLISH): a stall or max-iteration exit at the rounding floor leaves its last iterate
+    // too (a breakdown wrote it above)
+    if (c.polish && P.ws && stop != kStopConverged && stop != kStopBreakdown && stop != kStopNonFinite &&
+        best_m < 1e3 * c.tol)
+        write_image();
     if (stop != kStopConverged) {
         if (best_it > 0) {  // restore the best iterate
             for (int i = l; i < NP; i += 64) U[i] = bU[i];
@@ -1638,8 +1647,14 @@ __global__ __launch_bounds__(64, 1) void mpc_ipm3_kernel(const MpcConst c, const
         if (P.kkt) P.kkt[b] = kkt;
         if (P.iters) P.iters[b] = it;
         if (P.status) P.status[b] = status;
-        // rescue hand-over flag: set only by a breakdown (the iterate was written there)
-        if (c.rescue && P.ws) P.ws[(size_t)b * c.ws_stride] = hand_over(stop, best_m, c) ? 1.0 : 0.0;
+        if (c.rescue && P.ws) {  // rescue image flag: 1 handed over (a breakdown), 2 polish (a
+            // breakdown at the rounding floor with CMPC_FLAG_POLISH; slot 1 then holds its best merit)
+            double* hd = P.ws + (size_t)b * c.ws_stride;
+            const bool ho = hand_over(stop, best_m, c);
+            const bool pol = !ho && c.polish && stop != kStopConverged && stop != kStopNonFinite && best_m < 1e3 * c.tol;
+            hd[0] = ho ? 1.0 : (pol ? 2.0 : 0.0);
+            if (pol) hd[1] = best_m;
+        }
         if (stamp) {
             unsigned long long* st = P.stamps + (size_t)b * kStampSlots;
             for (int i = 0; i < kStampSlots - 1; ++i) st[i] = tsum[i];

@@ -1,0 +1,666 @@
+// Active-set polish of condensed solves that stop at the rounding floor (CMPC_FLAG_POLISH).
+//
+// The reference solves every agent-QP with OSQP and `polish=True` (LPV_Planner.py:233): after the
+// ADMM iterations, OSQP guesses the active set from the multipliers, solves the equality-
+// constrained QP on it (a reduced KKT system) and keeps that point when its residuals are lower.
+// This is the same step for the interior-point iterate.  A condensed kernel (mpc_ipm3.hip,
+// mpc_ipm.hip) whose Newton matrix breaks down at the rounding floor (theta = lambda / t ~ 1e18 on
+// the active rows: the merit is below 1e3 tol but not below tol, status 2) leaves its iterate in
+// the rescue image (hand_doubles, internal.h) with flag 2 and its best merit in slot 1.  This
+// kernel — one 256-thread workgroup per agent, every other workgroup returns at once — takes
+// A = {r : lambda_r > t_r} as exact and solves
+//     min f(U) + sum Qs sigma^2   s.t.   row_r(U, sigma) = w_r   (r in A)
+// by Newton steps on its linear KKT system, in the range-space form:
+//     H  = the condensed Hessian of f alone (2Q stage weights, 2R, 2dR; no theta: well conditioned),
+//          H = L L' (LDS);
+//     Y  = L^-1 G_A'  (G_A: the active rows as functions of U, c_r' Gamma_{k+1} or +-e_i, formed by
+//          one adjoint recursion per row, psi_{j} = A_j' psi_{j+1}, g_j = B_j' psi_{j+1});
+//     S  = Y'Y + E    (E: the slack coupling sign_r sign_r' / 2Qs_j within a slack group), S = M M';
+//     z  = L^-1 rU,  S dlam = rA' - Y'z,  dU = -L^-T (z + Y dlam),
+//     dsig = -(rsig + sign' dlam) / 2Qs,   rA' = rA - sign rsig / 2Qs.
+// The polished point (t = 0 and lambda = max(lambda_A, 0) on A; t = max(w - row, 0) and lambda = 0
+// elsewhere) replaces the returned solution when its merit max(res, 1e4 mu) is below the best
+// merit the interior-point method reached — status 1 when below tol.  A second pass drops rows
+// with a negative multiplier and adds violated ones (kPolishPasses).  oracle/cmpc_oracle.c
+// restates it (polish_one) and the GPU tests compare the two.
+#include "internal.h"
+#include "wave_ops.h"
+
+namespace cmpc {
+namespace {
+
+constexpr int kPT = 256;           // threads per workgroup (four waves)
+constexpr int kPolishMaxActive = 96;
+constexpr int kPolishSteps = 3;    // Newton steps on the (linear) KKT system: one solve + two refinements
+constexpr int kPolishPasses = 2;
+
+struct PolLayout {
+    int cst, Lh, Y, S, G0, G1, U, sig, Uc, sc, Ub, sb, X, ybar, lamh, w, lamp, tp, rp, rd, gU, rsig, zv, gz, lA,
+        rA, dl, red, in, Ar;
+    int amax, total;
+};
+
+__host__ __device__ inline PolLayout pol_layout_for(const MpcConst& c, int amax) {
+    PolLayout L{};
+    int o = 0;
+    auto take = [&](int cnt) {
+        const int at = o;
+        o += (cnt + 1) & ~1;  // 16-byte alignment
+        return at;
+    };
+    const int n = c.n, nx = c.nx, N = c.N, ns = c.ns, m = c.m;
+    L.amax = amax;
+    L.cst = take(mpc_const_used_doubles(c));
+    L.Lh = take(n * n);
+    L.Y = take(amax * n > nx * n ? amax * n : nx * n);  // also 2Q Gamma while H is built
+    L.S = take(amax * (amax + 1) / 2);
+    L.G0 = take(nx * n);
+    L.G1 = take(nx * n);
+    L.U = take(n);
+    L.sig = take(N * ns);
+    L.Uc = take(n);
+    L.sc = take(N * ns);
+    L.Ub = take(n);
+    L.sb = take(N * ns);
+    L.X = take((N + 1) * nx);
+    L.ybar = take((N + 1) * nx);
+    L.lamh = take(m);
+    L.w = take(m);
+    L.lamp = take(m);
+    L.tp = take(m);
+    L.rp = take(m);
+    L.rd = take(n);
+    L.gU = take(n);
+    L.rsig = take(N * ns);
+    L.zv = take(n);
+    L.gz = take(n);
+    L.lA = take(amax);
+    L.rA = take(amax);
+    L.dl = take(amax);
+    L.red = take(16);
+    L.in = take((m + 1) / 2);      // int flags
+    L.Ar = take((amax + 1) / 2);   // int row indices
+    L.total = o;
+    return L;
+}
+
+__host__ __device__ inline PolLayout pol_layout(const MpcConst& c) {
+    int amax = c.m < kPolishMaxActive ? c.m : kPolishMaxActive;
+    PolLayout L = pol_layout_for(c, amax);
+    while (amax > 8 && (size_t)L.total * sizeof(double) + 1024 > kMaxLdsBytes) {  // 1 KB: static LDS
+        amax -= 8;
+        L = pol_layout_for(c, amax);
+    }
+    return L;
+}
+
+// NaN-propagating block reductions over the four waves (scratch: 4 doubles)
+__device__ double block_nmax(double v, double* red) {
+    v = wave_max(v);
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+    __syncthreads();
+    return nmax(nmax(red[0], red[1]), nmax(red[2], red[3]));
+}
+__device__ double block_sum(double v, double* red) {
+    v = wave_sum(v);
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) red[4 + (threadIdx.x >> 6)] = v;
+    __syncthreads();
+    return (red[4] + red[5]) + (red[6] + red[7]);
+}
+
+// in-place Cholesky of an n x n matrix (lower triangle, element (i, j) at M[idx(i, j)]),
+// right-looking, whole workgroup; returns false when a pivot is not positive
+template <class Idx>
+__device__ bool block_chol(double* M, int n, Idx idx, double* red) {
+    const int tid = threadIdx.x;
+    for (int j = 0; j < n; ++j) {
+        const double d = M[idx(j, j)];
+        if (!(d > 0.0)) return false;  // uniform: every thread read the same value
+        if (tid == 0) red[13] = j ? fmin(red[13], d) : d;  // smallest pivot (diagnostics)
+        const double s = sqrt(d);
+        const double inv = 1.0 / s;
+        __syncthreads();
+        if (tid == 0) M[idx(j, j)] = s;
+        for (int i = j + 1 + tid; i < n; i += kPT) M[idx(i, j)] *= inv;
+        __syncthreads();
+        // trailing update of the lower triangle: (i, p), j < p <= i
+        const int rem = n - j - 1;
+        const int cnt = rem * (rem + 1) / 2;
+        for (int e = tid; e < cnt; e += kPT) {
+            // e -> (a, b) with 0 <= b <= a < rem, e = a (a + 1) / 2 + b
+            int a = (int)((sqrt(8.0 * e + 1.0) - 1.0) * 0.5);
+            while (a * (a + 1) / 2 > e) --a;
+            while ((a + 1) * (a + 2) / 2 <= e) ++a;
+            const int b = e - a * (a + 1) / 2;
+            const int i = j + 1 + a, p = j + 1 + b;
+            M[idx(i, p)] -= M[idx(i, j)] * M[idx(p, j)];
+        }
+        __syncthreads();
+    }
+    (void)red;
+    return true;
+}
+
+// forward substitution L x = b in place (x overwrites b), wave 0 only (n <= 128: two rows a lane)
+template <class Idx>
+__device__ void wave_fsub(const double* M, int n, Idx idx, double* x) {
+    const int l = threadIdx.x;
+    for (int p = 0; p < n; ++p) {
+        const double xp = x[p] / M[idx(p, p)];
+        wsync();
+        if (l == 0) x[p] = xp;
+        for (int i = p + 1 + l; i < n; i += kWave) x[i] -= M[idx(i, p)] * xp;
+        wsync();
+    }
+}
+// backward substitution L' x = b in place, wave 0 only
+template <class Idx>
+__device__ void wave_bsub(const double* M, int n, Idx idx, double* x) {
+    const int l = threadIdx.x;
+    for (int p = n - 1; p >= 0; --p) {
+        const double xp = x[p] / M[idx(p, p)];
+        wsync();
+        if (l == 0) x[p] = xp;
+        for (int i = l; i < p; i += kWave) x[i] -= M[idx(p, i)] * xp;
+        wsync();
+    }
+}
+
+struct PolCtx {
+    const MpcConst& c;
+    const PolLayout& L;
+    double* sm;
+    const double* A;
+    const double* B;
+    const double* x0;
+    const double* up;
+    const double* pl;
+    const double* C;
+};
+
+// X = simulation of (x0, U) (wave 0; the other waves wait at the caller's barrier)
+__device__ void pol_fwd(const PolCtx& q, const double* U, double* X) {
+    const MpcConst& c = q.c;
+    const int nx = c.nx, nu = c.nu, N = c.N, l = threadIdx.x;
+    if (l >= kWave) return;
+    if (l < nx) X[l] = q.x0[l];
+    wsync();
+    for (int k = 0; k < N; ++k) {
+        if (l < nx) {
+            const double* Ak = q.A + ((size_t)k * nx + l) * nx;
+            const double* Bk = q.B + ((size_t)k * nx + l) * nu;
+            double v = 0.0;
+            for (int t = 0; t < nx; ++t) v += Ak[t] * X[k * nx + t];
+            for (int i = 0; i < nu; ++i) v += Bk[i] * U[k * nu + i];
+            X[(k + 1) * nx + l] = v;
+        }
+        wsync();
+    }
+}
+
+// out_k = B_k' psi_{k+1}, psi_N = y_N, psi_k = y_k + A_k' psi_{k+1} (wave 0; psi kept in y's slots,
+// y is overwritten)
+__device__ void pol_adjoint(const PolCtx& q, double* y, double* out) {
+    const MpcConst& c = q.c;
+    const int nx = c.nx, nu = c.nu, N = c.N, l = threadIdx.x;
+    if (l >= kWave) return;
+    for (int k = N - 1; k >= 0; --k) {
+        const double* psi = y + (k + 1) * nx;
+        if (l < nu) {
+            const double* Bk = q.B + (size_t)k * nx * nu;
+            double v = 0.0;
+            for (int s = 0; s < nx; ++s) v += Bk[s * nu + l] * psi[s];
+            out[k * nu + l] = v;
+        }
+        if (k > 0 && l < nx) {
+            const double* Ak = q.A + (size_t)k * nx * nx;
+            double v = y[k * nx + l];
+            for (int s = 0; s < nx; ++s) v += Ak[s * nx + l] * psi[s];
+            y[k * nx + l] = v;
+        }
+        wsync();
+    }
+}
+
+__device__ double pol_row(const PolCtx& q, const double* X, const double* U, const double* sg, int r) {
+    const MpcConst& c = q.c;
+    const int nx = c.nx, mc = c.mc, ms = c.ms;
+    if (r < ms) {
+        const int k = r / mc, rr = r - k * mc;
+        const double* cr = q.C + (size_t)r * nx;
+        double v = 0.0;
+        for (int s = 0; s < nx; ++s) v += cr[s] * X[(k + 1) * nx + s];
+        const int j = c.row_slack[rr];
+        if (j >= 0) v += c.row_sign[rr] * sg[k * c.ns + j];
+        return v;
+    }
+    const int qq = r - ms;
+    return (qq & 1) ? -U[qq >> 1] : U[qq >> 1];
+}
+
+// The interior-point residuals at (U, sigma, t, lambda) into rd / rsig / rp (cmpc_oracle.c merit_at);
+// X is re-simulated.  With `full`, returns the merit max(res, 1e4 mu) and *kkt = max(res, mu).
+__device__ double pol_residuals(const PolCtx& q, const double* U, const double* sg, const double* t,
+                                const double* lam, const int* act_w, bool full, double* kkt) {
+    const MpcConst& c = q.c;
+    const PolLayout& L = q.L;
+    double* sm = q.sm;
+    const int nx = c.nx, nu = c.nu, N = c.N, ns = c.ns, mc = c.mc, ms = c.ms, m = c.m, n = c.n;
+    const int tid = threadIdx.x;
+    double *X = sm + L.X, *ybar = sm + L.ybar, *rd = sm + L.rd, *gU = sm + L.gU, *rsig = sm + L.rsig,
+           *rp = sm + L.rp, *red = sm + L.red;
+    pol_fwd(q, U, X);
+    __syncthreads();
+    auto ucost = [&](int k, int i) {
+        double v = 0.0;
+        for (int j = 0; j < nu; ++j) {
+            const double du_k = U[k * nu + j] - (k ? U[(k - 1) * nu + j] : q.up[j]);
+            const double du_n = (k + 1 < N) ? U[(k + 1) * nu + j] - U[k * nu + j] : 0.0;
+            v += 2.0 * c.R[i * nu + j] * U[k * nu + j] + 2.0 * c.dR[i * nu + j] * (du_k - du_n);
+        }
+        return v;
+    };
+    double gscale = 1.0;
+    if (full) {
+        for (int e = tid; e < (N + 1) * nx; e += kPT) {
+            const int k = e / nx, s = e - k * nx;
+            double v = 2.0 * q.pl[e];
+            for (int t2 = 0; t2 < nx; ++t2) v += 2.0 * c.Q[s * nx + t2] * X[k * nx + t2];
+            ybar[e] = v;
+        }
+        __syncthreads();
+        pol_adjoint(q, ybar, gU);
+        __syncthreads();
+        double g_l = 0.0;
+        for (int e = tid; e < n; e += kPT) g_l = nmax(g_l, fabs(gU[e] + ucost(e / nu, e % nu)));
+        gscale = nmax(1.0, block_nmax(g_l, red));
+    }
+    for (int e = tid; e < (N + 1) * nx; e += kPT) {
+        const int k = e / nx, s = e - k * nx;
+        double v = 2.0 * q.pl[e];
+        for (int t2 = 0; t2 < nx; ++t2) v += 2.0 * c.Q[s * nx + t2] * X[k * nx + t2];
+        if (k > 0)
+            for (int r = 0; r < mc; ++r) v += lam[(k - 1) * mc + r] * q.C[((size_t)(k - 1) * mc + r) * nx + s];
+        ybar[e] = v;
+    }
+    __syncthreads();
+    pol_adjoint(q, ybar, rd);
+    __syncthreads();
+    for (int e = tid; e < n; e += kPT) {
+        const int k = e / nu, i = e - k * nu, r = ms + 2 * e;
+        rd[e] += ucost(k, i) + lam[r] - lam[r + 1];
+    }
+    for (int e = tid; e < N * ns; e += kPT) {
+        const int k = e / ns, j = e - k * ns;
+        double v = 2.0 * c.Qs[j] * sg[e];
+        for (int r = 0; r < mc; ++r)
+            if (c.row_slack[r] == j) v += c.row_sign[r] * lam[k * mc + r];
+        rsig[e] = v;
+    }
+    double nrp = 0.0, mu = 0.0, sp = 1.0, cnt = 0.0;
+    for (int r = tid; r < m; r += kPT) {
+        if (!(act_w[r] & 1)) { rp[r] = 0.0; continue; }
+        const double w = sm[L.w + r];
+        rp[r] = pol_row(q, X, U, sg, r) + t[r] - w;
+        nrp = nmax(nrp, fabs(rp[r]));
+        mu += t[r] * lam[r];
+        sp = fmax(sp, fabs(w));
+        cnt += 1.0;
+    }
+    __syncthreads();
+    if (!full) return 0.0;
+    double nrd = 0.0, nrs = 0.0;
+    for (int e = tid; e < n; e += kPT) nrd = nmax(nrd, fabs(rd[e]));
+    for (int e = tid; e < N * ns; e += kPT) nrs = nmax(nrs, fabs(rsig[e]));
+    nrd = block_nmax(nrd, red);
+    nrs = block_nmax(nrs, red);
+    nrp = block_nmax(nrp, red);
+    const double scale_p = block_nmax(sp, red);
+    const double mact = block_sum(cnt, red);
+    mu = block_sum(mu, red);
+    mu = mact > 0.0 ? mu / mact : 0.0;
+    const double res = nmax(nmax(nrd / gscale, nrs / c.qs_max), nrp / scale_p);
+    if (tid == 0) {  // diagnostics (the stamps of mpc_polish_kernel)
+        red[8] = nrd / gscale;
+        red[9] = nrs / c.qs_max;
+        red[10] = nrp / scale_p;
+    }
+    *kkt = nmax(res, mu);
+    return nmax(res, 1e4 * mu);
+}
+
+__global__ __launch_bounds__(kPT) void mpc_polish_kernel(const MpcConst c_arg, const MpcPtrs P) {
+    extern __shared__ __attribute__((aligned(16))) double sm[];
+    const int b = blockIdx.x;
+    double* hd = P.ws + (size_t)b * c_arg.ws_stride;
+    if (hd[0] != 2.0) return;  // not a breakdown at the rounding floor
+    const int tid = threadIdx.x;
+    const PolLayout L = pol_layout(c_arg);
+    {
+        const unsigned long long* src = reinterpret_cast<const unsigned long long*>(&c_arg);
+        unsigned long long* dst = reinterpret_cast<unsigned long long*>(sm + L.cst);
+        for (int i = tid; i < mpc_const_used_doubles(c_arg); i += kPT) dst[i] = src[i];
+    }
+    __syncthreads();
+    const MpcConst& c = *reinterpret_cast<const MpcConst*>(sm + L.cst);
+    const int nx = c.nx, nu = c.nu, N = c.N, ns = c.ns, mc = c.mc, ms = c.ms, m = c.m, n = c.n;
+    const int amax = L.amax;
+    const PolCtx q{c, L, sm, P.A + (size_t)b * N * nx * nx, P.B + (size_t)b * N * nx * nu, P.x0 + (size_t)b * nx,
+                   P.up + (size_t)b * nu, P.p + (size_t)b * (N + 1) * nx, P.C + (size_t)b * N * mc * nx};
+    const double* hC = P.h + (size_t)b * N * mc;
+    const double best_m = hd[1];
+    const int ht = (int)hand_t(c);
+    double *Lh = sm + L.Lh, *Y = sm + L.Y, *Sm = sm + L.S, *U = sm + L.U, *sig = sm + L.sig, *Uc = sm + L.Uc,
+           *sc = sm + L.sc, *Ub = sm + L.Ub, *sb = sm + L.sb, *lamh = sm + L.lamh, *w = sm + L.w, *lamp = sm + L.lamp,
+           *tp = sm + L.tp, *rp = sm + L.rp, *rd = sm + L.rd, *rsig = sm + L.rsig, *zv = sm + L.zv, *gz = sm + L.gz,
+           *lA = sm + L.lA, *rA = sm + L.rA, *dl = sm + L.dl;
+    int* in = reinterpret_cast<int*>(sm + L.in);
+    int* Ar = reinterpret_cast<int*>(sm + L.Ar);
+    // act flags: kept in the low bit of in[] (bit 1: in A)
+    for (int r = tid; r < m; r += kPT) {
+        double wr;
+        if (r < ms) {
+            wr = hC[r];
+        } else {
+            const int qq = r - ms, i = (qq >> 1) % nu;
+            wr = (qq & 1) ? -c.u_lb[i] : c.u_ub[i];
+        }
+        const int act = isfinite(wr) ? 1 : 0;
+        w[r] = act ? wr : 0.0;
+        const double tr = hd[ht + r], lr = hd[ht + m + r];
+        lamh[r] = act ? lr : 0.0;
+        in[r] = act | ((act && lr > tr) ? 2 : 0);
+    }
+    for (int i = tid; i < n; i += kPT) U[i] = hd[2 + i];
+    for (int i = tid; i < N * ns; i += kPT) sig[i] = hd[2 + n + i];
+    for (int i = tid; i < n * n; i += kPT) Lh[i] = 0.0;
+    for (int i = tid; i < nx * n; i += kPT) sm[L.G0 + i] = 0.0;
+    __syncthreads();
+    // ---- H = sum_k Gamma_{k+1}' 2Q Gamma_{k+1} + the 2R / 2dR band (lower triangle), H = L L' ----
+    {
+        double* G = sm + L.G0;
+        double* Gn = sm + L.G1;
+        double* WG = Y;
+        for (int k = 0; k < N; ++k) {
+            const double* Ak = q.A + (size_t)k * nx * nx;
+            const double* Bk = q.B + (size_t)k * nx * nu;
+            const int ncol = (k + 1) * nu;
+            for (int e = tid; e < nx * n; e += kPT) {
+                const int s = e / n, col = e - s * n;
+                double v = 0.0;
+                if (col < ncol) {
+                    for (int t2 = 0; t2 < nx; ++t2) v += Ak[s * nx + t2] * G[t2 * n + col];
+                    if (col >= k * nu) v += Bk[s * nu + col - k * nu];
+                }
+                Gn[e] = v;
+            }
+            __syncthreads();
+            for (int e = tid; e < nx * n; e += kPT) {
+                const int s = e / n, col = e - s * n;
+                double v = 0.0;
+                if (col < ncol)
+                    for (int u = 0; u < nx; ++u) v += 2.0 * c.Q[s * nx + u] * Gn[u * n + col];
+                WG[e] = v;
+            }
+            __syncthreads();
+            for (int e = tid; e < ncol * ncol; e += kPT) {
+                const int c1 = e / ncol, c2 = e - c1 * ncol;
+                if (c2 > c1) continue;
+                double v = 0.0;
+                for (int s = 0; s < nx; ++s) v += Gn[s * n + c1] * WG[s * n + c2];
+                Lh[c1 * n + c2] += v;
+            }
+            __syncthreads();
+            double* tmp = G;
+            G = Gn;
+            Gn = tmp;
+        }
+        for (int ci = tid; ci < n; ci += kPT) {
+            const int k = ci / nu, i = ci - k * nu;
+            for (int j = 0; j < nu; ++j) {
+                const int cj = k * nu + j;
+                const double d = 2.0 * c.R[i * nu + j] + 2.0 * c.dR[i * nu + j] * (k + 1 < N ? 2.0 : 1.0);
+                if (cj <= ci) Lh[ci * n + cj] += d;
+                if (k > 0) Lh[ci * n + (k - 1) * nu + j] += -2.0 * c.dR[i * nu + j];
+            }
+        }
+        __syncthreads();
+    }
+    auto ih = [n](int i, int j) { return i * n + j; };
+    auto is = [](int i, int j) { return i * (i + 1) / 2 + j; };
+    const bool h_ok = block_chol(Lh, n, ih, sm + L.red);
+    __syncthreads();
+    double best = INFINITY, best_kkt = INFINITY;
+    int& nA_s = *reinterpret_cast<int*>(sm + L.red + 12);
+    int passes = 0;
+    if (tid == 0) nA_s = -1;
+    __syncthreads();
+    for (int pass = 0; pass < kPolishPasses && h_ok; ++pass) {
+        passes = pass + 1;
+        // the active list (ascending rows), wave 0 by ballot
+        if (tid < kWave) {
+            int base = 0;
+            for (int r0 = 0; r0 < m; r0 += kWave) {
+                const int r = r0 + tid;
+                const bool f = r < m && (in[r] & 2);
+                const unsigned long long msk = __ballot(f);
+                const int pos = base + __popcll(msk & ((1ull << tid) - 1ull));
+                if (f && pos < amax) Ar[pos] = r;
+                base += __popcll(msk);
+            }
+            if (tid == 0) nA_s = base;
+        }
+        __syncthreads();
+        const int nA = nA_s;
+        if (nA > amax) break;
+        // G_A rows by adjoint recursions (one thread a row), then Y rows = L^-1 g (in place)
+        for (int qa = tid; qa < nA; qa += kPT) {
+            const int r = Ar[qa];
+            double* g = Y + (size_t)qa * n;
+            for (int i = 0; i < n; ++i) g[i] = 0.0;
+            if (r < ms) {
+                const int k = r / mc;
+                double psi[CMPC_MAX_NX], nps[CMPC_MAX_NX];
+                for (int s = 0; s < nx; ++s) psi[s] = q.C[(size_t)r * nx + s];
+                for (int j = k; j >= 0; --j) {
+                    const double* Bj = q.B + (size_t)j * nx * nu;
+                    for (int i = 0; i < nu; ++i) {
+                        double v = 0.0;
+                        for (int s = 0; s < nx; ++s) v += Bj[s * nu + i] * psi[s];
+                        g[j * nu + i] = v;
+                    }
+                    if (j > 0) {
+                        const double* Aj = q.A + (size_t)j * nx * nx;
+                        for (int t2 = 0; t2 < nx; ++t2) {
+                            double v = 0.0;
+                            for (int s = 0; s < nx; ++s) v += Aj[s * nx + t2] * psi[s];
+                            nps[t2] = v;
+                        }
+                        for (int s = 0; s < nx; ++s) psi[s] = nps[s];
+                    }
+                }
+            } else {
+                const int qq = r - ms;
+                g[qq >> 1] = (qq & 1) ? -1.0 : 1.0;
+            }
+            for (int i = 0; i < n; ++i) {
+                double v = g[i];
+                for (int p2 = 0; p2 < i; ++p2) v -= Lh[i * n + p2] * g[p2];
+                g[i] = v / Lh[i * n + i];
+            }
+        }
+        __syncthreads();
+        // S = Y Y' + E (packed lower)
+        for (int e = tid; e < nA * (nA + 1) / 2; e += kPT) {
+            int a = (int)((sqrt(8.0 * e + 1.0) - 1.0) * 0.5);
+            while (a * (a + 1) / 2 > e) --a;
+            while ((a + 1) * (a + 2) / 2 <= e) ++a;
+            const int b2 = e - a * (a + 1) / 2;
+            double v = 0.0;
+            for (int i = 0; i < n; ++i) v += Y[(size_t)a * n + i] * Y[(size_t)b2 * n + i];
+            const int r = Ar[a], r2 = Ar[b2];
+            if (r < ms && r2 < ms && r / mc == r2 / mc) {
+                const int j = c.row_slack[r % mc];
+                if (j >= 0 && c.row_slack[r2 % mc] == j) v += c.row_sign[r % mc] * c.row_sign[r2 % mc] / (2.0 * c.Qs[j]);
+            }
+            Sm[e] = v;
+        }
+        __syncthreads();
+        if (!block_chol(Sm, nA, is, sm + L.red)) break;
+        // Newton steps from (U, sigma, lambda_A)
+        for (int i = tid; i < n; i += kPT) Uc[i] = U[i];
+        for (int i = tid; i < N * ns; i += kPT) sc[i] = sig[i];
+        for (int r = tid; r < m; r += kPT) {
+            lamp[r] = 0.0;
+            tp[r] = 0.0;
+        }
+        for (int qa = tid; qa < nA; qa += kPT) lA[qa] = lamh[Ar[qa]];
+        __syncthreads();
+        for (int step = 0; step < kPolishSteps; ++step) {
+            for (int qa = tid; qa < nA; qa += kPT) lamp[Ar[qa]] = lA[qa];
+            __syncthreads();
+            double kk;
+            pol_residuals(q, Uc, sc, tp, lamp, in, false, &kk);  // t = 0: rp = row - w on A
+            for (int qa = tid; qa < nA; qa += kPT) {
+                const int r = Ar[qa];
+                double ra = rp[r];
+                if (r < ms) {
+                    const int j = c.row_slack[r % mc];
+                    if (j >= 0) ra -= c.row_sign[r % mc] * rsig[(r / mc) * ns + j] / (2.0 * c.Qs[j]);
+                }
+                rA[qa] = ra;
+            }
+            for (int i = tid; i < n; i += kPT) zv[i] = rd[i];
+            __syncthreads();
+            if (tid < kWave) wave_fsub(Lh, n, ih, zv);  // z = L^-1 rU
+            __syncthreads();
+            for (int qa = tid; qa < nA; qa += kPT) {
+                double v = rA[qa];
+                for (int i = 0; i < n; ++i) v -= Y[(size_t)qa * n + i] * zv[i];
+                dl[qa] = v;
+            }
+            __syncthreads();
+            if (tid < kWave) {
+                wave_fsub(Sm, nA, is, dl);
+                wave_bsub(Sm, nA, is, dl);
+            }
+            __syncthreads();
+            for (int i = tid; i < n; i += kPT) {  // z + Y dlam
+                double v = zv[i];
+                for (int qa = 0; qa < nA; ++qa) v += Y[(size_t)qa * n + i] * dl[qa];
+                gz[i] = v;
+            }
+            __syncthreads();
+            if (tid < kWave) wave_bsub(Lh, n, ih, gz);  // H^-1 (rU + G_A' dlam)
+            __syncthreads();
+            for (int i = tid; i < n; i += kPT) Uc[i] -= gz[i];
+            for (int e = tid; e < N * ns; e += kPT) {
+                const int k = e / ns, j = e - k * ns;
+                double v = rsig[e];
+                for (int qa = 0; qa < nA; ++qa) {
+                    const int r = Ar[qa];
+                    if (r < ms && r / mc == k && c.row_slack[r % mc] == j) v += c.row_sign[r % mc] * dl[qa];
+                }
+                sc[e] -= v / (2.0 * c.Qs[j]);
+            }
+            for (int qa = tid; qa < nA; qa += kPT) lA[qa] += dl[qa];
+            __syncthreads();
+        }
+        // the polished point as an interior-point iterate; the next pass's active set
+        pol_fwd(q, Uc, sm + L.X);
+        __syncthreads();
+        int ch = 0;
+        for (int r = tid; r < m; r += kPT) {
+            lamp[r] = 0.0;
+            tp[r] = 1.0;
+            if (!(in[r] & 1) || (in[r] & 2)) continue;
+            const double g = w[r] - pol_row(q, sm + L.X, Uc, sc, r);
+            tp[r] = fmax(g, 0.0);
+            if (g < 0.0) ch = 1;
+        }
+        __syncthreads();  // the active rows' entries below overwrite the defaults above
+        for (int qa = tid; qa < nA; qa += kPT) {
+            lamp[Ar[qa]] = fmax(lA[qa], 0.0);
+            tp[Ar[qa]] = 0.0;
+            if (lA[qa] < 0.0) ch = 1;
+        }
+        __syncthreads();
+        double kk = 0.0;
+        const double mp = pol_residuals(q, Uc, sc, tp, lamp, in, true, &kk);
+        if (mp < best) {
+            best = mp;
+            best_kkt = kk;
+            for (int i = tid; i < n; i += kPT) Ub[i] = Uc[i];
+            for (int i = tid; i < N * ns; i += kPT) sb[i] = sc[i];
+        }
+        const int changed = __syncthreads_or(ch);
+        if (!changed) break;
+        // negative multipliers leave the active set, violated rows join it
+        for (int r = tid; r < m; r += kPT)
+            if ((in[r] & 1) && !(in[r] & 2) && tp[r] == 0.0 && w[r] - pol_row(q, sm + L.X, Uc, sc, r) < 0.0) in[r] |= 2;
+        for (int qa = tid; qa < nA; qa += kPT)
+            if (lA[qa] < 0.0) in[Ar[qa]] &= ~2;
+        __syncthreads();
+    }
+    __syncthreads();
+    // diagnostics (MpcPtrs::stamps, tools/polish_diag.py): [passes run, |A| of the last, polished merit,
+    // the method's best merit, H factored]
+    if (P.stamps && tid == 0) {
+        unsigned long long* st = P.stamps + (size_t)b * kStampSlots;
+        st[0] = (unsigned long long)passes;
+        st[1] = (unsigned long long)nA_s;
+        st[2] = (unsigned long long)__double_as_longlong(best);
+        st[3] = (unsigned long long)__double_as_longlong(best_m);
+        st[4] = h_ok ? 1ull : 0ull;
+        for (int i = 0; i < 3; ++i) st[5 + i] = (unsigned long long)__double_as_longlong(sm[L.red + 8 + i]);
+        st[8] = (unsigned long long)__double_as_longlong(sm[L.red + 13]);
+    }
+    if (!(best < best_m)) {
+        if (tid == 0) hd[0] = 0.0;
+        return;
+    }
+    // ---- output in the reference layout (the condensed kernels' expansion) ----
+    double* X = sm + L.X;
+    pol_fwd(q, Ub, X);
+    __syncthreads();
+    const int nxe = nx + ns;
+    const size_t nz = (size_t)nxe * (N + 1) + 2 * (size_t)n;
+    double* z = P.z + (size_t)b * nz;
+    for (int i = tid; i < (N + 1) * nx; i += kPT) {
+        const int kk = i / nx, s = i - kk * nx;
+        z[(size_t)kk * nxe + s] = X[i];
+    }
+    for (int i = tid; i < (N + 1) * ns; i += kPT) {
+        const int kk = i / ns, j = i - kk * ns;
+        z[(size_t)kk * nxe + nx + j] = kk ? sb[(kk - 1) * ns + j] : 0.0;
+    }
+    for (int i = tid; i < n; i += kPT) {
+        const int kk = i / nu, j = i - kk * nu;
+        z[(size_t)(N + 1) * nxe + i] = Ub[i];
+        z[(size_t)(N + 1) * nxe + n + i] = Ub[i] - (kk ? Ub[(kk - 1) * nu + j] : q.up[j]);
+    }
+    if (tid == 0) {
+        if (P.kkt) P.kkt[b] = best_kkt;
+        if (P.status) P.status[b] = best < c.tol ? CMPC_SOLVED : CMPC_SOLVED_INACCURATE;
+        hd[0] = 0.0;
+    }
+}
+
+}  // namespace
+
+size_t mpc_polish_lds_bytes(const MpcConst& c) { return sizeof(double) * (size_t)pol_layout(c).total; }
+
+hipError_t mpc_polish_launch(const MpcConst& c, const MpcPtrs& p, int batch, hipStream_t s) {
+    if (batch == 0) return hipSuccess;
+    const size_t lds = mpc_polish_lds_bytes(c);
+    if (lds > kMaxLdsBytes) return hipErrorInvalidValue;
+    hipError_t e = hipFuncSetAttribute((const void*)mpc_polish_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       (int)lds);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(mpc_polish_kernel, dim3(batch), dim3(kPT), lds, s, c, p);
+    return hipGetLastError();
+}
+
+}  // namespace cmpc

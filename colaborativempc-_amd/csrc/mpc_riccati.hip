@@ -1683,7 +1683,7 @@ __global__ __launch_bounds__(kWave) void mpc_riccati_kernel(const MpcConst c_arg
     const int b = P.order ? min(max(P.order[blockIdx.x], 0), (int)gridDim.x - 1) : (int)blockIdx.x;
     if (c_arg.rescue) {  // rescue pass: agents handed over at a breakdown, or left CMPC_UNSOLVED, only
         const RGlb g0 = r_glb(c_arg);
-        if (P.ws[(size_t)b * g0.total + g0.hand] == 0.0 && P.status[b] != CMPC_UNSOLVED) return;
+        if (P.ws[(size_t)b * g0.total + g0.hand] != 1.0 && P.status[b] != CMPC_UNSOLVED) return;
     }
     const int l = threadIdx.x;
     const RLds L = r_layout(c_arg);
@@ -1750,7 +1750,7 @@ __global__ __launch_bounds__(kWave) void mpc_riccati_kernel(const MpcConst c_arg
     // (hand_doubles, internal.h), or start cold; the flag is consumed here, so a second rescue
     // pass over an agent this one leaves CMPC_UNSOLVED starts cold
     double* hand = ws + gl.hand;
-    const bool warm = c_arg.rescue && hand[0] != 0.0;
+    const bool warm = c_arg.rescue && hand[0] == 1.0;
     // double-double near the solution: a continued (rescue) solve from the start, a cold one only
     // once the fp64 recursion stops making progress or breaks down (kDdStall)
     bool dd_on = warm;
@@ -2118,6 +2118,23 @@ __global__ __launch_bounds__(kWave) void mpc_riccati_kernel(const MpcConst c_arg
     if (it > c.max_iter) it = c.max_iter;
     wsync();
     int status = CMPC_SOLVED;
+    // polish (CMPC_FLAG_POLISH): a rescue-pass solve that stops at the rounding floor leaves its last
+    // iterate in the rescue image with flag 2 and its best merit (mpc_polish.hip)
+    const bool pol = c_arg.rescue && c.polish && stop != kStopConverged && stop != kStopNonFinite &&
+                     best_m < 1e3 * c.tol;
+    if (pol) {
+        const int ht = (int)hand_t(c);
+        for (int i = l; i < n; i += kWave) hand[2 + i] = U[i];
+        for (int i = l; i < N * ns; i += kWave) hand[2 + n + i] = sig[i];
+        for (int r = l; r < m; r += kWave) {
+            hand[ht + r] = t[r];
+            hand[ht + m + r] = lam[r];
+        }
+        if (l == 0) {
+            hand[0] = 2.0;
+            hand[1] = best_m;
+        }
+    }
     if (stop != kStopConverged) {
         if (best_it > 0) {  // restore the best iterate
             for (int i = l; i < n; i += kWave) U[i] = bU[i];

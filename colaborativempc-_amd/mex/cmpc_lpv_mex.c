@@ -20,7 +20,8 @@
  *      min_vel max_rs max_ls max_ac max_dc (:30-41), dt, wq, Q 9x9, Qs 3x1 (diagonal), R 2x2, dR 2x2
  *      (scripts/config_files/config_LPV.py:6-11), N, track (struct s0, len, curv, half_width: one
  *      entry per PointAndTangent row, track_initialization.py:220-300); optional tol, max_iter,
- *      rescue (default 1: CMPC_FLAG_RESCUE, as PlannerLPV).
+ *      rescue (default 1: CMPC_FLAG_RESCUE, as PlannerLPV), polish (default 1: CMPC_FLAG_POLISH with
+ *      rescue, as PlannerLPV — OSQP's polish=True, LPV_Planner.py:233).
  *   D: struct, MATLAB order (B agents, last dimension): x0 9xB, x_last 9 x rows x B (rows N+1 at the
  *      first step, N afterwards), u_last 2xNxB, u_old 2xB, pose 2x(N+1)xB, x_agents 2 x nb x (N+1) x B
  *      (optional: none = no neighbours).  This is the C ABI's row-major layout read backwards, so
@@ -144,7 +145,9 @@ static void read_params(const mxArray* P, lpv_setup* s) {
     s->track.half_width = mxGetPr(field(T, "half_width", ns, 1));
     s->opts.tol = scalar_or(P, "tol", 0.0);
     s->opts.max_iter = (int)scalar_or(P, "max_iter", 0.0);
-    s->opts.flags = scalar_or(P, "rescue", 1.0) != 0.0 ? CMPC_FLAG_RESCUE : 0;
+    s->opts.flags = scalar_or(P, "rescue", 1.0) != 0.0
+                        ? CMPC_FLAG_RESCUE | (scalar_or(P, "polish", 1.0) != 0.0 ? CMPC_FLAG_POLISH : 0)
+                        : 0;
 }
 
 /* D -> batch, neighbours, rows of x_last, data pointers (no copies: MATLAB order is the ABI's) */

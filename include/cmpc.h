@@ -42,8 +42,8 @@
 extern "C" {
 #endif
 
-#define CMPC_ABI_VERSION 4   /* 2: cmpc_lpv_advance_dev status / infeasible, cmpc_lpv_rounds_*; 3: cmpc_opts.order;
-                                4: cmpc_comm_sum_i32, cmpc_plan_mpc */
+#define CMPC_ABI_VERSION 5   /* 2: cmpc_lpv_advance_dev status / infeasible, cmpc_lpv_rounds_*; 3: cmpc_opts.order;
+                                4: cmpc_comm_sum_i32, cmpc_plan_mpc; 5: CMPC_FLAG_POLISH */
 
 /* API error codes */
 #define CMPC_OK 0
@@ -87,8 +87,13 @@ typedef struct cmpc_ctx cmpc_ctx;
 #define CMPC_FLAG_LANE 128  /* lane-per-agent stage-wise solver in fp64 (one lane per agent, 64 agents per
                                wavefront: large batches of long horizons); CMPC_ERR_UNSUPPORTED for
                                dimensions it is not instantiated for (see CMPC_FLAG_FP32) */
+#define CMPC_FLAG_POLISH 256 /* with CMPC_FLAG_RESCUE: OSQP's polish=True (LPV_Planner.py:233) for the interior-
+                               point iterate — a condensed breakdown at the rounding floor (status 2) takes
+                               its active set {lambda_r > t_r} as exact, solves that equality-constrained QP
+                               (range-space KKT, two active-set corrections) and returns it when its merit
+                               is lower (status 1 below tol) */
 #define CMPC_FLAG_ALL (CMPC_FLAG_GENERIC | CMPC_FLAG_FP32 | CMPC_FLAG_RICCATI | CMPC_FLAG_RESCUE | CMPC_FLAG_FINISH | \
-                       CMPC_FLAG_LANE)  /* other bits: CMPC_ERR_ARG */
+                       CMPC_FLAG_LANE | CMPC_FLAG_POLISH)  /* other bits: CMPC_ERR_ARG */
 
 typedef struct {
     double tol;    /* relative stationarity/feasibility tolerance (complementarity: 1e-4*tol); <= 0 selects 1e-9 */

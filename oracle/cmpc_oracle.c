@@ -17,7 +17,7 @@
  * (oracle/qp_ipm.py) on QPs captured from the reference (tests/golden).
  */
 #include <math.h>
-#if defined(ORACLE_TRACE) || defined(RIC_DEBUG) || defined(LAB_THDUMP) || defined(DIRCHECK) || defined(LAB_STOPDUMP)
+#if defined(ORACLE_TRACE) || defined(POLISH_DEBUG) || defined(RIC_DEBUG) || defined(LAB_THDUMP) || defined(DIRCHECK) || defined(LAB_STOPDUMP)
 #include <stdio.h>
 #endif
 #include <stdlib.h>
@@ -33,6 +33,7 @@ typedef struct {
     int newton, refine; /* refine: iterative-refinement steps of the Riccati solve */
     int refine_dd;      /* refinement steps of a double-double iteration (RIC_REFINE_MAX; continued
                            rescue solves RIC_REFINE_WARM, the kernels' kRefineMaxWarm) */
+    int polish;         /* CMPC_FLAG_POLISH: active-set polish of a breakdown at the rounding floor */
     /* newton: 0 condensed Cholesky; 1 Riccati (P = Qyy + A'PA + Hvy'K); 2 Riccati, Joseph form */
 } shared_t;
 
@@ -1134,6 +1135,292 @@ typedef struct {
     unsigned char* act;
 } work_t;
 
+/* value of row r at (X, U, sigma): stage rows c'X_{k+1} (+ sign sigma_kj), input rows +-u */
+static double row_val(const shared_t* S, const agent_t* a, const double* X, const double* U, const double* sig, int r) {
+    const int nx = S->nx, ns = S->ns, mc = S->mc, ms = S->N * mc;
+    if (r < ms) {
+        const int k = r / mc, rr = r % mc;
+        const double* c = a->C + ((size_t)k * mc + rr) * nx;
+        double v = 0.0;
+        for (int s = 0; s < nx; ++s) v += c[s] * X[(k + 1) * nx + s];
+        const int j = S->row_slack[rr];
+        if (j >= 0 && sig) v += S->row_sign[rr] * sig[k * ns + j];
+        return v;
+    }
+    const int q = r - ms;
+    return (q & 1) ? -U[q / 2] : U[q / 2];
+}
+
+/* The interior-point method's scaled residuals at (U, sigma, t, lambda) — the loop of solve_one
+   (stationarity rd, slack stationarity rsig, rows rp, mu), into wk->rd / rsig / rp; X is
+   re-simulated from U.  Returns the merit max(res, MU_FACTOR mu), *kkt = max(res, mu). */
+static double merit_at(const shared_t* S, const agent_t* a, work_t* wk, const double* U, const double* sig,
+                       const double* t, const double* lam, double* X, double* kkt) {
+    const int nx = S->nx, nu = S->nu, N = S->N, ns = S->ns, mc = S->mc;
+    const int n = N * nu, ms = N * mc, m = ms + 2 * nu * N;
+    fwd_sim(S, a, a->x0, U, X);
+    double* ybar = wk->ybar;
+    for (int k = 0; k <= N; ++k)
+        for (int s = 0; s < nx; ++s) {
+            double v = 2.0 * a->p[k * nx + s];
+            for (int t2 = 0; t2 < nx; ++t2) v += 2.0 * S->Q[s * nx + t2] * X[k * nx + t2];
+            ybar[k * nx + s] = v;
+        }
+    double gscale = 1.0;
+    adjoint(S, a, ybar, wk->gU, wk->psi, wk->tmp);
+    for (int k = 0; k < N; ++k)
+        for (int i = 0; i < nu; ++i) {
+            double v = 0.0;
+            for (int j = 0; j < nu; ++j) {
+                double du_k = U[k * nu + j] - (k ? U[(k - 1) * nu + j] : a->up[j]);
+                double du_n = (k + 1 < N) ? U[(k + 1) * nu + j] - U[k * nu + j] : 0.0;
+                v += 2.0 * S->R[i * nu + j] * U[k * nu + j] + 2.0 * S->dR[i * nu + j] * (du_k - du_n);
+            }
+            wk->gU[k * nu + i] += v;
+            gscale = nmax(gscale, fabs(wk->gU[k * nu + i]));
+        }
+    for (int k = 0; k < N; ++k)
+        for (int r = 0; r < mc; ++r) {
+            const double* c_ = a->C + ((size_t)k * mc + r) * nx;
+            for (int s = 0; s < nx; ++s) ybar[(k + 1) * nx + s] += lam[k * mc + r] * c_[s];
+        }
+    adjoint(S, a, ybar, wk->rd, wk->psi, wk->tmp);
+    for (int k = 0; k < N; ++k)
+        for (int i = 0; i < nu; ++i) {
+            double v = 0.0;
+            for (int j = 0; j < nu; ++j) {
+                double du_k = U[k * nu + j] - (k ? U[(k - 1) * nu + j] : a->up[j]);
+                double du_n = (k + 1 < N) ? U[(k + 1) * nu + j] - U[k * nu + j] : 0.0;
+                v += 2.0 * S->R[i * nu + j] * U[k * nu + j] + 2.0 * S->dR[i * nu + j] * (du_k - du_n);
+            }
+            const int r = ms + (k * nu + i) * 2;
+            wk->rd[k * nu + i] += v + lam[r] - lam[r + 1];
+        }
+    for (int k = 0; k < N; ++k)
+        for (int j = 0; j < ns; ++j) {
+            double v = 2.0 * S->Qs[j] * sig[k * ns + j];
+            for (int r = 0; r < mc; ++r)
+                if (S->row_slack[r] == j) v += S->row_sign[r] * lam[k * mc + r];
+            wk->rsig[k * ns + j] = v;
+        }
+    double mu = 0.0, nrp = 0.0, nrd = 0.0, nrs = 0.0, scale_p = 1.0, qs_max = 1.0;
+    int mact = 0;
+    for (int r = 0; r < m; ++r) {
+        if (!wk->act[r]) { wk->rp[r] = 0.0; continue; }
+        wk->rp[r] = row_val(S, a, X, U, sig, r) + t[r] - wk->w[r];
+        nrp = nmax(nrp, fabs(wk->rp[r]));
+        mu += t[r] * lam[r];
+        ++mact;
+        if (fabs(wk->w[r]) > scale_p) scale_p = fabs(wk->w[r]);
+    }
+    for (int j = 0; j < ns; ++j) if (2 * S->Qs[j] > qs_max) qs_max = 2 * S->Qs[j];
+    mu = mact ? mu / mact : 0.0;
+    for (int c = 0; c < n; ++c) nrd = nmax(nrd, fabs(wk->rd[c]));
+    for (int q = 0; q < N * ns; ++q) nrs = nmax(nrs, fabs(wk->rsig[q]));
+    const double res = nmax(nmax(nrd / gscale, nrs / qs_max), nrp / scale_p);
+    *kkt = nmax(res, mu);
+    return nmax(res, MU_FACTOR * mu);
+}
+
+#ifndef POLISH_MAX_ACTIVE
+#define POLISH_MAX_ACTIVE 128 /* kPolishMaxActive (internal.h): larger active sets are not polished */
+#endif
+#ifndef POLISH_STEPS
+#define POLISH_STEPS 3        /* kPolishSteps: Newton steps on the (linear) equality-constrained KKT system */
+#endif
+#ifndef POLISH_PASSES
+#define POLISH_PASSES 2       /* kPolishPasses: active-set corrections (negative multipliers out, violated rows in) */
+#endif
+
+/* Polish (CMPC_FLAG_POLISH) — OSQP's `polish=True` (LPV_Planner.py:233) restated for the
+   interior-point iterate.  From an iterate at the rounding floor (t, lambda), the active set
+   A = {r : lambda_r > t_r} is taken as exact: the equality-constrained QP
+       min f(U) + sum Qs sigma^2   s.t.   row_r(U, sigma) = w_r  (r in A)
+   is solved by Newton steps on its (linear) KKT system from (U, sigma, lambda_A), each through the
+   range-space form:  H = the condensed Hessian of f (the Newton matrix without any theta: 2Q
+   stage weights, 2R, 2dR; well conditioned), G_A = the active rows as functions of U (c'Gamma_{k+1}
+   or +-e_i), E = the slack coupling (sign_r sign_r' / 2Qs_j within a slack group):
+       S dlam = rA' - G_A H^-1 rU,   dU = -H^-1 (rU + G_A' dlam),   S = G_A H^-1 G_A' + E,
+       dsig = -(rsig + sign' dlam) / 2Qs,   rA' = rA - sign rsig / 2Qs.
+   The polished point (t = max(w - row, 0), lambda = max(lambda_A, 0) on A, 0 elsewhere) replaces
+   the iterate when its merit is below the best merit the method reached (status 1 below tol).
+   The condensed Gamma (wk->Gam) must be built; wk->K is overwritten.  Returns the merit of the
+   polished point (+inf when H or S is not positive definite or |A| > POLISH_MAX_ACTIVE), and
+   the polished U, sigma, kkt in Up, sigp, *kkt. */
+static double polish_one(const shared_t* S, const agent_t* a, work_t* wk, const double* U, const double* sig,
+                         const double* t, const double* lam, double* Up, double* sigp, double* kkt) {
+    const int nx = S->nx, nu = S->nu, N = S->N, ns = S->ns, mc = S->mc;
+    const int n = N * nu, ms = N * mc, m = ms + 2 * nu * N;
+    const int amax = POLISH_MAX_ACTIVE;
+    unsigned char* in = malloc((size_t)m);
+    int* Ar = malloc(sizeof(int) * amax);
+    double* GA = malloc(sizeof(double) * (2 * (size_t)amax * n + (size_t)amax * amax + 3 * (size_t)amax +
+                                          3 * (size_t)n + (size_t)N * ns + (size_t)m));
+    double *Y = GA + (size_t)amax * n, *Ssch = Y + (size_t)amax * n, *lA = Ssch + (size_t)amax * amax;
+    double *rA = lA + amax, *dl = rA + amax, *v = dl + amax, *gv = v + n, *Uc = gv + n, *sc = Uc + n, *lamp = sc + N * ns;
+    double best = INFINITY;
+    double* X = wk->dX;
+    const double* Gam = wk->Gam;
+#ifndef POL_AFAC
+#define POL_AFAC 1.0
+#endif
+    for (int r = 0; r < m; ++r) in[r] = wk->act[r] && lam[r] > POL_AFAC * t[r];
+    /* H: the condensed Newton matrix with every theta = 0 (solve_one's K build) */
+    double* K = wk->K;
+    memset(K, 0, sizeof(double) * n * n);
+    for (int k = 0; k < N; ++k) {
+        const double* G = Gam + (size_t)(k + 1) * nx * n;
+        const int ncol = (k + 1) * nu;
+        double* Yk = wk->Yk;
+        for (int s = 0; s < nx; ++s)
+            for (int c2 = 0; c2 < ncol; ++c2) {
+                double acc = 0.0;
+                for (int u = 0; u < nx; ++u) acc += 2.0 * S->Q[s * nx + u] * G[u * n + c2];
+                Yk[s * n + c2] = acc;
+            }
+        for (int c1 = 0; c1 < ncol; ++c1)
+            for (int c2 = 0; c2 <= c1; ++c2) {
+                double acc = 0.0;
+                for (int s = 0; s < nx; ++s) acc += G[s * n + c1] * Yk[s * n + c2];
+                K[IDX2(c1, c2, n)] += acc;
+            }
+    }
+    for (int k = 0; k < N; ++k)
+        for (int i = 0; i < nu; ++i)
+            for (int j = 0; j < nu; ++j) {
+                const int ci = k * nu + i, cj = k * nu + j;
+                const double d = 2.0 * S->R[i * nu + j] + 2.0 * S->dR[i * nu + j] * (k + 1 < N ? 2.0 : 1.0);
+                if (cj <= ci) K[IDX2(ci, cj, n)] += d;
+                if (k > 0) K[IDX2(ci, (k - 1) * nu + j, n)] += -2.0 * S->dR[i * nu + j];
+            }
+    if (chol(K, n)) goto done;
+    for (int pass = 0; pass < POLISH_PASSES; ++pass) {
+        int nA = 0;
+        for (int r = 0; r < m; ++r)
+            if (in[r]) {
+                if (nA == amax) goto done;
+                Ar[nA++] = r;
+            }
+        /* G_A rows and Y = L^-1 G_A' */
+        for (int q = 0; q < nA; ++q) {
+            const int r = Ar[q];
+            double* g = GA + (size_t)q * n;
+            memset(g, 0, sizeof(double) * n);
+            if (r < ms) {
+                const int k = r / mc;
+                const double* c = a->C + (size_t)r * nx;
+                const double* G = Gam + (size_t)(k + 1) * nx * n;
+                for (int col = 0; col < (k + 1) * nu; ++col) {
+                    double acc = 0.0;
+                    for (int s = 0; s < nx; ++s) acc += c[s] * G[s * n + col];
+                    g[col] = acc;
+                }
+            } else {
+                const int qq = r - ms;
+                g[qq / 2] = (qq & 1) ? -1.0 : 1.0;
+            }
+            double* y = Y + (size_t)q * n;
+            for (int i = 0; i < n; ++i) {
+                double acc = g[i];
+                for (int p2 = 0; p2 < i; ++p2) acc -= K[IDX2(i, p2, n)] * y[p2];
+                y[i] = acc / K[IDX2(i, i, n)];
+            }
+        }
+        /* S = G_A H^-1 G_A' + E = Y'Y + E */
+        for (int q = 0; q < nA; ++q)
+            for (int q2 = 0; q2 <= q; ++q2) {
+                double acc = 0.0;
+                for (int i = 0; i < n; ++i) acc += Y[(size_t)q * n + i] * Y[(size_t)q2 * n + i];
+                const int r = Ar[q], r2 = Ar[q2];
+                if (r < ms && r2 < ms && r / mc == r2 / mc) {
+                    const int j = S->row_slack[r % mc];
+                    if (j >= 0 && S->row_slack[r2 % mc] == j)
+                        acc += S->row_sign[r % mc] * S->row_sign[r2 % mc] / (2.0 * S->Qs[j]);
+                }
+                Ssch[IDX2(q, q2, nA)] = acc;
+            }
+        if (chol(Ssch, nA)) goto done;
+        /* Newton steps on the KKT system from (U, sigma, lambda_A) */
+        memcpy(Uc, U, sizeof(double) * n);
+        memcpy(sc, sig, sizeof(double) * N * ns);
+        for (int r = 0; r < m; ++r) lamp[r] = 0.0;
+        for (int q = 0; q < nA; ++q) lA[q] = lam[Ar[q]];
+        for (int step = 0; step < POLISH_STEPS; ++step) {
+            for (int q = 0; q < nA; ++q) lamp[Ar[q]] = lA[q];
+            /* residuals with t = 0 (rp = row - w on A): rU = wk->rd, rsig = wk->rsig */
+            for (int r = 0; r < m; ++r) wk->dt_a[r] = 0.0;
+            double kk;
+            merit_at(S, a, wk, Uc, sc, wk->dt_a, lamp, X, &kk);
+            for (int q = 0; q < nA; ++q) {
+                const int r = Ar[q];
+                double ra = wk->rp[r];
+                if (r < ms) {
+                    const int j = S->row_slack[r % mc];
+                    if (j >= 0) ra -= S->row_sign[r % mc] * wk->rsig[(r / mc) * ns + j] / (2.0 * S->Qs[j]);
+                }
+                rA[q] = ra;
+            }
+            memcpy(v, wk->rd, sizeof(double) * n);
+            chol_solve(K, n, v); /* H^-1 rU */
+            for (int q = 0; q < nA; ++q) {
+                double acc = rA[q];
+                for (int i = 0; i < n; ++i) acc -= GA[(size_t)q * n + i] * v[i];
+                dl[q] = acc;
+            }
+            chol_solve(Ssch, nA, dl);
+            for (int i = 0; i < n; ++i) gv[i] = wk->rd[i];
+            for (int q = 0; q < nA; ++q)
+                for (int i = 0; i < n; ++i) gv[i] += GA[(size_t)q * n + i] * dl[q];
+            chol_solve(K, n, gv);
+            for (int i = 0; i < n; ++i) Uc[i] -= gv[i];
+            for (int k = 0; k < N; ++k)
+                for (int j = 0; j < ns; ++j) {
+                    double acc = wk->rsig[k * ns + j];
+                    for (int q = 0; q < nA; ++q) {
+                        const int r = Ar[q];
+                        if (r < ms && r / mc == k && S->row_slack[r % mc] == j) acc += S->row_sign[r % mc] * dl[q];
+                    }
+                    sc[k * ns + j] -= acc / (2.0 * S->Qs[j]);
+                }
+            for (int q = 0; q < nA; ++q) lA[q] += dl[q];
+        }
+        /* the polished point as an interior-point iterate: t = 0 and lambda = max(lambda_A, 0) on A,
+           t = max(w - row, 0) and lambda = 0 elsewhere */
+        fwd_sim(S, a, a->x0, Uc, X);
+        int changed = 0;
+        for (int r = 0; r < m; ++r) {
+            lamp[r] = 0.0;
+            wk->dt_a[r] = 1.0;
+            if (!wk->act[r] || in[r]) continue;
+            const double g = wk->w[r] - row_val(S, a, X, Uc, sc, r);
+            wk->dt_a[r] = fmax(g, 0.0);
+            if (g < 0.0) in[r] = 1, changed = 1;   /* violated: enters the next pass's active set */
+        }
+        for (int q = 0; q < nA; ++q) {
+            lamp[Ar[q]] = fmax(lA[q], 0.0);
+            wk->dt_a[Ar[q]] = 0.0;
+            if (lA[q] < 0.0) in[Ar[q]] = 0, changed = 1;  /* negative multiplier: leaves it */
+        }
+        double kk;
+        const double mp = merit_at(S, a, wk, Uc, sc, wk->dt_a, lamp, X, &kk);
+#ifdef POLISH_DEBUG
+        fprintf(stderr, "PD pass %d nA %d merit %.2e changed %d\n", pass, nA, mp, changed);
+#endif
+        if (mp < best) {
+            best = mp;
+            *kkt = kk;
+            memcpy(Up, Uc, sizeof(double) * n);
+            memcpy(sigp, sc, sizeof(double) * N * ns);
+        }
+        if (!changed) break;
+    }
+done:
+    free(in);
+    free(Ar);
+    free(GA);
+    return best;
+}
+
 /* Solve one agent.  Returns OSQP-style status: 1 solved, 2 solved inaccurate, -2 max_iter, -10 unsolved. */
 static int solve_one(const shared_t* S, const agent_t* a, double tol, int max_iter, work_t* wk,
                      double* z, double* kkt_out, int* iters_out) {
@@ -1158,9 +1445,10 @@ static int solve_one(const shared_t* S, const agent_t* a, double tol, int max_it
     }
     const int nx = S->nx, nu = S->nu, N = S->N, ns = S->ns, mc = S->mc;
     const int n = N * nu, ms = N * mc, m = ms + 2 * nu * N;
-    double* Gam = wk->Gam; /* (N+1) x nx x n */
-    if (!NEWTON_C) memset(Gam, 0, sizeof(double) * (size_t)(N + 1) * nx * n);
-    for (int k = 0; k < N && !NEWTON_C; ++k) {
+    double* Gam = wk->Gam; /* (N+1) x nx x n; also for the polish */
+    const int need_gam = !NEWTON_C || S->polish;
+    if (need_gam) memset(Gam, 0, sizeof(double) * (size_t)(N + 1) * nx * n);
+    for (int k = 0; k < N && need_gam; ++k) {
         const double* Ak = a->A + (size_t)k * nx * nx;
         const double* Bk = a->B + (size_t)k * nx * nu;
         double* Gn = Gam + (size_t)(k + 1) * nx * n;
@@ -1897,9 +2185,23 @@ static int solve_one(const shared_t* S, const agent_t* a, double tol, int max_it
 #ifdef LAB_STOPDUMP
     if (it_switch) fprintf(stderr, "WARM switch %d after %d stop %d best_m %.2e\n", it_switch, it - it_switch, stop, best_m);
 #endif
+    /* polish (CMPC_FLAG_POLISH): a solve of the rescue policy that stops at the rounding floor — a
+       condensed breakdown or stall, a continued or cold Riccati solve — from its last iterate (the
+       kernels' rescue image, flag 2) */
+    double pol_m = INFINITY, pol_kkt = INFINITY;
+    if (S->polish && stop != 1 && stop != 4 && best_m < 1e3 * tol)
+        pol_m = polish_one(S, a, wk, U, sig, t, lam, wk->dU, wk->dsig, &pol_kkt);
+#ifdef POLISH_DEBUG
+    if (stop != 1) fprintf(stderr, "POL stop %d newton %d best_m %.2e pol_m %.2e\n", stop, S->newton, best_m, pol_m);
+#endif
     int status;
     if (stop == 1) {
         status = 1;
+    } else if (pol_m < best_m) {
+        memcpy(U, wk->dU, sizeof(double) * n);
+        memcpy(sig, wk->dsig, sizeof(double) * N * ns);
+        kkt = pol_kkt;
+        status = pol_m < tol ? 1 : 2;
     } else {
         if (best_it > 0) { /* restore the best iterate */
             memcpy(U, bU, sizeof(double) * n);
@@ -1939,7 +2241,10 @@ int cmpc_oracle_solve_ex(int nx, int nu, int N, int ns, int mc, int batch,
                          const double* qlin, const double* Crow, const double* hrow,
                          double tol, int max_iter, int nthreads, int newton, int refine, const double* U0,
                          double* z, double* kkt, int* iters, int* status) {
-    shared_t S = {nx, nu, N, ns, mc, Q, R, dR, Qs, u_ub, u_lb, row_slack, row_sign, newton, refine, RIC_REFINE_MAX};
+    const int polish = (newton >> 8) & 1; /* newton | 0x100: CMPC_FLAG_POLISH */
+    newton &= 0xff;
+    shared_t S = {nx, nu, N, ns, mc, Q, R, dR, Qs, u_ub, u_lb, row_slack, row_sign, newton, refine, RIC_REFINE_MAX,
+                  polish};
     if (newton && (nx + nu > NA_MAX || nu > NU_MAX)) return -1;
     const int n = N * nu, m = N * mc + 2 * nu * N;
     const size_t nz = (size_t)(nx + ns) * (N + 1) + 2 * (size_t)nu * N;
@@ -1956,7 +2261,7 @@ int cmpc_oracle_solve_ex(int nx, int nu, int N, int ns, int mc, int batch,
 #ifdef RIC_DEBUG
         const size_t nG = (size_t)(N + 1) * nx * n, nK = (size_t)n * n;
 #else
-        const int cond = newton == 0 || newton == 4 || newton == 5; /* the condensed Newton matrix is formed */
+        const int cond = newton == 0 || newton == 4 || newton == 5 || polish; /* condensed Newton matrix (or H) */
         const size_t nG = cond ? (size_t)(N + 1) * nx * n : 0, nK = cond ? (size_t)n * n : 0;
 #endif
         size_t need = nF + (size_t)n + (size_t)N * ns + nG + nK + 4 * (size_t)(N + 1) * nx + 4 * (size_t)n +

@@ -1,0 +1,56 @@
+"""Active-set polish (CMPC_FLAG_POLISH; OSQP's polish=True, LPV_Planner.py:233) on agent-QPs of the
+reference's agent model whose condensed factorisation breaks down at the rounding floor
+(tests/golden/polish_lpv.npz, made by oracle/gen_polish_fixture.py from bench.py's lpv_rounds
+population in the CPU lab)."""
+import numpy as np
+import pytest
+
+from conftest import golden
+
+
+def _problems():
+    d = golden("polish_lpv")
+    P = {k: d[k] for k in d.files if not k.startswith("status_")}
+    for k in ("nx", "nu", "N", "ns", "mc"):
+        P[k] = int(P[k])
+    return P, d["status_plain"], d["status_polish"]
+
+
+def test_oracle_polish_finishes_floor_breakdowns():
+    """The C restatement: without the polish the breakdown agents stop at the rounding floor
+    (status 2); with it every agent is solved (merit < tol), the agents that converged are
+    untouched (bit-identical), and the polished optimum agrees with the rounding-floor iterate to
+    its accuracy and with the Riccati double-double method's solution (newton 3) where that one
+    converges."""
+    from oracle import cmpc_oracle as CO
+
+    P, st_plain, st_pol = _problems()
+    z0, k0, i0, s0 = CO.solve_batch_rescue(P, nthreads=4)
+    z1, k1, i1, s1 = CO.solve_batch_rescue(P, nthreads=4, polish=True)
+    assert np.array_equal(s0, st_plain) and np.array_equal(s1, st_pol)
+    assert (s1 == 1).all() and (k1 < 1e-9).all(), k1
+    same = s0 == 1
+    assert np.array_equal(z0[same], z1[same])
+    assert np.abs(z1 - z0).max() < 1e-4
+    z3, k3, i3, s3 = CO.solve_batch(P, nthreads=4, newton=3)
+    ok = s3 == 1
+    assert ok.any()
+    assert np.abs(z1[ok] - z3[ok]).max() < 1e-6, np.abs(z1[ok] - z3[ok]).max()
+
+
+@pytest.mark.gpu
+def test_gpu_polish_matches_c_restatement(gpu_ctx):
+    """The HIP polish (mpc_polish.hip) on the same agents: every agent solved (status 1), z within
+    1e-6 of the C restatement's polished optimum."""
+    import cmpc
+    from oracle import cmpc_oracle as CO
+
+    P, _, _ = _problems()
+    z, kkt, it, st = cmpc.solve_mpc(P, gpu_ctx, rescue=True, polish=True)
+    zp, kp, ip, sp = cmpc.solve_mpc(P, gpu_ctx, rescue=True)
+    z1, k1, i1, s1 = CO.solve_batch_rescue(P, nthreads=4, polish=True)
+    print("GPU without polish", sp.tolist(), "with", st.tolist(), "kkt", kkt.max(),
+          "|z - z_cpu|", np.abs(z - z1).max())
+    assert (st == cmpc.CMPC_SOLVED).all(), st
+    assert (kkt < 1e-9).all(), kkt
+    assert np.abs(z - z1).max() < 1e-6

@@ -166,9 +166,18 @@ def test_lpv_rounds_at_scale_against_c_restatement(gpu_ctx):
     out = bench.lpv_rounds(gpu_ctx, replicas=341, rounds=20, warmup=2, check=True, sample=128)
     st = out["status_counts"]
     print({k: v for k, v in out.items() if k in ("agent_qp_per_s", "status_counts", "max_kkt", "oracle_sample")})
+    assert out["polish"]   # PlannerLPVBatch's default, as the reference's OSQP polish=True
     assert all(k in (1, 2) for k in st), st
+    # the rounding floor (status 2) after the polish: <= 0.5 % of the solves (3.5 % without it)
+    assert st.get(2, 0) <= 0.005 * sum(st.values()), st
     assert out["max_kkt"] <= 1e-6
     smp = out["oracle_sample"]
     assert smp["checked"] == 20 * 128, smp
-    assert smp["both_solved"] >= 0.9 * smp["checked"], smp
+    assert smp["both_solved"] >= 0.99 * smp["checked"], smp
     assert smp["max_abs_err_vs_cpu"] <= 1e-6, smp
+    # both solved but farther apart than 1e-6: an interior-point endpoint against a polished one on a
+    # degenerate optimum; the GPU point certifies itself (reference-form KKT, objective not above the
+    # C restatement's)
+    dg = smp["degenerate"]
+    if dg["count"]:
+        assert dg["max_ref_kkt_gpu"] <= 1e-6 and dg["max_obj_gap_rel"] <= 1e-10, dg
