@@ -635,7 +635,7 @@ __global__ __launch_bounds__(kWave) void mpc_ipm_kernel(const MpcConst c, const 
     // polish (CMPC_FLAG_POLISH): a stall or max-iteration exit at the rounding floor leaves its last iterate
     // in the rescue image too (a breakdown wrote it above)
     if (c.polish && P.ws && stop != kStopConverged && stop != kStopBreakdown && stop != kStopNonFinite &&
-        best_m < 1e3 * c.tol) {
+        (best_m < 1e3 * c.tol || stop == kStopMaxIter)) {
         double* hd = P.ws + (size_t)b * c.ws_stride;
         const size_t ht = hand_t(c);
         for (int i = l; i < n; i += kWave) hd[2 + i] = U[i];
@@ -678,7 +678,9 @@ __global__ __launch_bounds__(kWave) void mpc_ipm_kernel(const MpcConst c, const 
             // breakdown at the rounding floor with CMPC_FLAG_POLISH; slot 1 then holds its best merit)
             double* hd = P.ws + (size_t)b * c.ws_stride;
             const bool ho = hand_over(stop, best_m, c);
-            const bool pol = !ho && c.polish && stop != kStopConverged && stop != kStopNonFinite && best_m < 1e3 * c.tol;
+            // polished: a final exit short of tol (status 2 or -2; CMPC_UNSOLVED goes on to the Riccati rescue)
+            const bool pol = !ho && c.polish && stop != kStopConverged && stop != kStopNonFinite &&
+                             (best_m < 1e3 * c.tol || stop == kStopMaxIter);
             hd[0] = ho ? 1.0 : (pol ? 2.0 : 0.0);
             if (pol) hd[1] = best_m;
         }
@@ -806,6 +808,11 @@ hipError_t mpc_launch(const MpcConst& c_in, const MpcPtrs& p, int batch, hipStre
         }
     }
     if (e != hipSuccess || !c.rescue || !p.status || !p.ws) return e;
+    // polish (CMPC_FLAG_POLISH) first: the condensed exits short of tol, and the breakdowns handed over to
+    // the Riccati rescue (those it polishes to tol never reach it); the fused double-integrator round
+    // keeps its rows in LDS only, so it has none to polish against
+    const bool pol = c.polish && !p.fuse.on;
+    if (pol && (e = mpc_polish_launch(c, p, batch, s)) != hipSuccess) return e;
     // rescue pass: the Riccati kernel re-solves, on the same problems, exactly the agents the
     // condensed solve left CMPC_UNSOLVED (its other workgroups return at once) — continuing from
     // the iterate a breakdown handed over (hand_doubles); a second pass restarts cold the rare
@@ -813,11 +820,10 @@ hipError_t mpc_launch(const MpcConst& c_in, const MpcPtrs& p, int batch, hipStre
     MpcConst cr = c;
     cr.riccati = 1;
     if ((e = mpc_riccati_launch(cr, p, batch, s)) != hipSuccess) return e;
+    cr.rescue = 2;  // the second (cold) pass: the last solve these agents get
     if ((e = mpc_riccati_launch(cr, p, batch, s)) != hipSuccess) return e;
-    // polish (CMPC_FLAG_POLISH): the breakdowns at the rounding floor (rescue image flag 2); the fused
-    // double-integrator round keeps its rows in LDS only, so it has none to polish against
-    if (!c.polish || p.fuse.on) return hipSuccess;
-    return mpc_polish_launch(c, p, batch, s);
+    // ... and the Riccati rescue's own exits short of tol (rescue image flag 2)
+    return pol ? mpc_polish_launch(c, p, batch, s) : hipSuccess;
 }
 
 // ---- f64 MFMA fragment-map self test: D(16x16) = A(16x4) * B(4x16) ----

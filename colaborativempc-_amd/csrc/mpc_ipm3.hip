@@ -1610,7 +1610,7 @@ __global__ __launch_bounds__(64, 1) void mpc_ipm3_kernel(const MpcConst c, const
     // polish (CMPC_FLAG_POLISH): a stall or max-iteration exit at the rounding floor leaves its last iterate
     // too (a breakdown wrote it above)
     if (c.polish && P.ws && stop != kStopConverged && stop != kStopBreakdown && stop != kStopNonFinite &&
-        best_m < 1e3 * c.tol)
+        (best_m < 1e3 * c.tol || stop == kStopMaxIter))
         write_image();
     if (stop != kStopConverged) {
         if (best_it > 0) {  // restore the best iterate
@@ -1651,7 +1651,9 @@ __global__ __launch_bounds__(64, 1) void mpc_ipm3_kernel(const MpcConst c, const
             // breakdown at the rounding floor with CMPC_FLAG_POLISH; slot 1 then holds its best merit)
             double* hd = P.ws + (size_t)b * c.ws_stride;
             const bool ho = hand_over(stop, best_m, c);
-            const bool pol = !ho && c.polish && stop != kStopConverged && stop != kStopNonFinite && best_m < 1e3 * c.tol;
+            // polished: a final exit short of tol (status 2 or -2; CMPC_UNSOLVED goes on to the Riccati rescue)
+            const bool pol = !ho && c.polish && stop != kStopConverged && stop != kStopNonFinite &&
+                             (best_m < 1e3 * c.tol || stop == kStopMaxIter);
             hd[0] = ho ? 1.0 : (pol ? 2.0 : 0.0);
             if (pol) hd[1] = best_m;
         }

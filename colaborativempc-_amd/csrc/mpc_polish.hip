@@ -31,12 +31,12 @@ namespace {
 
 constexpr int kPT = 256;           // threads per workgroup (four waves)
 constexpr int kPolishMaxActive = 96;
-constexpr int kPolishSteps = 3;    // Newton steps on the (linear) KKT system: one solve + two refinements
+constexpr int kPolishSteps = 3;    // Newton steps on the (linear) KKT system: one solve, refinements while above tol
 constexpr int kPolishPasses = 2;
 
 struct PolLayout {
-    int cst, Lh, Y, S, G0, G1, U, sig, Uc, sc, Ub, sb, X, ybar, lamh, w, lamp, tp, rp, rd, gU, rsig, zv, gz, lA,
-        rA, dl, red, in, Ar;
+    int cst, Lh, Y, S, G0, G1, sA, sB, sC, sp, U, sig, Uc, sc, Ub, sb, X, ybar, w, lamp, tp, rp, rd, gU, rsig, zv,
+        gz, lA, rA, dl, red, in, Ar;
     int amax, total;
 };
 
@@ -51,11 +51,17 @@ __host__ __device__ inline PolLayout pol_layout_for(const MpcConst& c, int amax)
     const int n = c.n, nx = c.nx, N = c.N, ns = c.ns, m = c.m;
     L.amax = amax;
     L.cst = take(mpc_const_used_doubles(c));
-    L.Lh = take(n * n);
+    const int mc = c.mc, nu = c.nu;
+    L.Lh = take(n * (n + 1) / 2);                       // packed lower triangle
     L.Y = take(amax * n > nx * n ? amax * n : nx * n);  // also 2Q Gamma while H is built
-    L.S = take(amax * (amax + 1) / 2);
-    L.G0 = take(nx * n);
-    L.G1 = take(nx * n);
+    const int sS = amax * (amax + 1) / 2;
+    L.S = take(sS > 2 * nx * n ? sS : 2 * nx * n);      // also Gamma's ping-pong while H is built
+    L.G0 = L.S;
+    L.G1 = L.S + nx * n;
+    L.sA = take(N * nx * nx);                           // the agent's stage data, staged once
+    L.sB = take(N * nx * nu);
+    L.sC = take(N * mc * nx);
+    L.sp = take((N + 1) * nx);
     L.U = take(n);
     L.sig = take(N * ns);
     L.Uc = take(n);
@@ -64,7 +70,6 @@ __host__ __device__ inline PolLayout pol_layout_for(const MpcConst& c, int amax)
     L.sb = take(N * ns);
     L.X = take((N + 1) * nx);
     L.ybar = take((N + 1) * nx);
-    L.lamh = take(m);
     L.w = take(m);
     L.lamp = take(m);
     L.tp = take(m);
@@ -110,36 +115,27 @@ __device__ double block_sum(double v, double* red) {
     return (red[4] + red[5]) + (red[6] + red[7]);
 }
 
-// in-place Cholesky of an n x n matrix (lower triangle, element (i, j) at M[idx(i, j)]),
-// right-looking, whole workgroup; returns false when a pivot is not positive
+// in-place Cholesky of an n x n matrix (lower triangle, element (i, j) at M[idx(i, j)]), right-looking,
+// by wave 0 alone (a wave's LDS operations execute in order: compiler fences, no barriers); lane l
+// owns rows l, l + 64, ...; returns false (on every lane) when a pivot is not positive
 template <class Idx>
-__device__ bool block_chol(double* M, int n, Idx idx, double* red) {
-    const int tid = threadIdx.x;
+__device__ bool wave_chol(double* M, int n, Idx idx) {
+    const int l = threadIdx.x;
     for (int j = 0; j < n; ++j) {
         const double d = M[idx(j, j)];
-        if (!(d > 0.0)) return false;  // uniform: every thread read the same value
-        if (tid == 0) red[13] = j ? fmin(red[13], d) : d;  // smallest pivot (diagnostics)
+        if (!(d > 0.0)) return false;
         const double s = sqrt(d);
         const double inv = 1.0 / s;
-        __syncthreads();
-        if (tid == 0) M[idx(j, j)] = s;
-        for (int i = j + 1 + tid; i < n; i += kPT) M[idx(i, j)] *= inv;
-        __syncthreads();
-        // trailing update of the lower triangle: (i, p), j < p <= i
-        const int rem = n - j - 1;
-        const int cnt = rem * (rem + 1) / 2;
-        for (int e = tid; e < cnt; e += kPT) {
-            // e -> (a, b) with 0 <= b <= a < rem, e = a (a + 1) / 2 + b
-            int a = (int)((sqrt(8.0 * e + 1.0) - 1.0) * 0.5);
-            while (a * (a + 1) / 2 > e) --a;
-            while ((a + 1) * (a + 2) / 2 <= e) ++a;
-            const int b = e - a * (a + 1) / 2;
-            const int i = j + 1 + a, p = j + 1 + b;
-            M[idx(i, p)] -= M[idx(i, j)] * M[idx(p, j)];
+        wsync();
+        if (l == 0) M[idx(j, j)] = s;
+        for (int i = j + 1 + l; i < n; i += kWave) M[idx(i, j)] *= inv;
+        wsync();
+        for (int i = j + 1 + l; i < n; i += kWave) {
+            const double lij = M[idx(i, j)];
+            for (int p = j + 1; p <= i; ++p) M[idx(i, p)] -= lij * M[idx(p, j)];
         }
-        __syncthreads();
+        wsync();
     }
-    (void)red;
     return true;
 }
 
@@ -335,7 +331,10 @@ __global__ __launch_bounds__(kPT) void mpc_polish_kernel(const MpcConst c_arg, c
     extern __shared__ __attribute__((aligned(16))) double sm[];
     const int b = blockIdx.x;
     double* hd = P.ws + (size_t)b * c_arg.ws_stride;
-    if (hd[0] != 2.0) return;  // not a breakdown at the rounding floor
+    // flag 2: a final exit short of tol; flag 1: a condensed breakdown handed over to the Riccati
+    // rescue — polished first, and handed over only when that does not reach tol
+    const double flag = hd[0];
+    if (flag != 2.0 && flag != 1.0) return;
     const int tid = threadIdx.x;
     const PolLayout L = pol_layout(c_arg);
     {
@@ -347,13 +346,23 @@ __global__ __launch_bounds__(kPT) void mpc_polish_kernel(const MpcConst c_arg, c
     const MpcConst& c = *reinterpret_cast<const MpcConst*>(sm + L.cst);
     const int nx = c.nx, nu = c.nu, N = c.N, ns = c.ns, mc = c.mc, ms = c.ms, m = c.m, n = c.n;
     const int amax = L.amax;
-    const PolCtx q{c, L, sm, P.A + (size_t)b * N * nx * nx, P.B + (size_t)b * N * nx * nu, P.x0 + (size_t)b * nx,
-                   P.up + (size_t)b * nu, P.p + (size_t)b * (N + 1) * nx, P.C + (size_t)b * N * mc * nx};
+    // the stage data (A, B, C rows, linear cost) staged in LDS once: every recursion below reads it
+    {
+        const double* gA = P.A + (size_t)b * N * nx * nx;
+        const double* gB = P.B + (size_t)b * N * nx * nu;
+        const double* gC = P.C + (size_t)b * N * mc * nx;
+        const double* gp = P.p + (size_t)b * (N + 1) * nx;
+        for (int i = tid; i < N * nx * nx; i += kPT) sm[L.sA + i] = gA[i];
+        for (int i = tid; i < N * nx * nu; i += kPT) sm[L.sB + i] = gB[i];
+        for (int i = tid; i < N * mc * nx; i += kPT) sm[L.sC + i] = gC[i];
+        for (int i = tid; i < (N + 1) * nx; i += kPT) sm[L.sp + i] = gp[i];
+    }
+    const PolCtx q{c, L, sm, sm + L.sA, sm + L.sB, P.x0 + (size_t)b * nx, P.up + (size_t)b * nu, sm + L.sp, sm + L.sC};
     const double* hC = P.h + (size_t)b * N * mc;
-    const double best_m = hd[1];
+    const double best_m = flag == 2.0 ? hd[1] : c_arg.tol;  // (flag 1: slot 1 holds the iterations done)
     const int ht = (int)hand_t(c);
     double *Lh = sm + L.Lh, *Y = sm + L.Y, *Sm = sm + L.S, *U = sm + L.U, *sig = sm + L.sig, *Uc = sm + L.Uc,
-           *sc = sm + L.sc, *Ub = sm + L.Ub, *sb = sm + L.sb, *lamh = sm + L.lamh, *w = sm + L.w, *lamp = sm + L.lamp,
+           *sc = sm + L.sc, *Ub = sm + L.Ub, *sb = sm + L.sb, *w = sm + L.w, *lamp = sm + L.lamp,
            *tp = sm + L.tp, *rp = sm + L.rp, *rd = sm + L.rd, *rsig = sm + L.rsig, *zv = sm + L.zv, *gz = sm + L.gz,
            *lA = sm + L.lA, *rA = sm + L.rA, *dl = sm + L.dl;
     int* in = reinterpret_cast<int*>(sm + L.in);
@@ -370,12 +379,11 @@ __global__ __launch_bounds__(kPT) void mpc_polish_kernel(const MpcConst c_arg, c
         const int act = isfinite(wr) ? 1 : 0;
         w[r] = act ? wr : 0.0;
         const double tr = hd[ht + r], lr = hd[ht + m + r];
-        lamh[r] = act ? lr : 0.0;
         in[r] = act | ((act && lr > tr) ? 2 : 0);
     }
     for (int i = tid; i < n; i += kPT) U[i] = hd[2 + i];
     for (int i = tid; i < N * ns; i += kPT) sig[i] = hd[2 + n + i];
-    for (int i = tid; i < n * n; i += kPT) Lh[i] = 0.0;
+    for (int i = tid; i < n * (n + 1) / 2; i += kPT) Lh[i] = 0.0;
     for (int i = tid; i < nx * n; i += kPT) sm[L.G0 + i] = 0.0;
     __syncthreads();
     // ---- H = sum_k Gamma_{k+1}' 2Q Gamma_{k+1} + the 2R / 2dR band (lower triangle), H = L L' ----
@@ -384,8 +392,8 @@ __global__ __launch_bounds__(kPT) void mpc_polish_kernel(const MpcConst c_arg, c
         double* Gn = sm + L.G1;
         double* WG = Y;
         for (int k = 0; k < N; ++k) {
-            const double* Ak = q.A + (size_t)k * nx * nx;
-            const double* Bk = q.B + (size_t)k * nx * nu;
+            const double* Ak = q.A + k * nx * nx;
+            const double* Bk = q.B + k * nx * nu;
             const int ncol = (k + 1) * nu;
             for (int e = tid; e < nx * n; e += kPT) {
                 const int s = e / n, col = e - s * n;
@@ -410,7 +418,7 @@ __global__ __launch_bounds__(kPT) void mpc_polish_kernel(const MpcConst c_arg, c
                 if (c2 > c1) continue;
                 double v = 0.0;
                 for (int s = 0; s < nx; ++s) v += Gn[s * n + c1] * WG[s * n + c2];
-                Lh[c1 * n + c2] += v;
+                Lh[c1 * (c1 + 1) / 2 + c2] += v;
             }
             __syncthreads();
             double* tmp = G;
@@ -422,15 +430,21 @@ __global__ __launch_bounds__(kPT) void mpc_polish_kernel(const MpcConst c_arg, c
             for (int j = 0; j < nu; ++j) {
                 const int cj = k * nu + j;
                 const double d = 2.0 * c.R[i * nu + j] + 2.0 * c.dR[i * nu + j] * (k + 1 < N ? 2.0 : 1.0);
-                if (cj <= ci) Lh[ci * n + cj] += d;
-                if (k > 0) Lh[ci * n + (k - 1) * nu + j] += -2.0 * c.dR[i * nu + j];
+                if (cj <= ci) Lh[ci * (ci + 1) / 2 + cj] += d;
+                if (k > 0) Lh[ci * (ci + 1) / 2 + (k - 1) * nu + j] += -2.0 * c.dR[i * nu + j];
             }
         }
         __syncthreads();
     }
-    auto ih = [n](int i, int j) { return i * n + j; };
+    auto ih = [](int i, int j) { return i * (i + 1) / 2 + j; };
     auto is = [](int i, int j) { return i * (i + 1) / 2 + j; };
-    const bool h_ok = block_chol(Lh, n, ih, sm + L.red);
+    int& flag_s = *reinterpret_cast<int*>(sm + L.red + 14);
+    if (tid < kWave) {
+        const bool ok = wave_chol(Lh, n, ih);
+        if (tid == 0) flag_s = ok ? 1 : 0;
+    }
+    __syncthreads();
+    const bool h_ok = flag_s != 0;
     __syncthreads();
     double best = INFINITY, best_kkt = INFINITY;
     int& nA_s = *reinterpret_cast<int*>(sm + L.red + 12);
@@ -463,16 +477,16 @@ __global__ __launch_bounds__(kPT) void mpc_polish_kernel(const MpcConst c_arg, c
             if (r < ms) {
                 const int k = r / mc;
                 double psi[CMPC_MAX_NX], nps[CMPC_MAX_NX];
-                for (int s = 0; s < nx; ++s) psi[s] = q.C[(size_t)r * nx + s];
+                for (int s = 0; s < nx; ++s) psi[s] = q.C[r * nx + s];
                 for (int j = k; j >= 0; --j) {
-                    const double* Bj = q.B + (size_t)j * nx * nu;
+                    const double* Bj = q.B + j * nx * nu;
                     for (int i = 0; i < nu; ++i) {
                         double v = 0.0;
                         for (int s = 0; s < nx; ++s) v += Bj[s * nu + i] * psi[s];
                         g[j * nu + i] = v;
                     }
                     if (j > 0) {
-                        const double* Aj = q.A + (size_t)j * nx * nx;
+                        const double* Aj = q.A + j * nx * nx;
                         for (int t2 = 0; t2 < nx; ++t2) {
                             double v = 0.0;
                             for (int s = 0; s < nx; ++s) v += Aj[s * nx + t2] * psi[s];
@@ -487,8 +501,8 @@ __global__ __launch_bounds__(kPT) void mpc_polish_kernel(const MpcConst c_arg, c
             }
             for (int i = 0; i < n; ++i) {
                 double v = g[i];
-                for (int p2 = 0; p2 < i; ++p2) v -= Lh[i * n + p2] * g[p2];
-                g[i] = v / Lh[i * n + i];
+                for (int p2 = 0; p2 < i; ++p2) v -= Lh[i * (i + 1) / 2 + p2] * g[p2];
+                g[i] = v / Lh[i * (i + 1) / 2 + i];
             }
         }
         __syncthreads();
@@ -508,7 +522,12 @@ __global__ __launch_bounds__(kPT) void mpc_polish_kernel(const MpcConst c_arg, c
             Sm[e] = v;
         }
         __syncthreads();
-        if (!block_chol(Sm, nA, is, sm + L.red)) break;
+        if (tid < kWave) {
+            const bool ok = wave_chol(Sm, nA, is);
+            if (tid == 0) flag_s = ok ? 1 : 0;
+        }
+        __syncthreads();
+        if (!flag_s) break;
         // Newton steps from (U, sigma, lambda_A)
         for (int i = tid; i < n; i += kPT) Uc[i] = U[i];
         for (int i = tid; i < N * ns; i += kPT) sc[i] = sig[i];
@@ -516,13 +535,15 @@ __global__ __launch_bounds__(kPT) void mpc_polish_kernel(const MpcConst c_arg, c
             lamp[r] = 0.0;
             tp[r] = 0.0;
         }
-        for (int qa = tid; qa < nA; qa += kPT) lA[qa] = lamh[Ar[qa]];
+        for (int qa = tid; qa < nA; qa += kPT) lA[qa] = hd[ht + m + Ar[qa]];
         __syncthreads();
+        double mp = INFINITY, kk = INFINITY;
         for (int step = 0; step < kPolishSteps; ++step) {
+            for (int r = tid; r < m; r += kPT) tp[r] = 0.0;
             for (int qa = tid; qa < nA; qa += kPT) lamp[Ar[qa]] = lA[qa];
             __syncthreads();
-            double kk;
-            pol_residuals(q, Uc, sc, tp, lamp, in, false, &kk);  // t = 0: rp = row - w on A
+            double kk0;
+            pol_residuals(q, Uc, sc, tp, lamp, in, false, &kk0);  // t = 0: rp = row - w on A
             for (int qa = tid; qa < nA; qa += kPT) {
                 const int r = Ar[qa];
                 double ra = rp[r];
@@ -567,39 +588,41 @@ __global__ __launch_bounds__(kPT) void mpc_polish_kernel(const MpcConst c_arg, c
             }
             for (int qa = tid; qa < nA; qa += kPT) lA[qa] += dl[qa];
             __syncthreads();
+            // the polished point as an interior-point iterate: t = 0 and lambda = max(lambda_A, 0) on A,
+            // t = max(w - row, 0) and lambda = 0 elsewhere; one Newton step normally reaches tol, a
+            // refinement step follows only when it does not
+            pol_fwd(q, Uc, sm + L.X);
+            __syncthreads();
+            for (int r = tid; r < m; r += kPT) {
+                lamp[r] = 0.0;
+                tp[r] = ((in[r] & 1) && !(in[r] & 2)) ? fmax(w[r] - pol_row(q, sm + L.X, Uc, sc, r), 0.0) : 1.0;
+            }
+            __syncthreads();  // the active rows' entries below overwrite the defaults above
+            for (int qa = tid; qa < nA; qa += kPT) {
+                lamp[Ar[qa]] = fmax(lA[qa], 0.0);
+                tp[Ar[qa]] = 0.0;
+            }
+            __syncthreads();
+            mp = pol_residuals(q, Uc, sc, tp, lamp, in, true, &kk);
+            if (mp < c.tol) break;
         }
-        // the polished point as an interior-point iterate; the next pass's active set
-        pol_fwd(q, Uc, sm + L.X);
-        __syncthreads();
-        int ch = 0;
-        for (int r = tid; r < m; r += kPT) {
-            lamp[r] = 0.0;
-            tp[r] = 1.0;
-            if (!(in[r] & 1) || (in[r] & 2)) continue;
-            const double g = w[r] - pol_row(q, sm + L.X, Uc, sc, r);
-            tp[r] = fmax(g, 0.0);
-            if (g < 0.0) ch = 1;
-        }
-        __syncthreads();  // the active rows' entries below overwrite the defaults above
-        for (int qa = tid; qa < nA; qa += kPT) {
-            lamp[Ar[qa]] = fmax(lA[qa], 0.0);
-            tp[Ar[qa]] = 0.0;
-            if (lA[qa] < 0.0) ch = 1;
-        }
-        __syncthreads();
-        double kk = 0.0;
-        const double mp = pol_residuals(q, Uc, sc, tp, lamp, in, true, &kk);
         if (mp < best) {
             best = mp;
             best_kkt = kk;
             for (int i = tid; i < n; i += kPT) Ub[i] = Uc[i];
             for (int i = tid; i < N * ns; i += kPT) sb[i] = sc[i];
         }
+        // the next pass's active set: violated rows join it, negative multipliers leave it (X: Uc's)
+        int ch = 0;
+        for (int r = tid; r < m; r += kPT)
+            if ((in[r] & 1) && !(in[r] & 2) && w[r] - pol_row(q, sm + L.X, Uc, sc, r) < 0.0) ch = 1;
+        for (int qa = tid; qa < nA; qa += kPT)
+            if (lA[qa] < 0.0) ch = 1;
         const int changed = __syncthreads_or(ch);
         if (!changed) break;
-        // negative multipliers leave the active set, violated rows join it
         for (int r = tid; r < m; r += kPT)
-            if ((in[r] & 1) && !(in[r] & 2) && tp[r] == 0.0 && w[r] - pol_row(q, sm + L.X, Uc, sc, r) < 0.0) in[r] |= 2;
+            if ((in[r] & 1) && !(in[r] & 2) && w[r] - pol_row(q, sm + L.X, Uc, sc, r) < 0.0) in[r] |= 2;
+        __syncthreads();  // (the loop above reads the active bits the one below clears)
         for (int qa = tid; qa < nA; qa += kPT)
             if (lA[qa] < 0.0) in[Ar[qa]] &= ~2;
         __syncthreads();
@@ -615,10 +638,9 @@ __global__ __launch_bounds__(kPT) void mpc_polish_kernel(const MpcConst c_arg, c
         st[3] = (unsigned long long)__double_as_longlong(best_m);
         st[4] = h_ok ? 1ull : 0ull;
         for (int i = 0; i < 3; ++i) st[5 + i] = (unsigned long long)__double_as_longlong(sm[L.red + 8 + i]);
-        st[8] = (unsigned long long)__double_as_longlong(sm[L.red + 13]);
     }
     if (!(best < best_m)) {
-        if (tid == 0) hd[0] = 0.0;
+        if (tid == 0 && flag == 2.0) hd[0] = 0.0;  // (flag 1 stays: the Riccati rescue takes the agent)
         return;
     }
     // ---- output in the reference layout (the condensed kernels' expansion) ----

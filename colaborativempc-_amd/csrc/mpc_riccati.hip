@@ -2118,10 +2118,11 @@ __global__ __launch_bounds__(kWave) void mpc_riccati_kernel(const MpcConst c_arg
     if (it > c.max_iter) it = c.max_iter;
     wsync();
     int status = CMPC_SOLVED;
-    // polish (CMPC_FLAG_POLISH): a rescue-pass solve that stops at the rounding floor leaves its last
-    // iterate in the rescue image with flag 2 and its best merit (mpc_polish.hip)
+    // polish (CMPC_FLAG_POLISH): a rescue-pass solve that stops short of tol for the last time — status 2 or
+    // -2, or anything on the second (cold) pass, rescue == 2 — leaves its last iterate in the rescue image
+    // with flag 2 and its best merit (mpc_polish.hip)
     const bool pol = c_arg.rescue && c.polish && stop != kStopConverged && stop != kStopNonFinite &&
-                     best_m < 1e3 * c.tol;
+                     (best_m < 1e3 * c.tol || stop == kStopMaxIter || c_arg.rescue == 2);
     if (pol) {
         const int ht = (int)hand_t(c);
         for (int i = l; i < n; i += kWave) hand[2 + i] = U[i];

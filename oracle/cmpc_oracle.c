@@ -1247,7 +1247,7 @@ static double merit_at(const shared_t* S, const agent_t* a, work_t* wk, const do
    The condensed Gamma (wk->Gam) must be built; wk->K is overwritten.  Returns the merit of the
    polished point (+inf when H or S is not positive definite or |A| > POLISH_MAX_ACTIVE), and
    the polished U, sigma, kkt in Up, sigp, *kkt. */
-static double polish_one(const shared_t* S, const agent_t* a, work_t* wk, const double* U, const double* sig,
+static double polish_one(const shared_t* S, const agent_t* a, work_t* wk, double tol, const double* U, const double* sig,
                          const double* t, const double* lam, double* Up, double* sigp, double* kkt) {
     const int nx = S->nx, nu = S->nu, N = S->N, ns = S->ns, mc = S->mc;
     const int n = N * nu, ms = N * mc, m = ms + 2 * nu * N;
@@ -1345,12 +1345,13 @@ static double polish_one(const shared_t* S, const agent_t* a, work_t* wk, const 
         memcpy(sc, sig, sizeof(double) * N * ns);
         for (int r = 0; r < m; ++r) lamp[r] = 0.0;
         for (int q = 0; q < nA; ++q) lA[q] = lam[Ar[q]];
+        double mp = INFINITY, kk = INFINITY;
         for (int step = 0; step < POLISH_STEPS; ++step) {
             for (int q = 0; q < nA; ++q) lamp[Ar[q]] = lA[q];
             /* residuals with t = 0 (rp = row - w on A): rU = wk->rd, rsig = wk->rsig */
             for (int r = 0; r < m; ++r) wk->dt_a[r] = 0.0;
-            double kk;
-            merit_at(S, a, wk, Uc, sc, wk->dt_a, lamp, X, &kk);
+            double kk0;
+            merit_at(S, a, wk, Uc, sc, wk->dt_a, lamp, X, &kk0);
             for (int q = 0; q < nA; ++q) {
                 const int r = Ar[q];
                 double ra = wk->rp[r];
@@ -1383,28 +1384,23 @@ static double polish_one(const shared_t* S, const agent_t* a, work_t* wk, const 
                     sc[k * ns + j] -= acc / (2.0 * S->Qs[j]);
                 }
             for (int q = 0; q < nA; ++q) lA[q] += dl[q];
+            /* the polished point as an interior-point iterate: t = 0 and lambda = max(lambda_A, 0) on A,
+               t = max(w - row, 0) and lambda = 0 elsewhere; one Newton step normally reaches tol, a
+               refinement step follows only when it does not */
+            fwd_sim(S, a, a->x0, Uc, X);
+            for (int r = 0; r < m; ++r) {
+                lamp[r] = 0.0;
+                wk->dt_a[r] = (wk->act[r] && !in[r]) ? fmax(wk->w[r] - row_val(S, a, X, Uc, sc, r), 0.0) : 1.0;
+            }
+            for (int q = 0; q < nA; ++q) {
+                lamp[Ar[q]] = fmax(lA[q], 0.0);
+                wk->dt_a[Ar[q]] = 0.0;
+            }
+            mp = merit_at(S, a, wk, Uc, sc, wk->dt_a, lamp, X, &kk);
+            if (mp < tol) break;
         }
-        /* the polished point as an interior-point iterate: t = 0 and lambda = max(lambda_A, 0) on A,
-           t = max(w - row, 0) and lambda = 0 elsewhere */
-        fwd_sim(S, a, a->x0, Uc, X);
-        int changed = 0;
-        for (int r = 0; r < m; ++r) {
-            lamp[r] = 0.0;
-            wk->dt_a[r] = 1.0;
-            if (!wk->act[r] || in[r]) continue;
-            const double g = wk->w[r] - row_val(S, a, X, Uc, sc, r);
-            wk->dt_a[r] = fmax(g, 0.0);
-            if (g < 0.0) in[r] = 1, changed = 1;   /* violated: enters the next pass's active set */
-        }
-        for (int q = 0; q < nA; ++q) {
-            lamp[Ar[q]] = fmax(lA[q], 0.0);
-            wk->dt_a[Ar[q]] = 0.0;
-            if (lA[q] < 0.0) in[Ar[q]] = 0, changed = 1;  /* negative multiplier: leaves it */
-        }
-        double kk;
-        const double mp = merit_at(S, a, wk, Uc, sc, wk->dt_a, lamp, X, &kk);
 #ifdef POLISH_DEBUG
-        fprintf(stderr, "PD pass %d nA %d merit %.2e changed %d\n", pass, nA, mp, changed);
+        fprintf(stderr, "PD pass %d nA %d merit %.2e\n", pass, nA, mp);
 #endif
         if (mp < best) {
             best = mp;
@@ -1412,6 +1408,12 @@ static double polish_one(const shared_t* S, const agent_t* a, work_t* wk, const 
             memcpy(Up, Uc, sizeof(double) * n);
             memcpy(sigp, sc, sizeof(double) * N * ns);
         }
+        /* the next pass's active set: violated rows join it, negative multipliers leave it */
+        int changed = 0;
+        for (int r = 0; r < m; ++r)
+            if (wk->act[r] && !in[r] && wk->w[r] - row_val(S, a, X, Uc, sc, r) < 0.0) in[r] = 1, changed = 1;
+        for (int q = 0; q < nA; ++q)
+            if (lA[q] < 0.0) in[Ar[q]] = 0, changed = 1;
         if (!changed) break;
     }
 done:
@@ -1823,6 +1825,17 @@ static int solve_one(const shared_t* S, const agent_t* a, double tol, int max_it
             fprintf(stderr, "\n");
 #endif
             if (warm_rescue && !S->newton && (finish || !(best_m < 1e3 * tol))) {
+                if (S->polish) { /* polish the breakdown iterate first; hand over only if that misses tol */
+                    double pk;
+                    const double pm = polish_one(S, a, wk, tol, U, sig, t, lam, wk->dU, wk->dsig, &pk);
+                    if (pm < tol) {
+                        memcpy(U, wk->dU, sizeof(double) * n);
+                        memcpy(sig, wk->dsig, sizeof(double) * N * ns);
+                        kkt = pk;
+                        stop = 1;
+                        break;
+                    }
+                }
 #ifdef LAB_STOPDUMP
                 it_switch = it;
 #endif
@@ -2185,12 +2198,14 @@ static int solve_one(const shared_t* S, const agent_t* a, double tol, int max_it
 #ifdef LAB_STOPDUMP
     if (it_switch) fprintf(stderr, "WARM switch %d after %d stop %d best_m %.2e\n", it_switch, it - it_switch, stop, best_m);
 #endif
-    /* polish (CMPC_FLAG_POLISH): a solve of the rescue policy that stops at the rounding floor — a
-       condensed breakdown or stall, a continued or cold Riccati solve — from its last iterate (the
-       kernels' rescue image, flag 2) */
+    /* polish (CMPC_FLAG_POLISH): the last solve of the rescue policy that an agent gets, when it stops
+       short of tol — a condensed or continued solve at the rounding floor or at max_iter (status 2 /
+       -2; an unsolved one goes on to the cold Riccati pass), the cold pass whatever its end — from its
+       last iterate (the kernels' rescue image, flag 2) */
     double pol_m = INFINITY, pol_kkt = INFINITY;
-    if (S->polish && stop != 1 && stop != 4 && best_m < 1e3 * tol)
-        pol_m = polish_one(S, a, wk, U, sig, t, lam, wk->dU, wk->dsig, &pol_kkt);
+    const int final_solve = !warm_rescue || best_m < 1e3 * tol || stop == 0;
+    if (S->polish && stop != 1 && stop != 4 && final_solve)
+        pol_m = polish_one(S, a, wk, tol, U, sig, t, lam, wk->dU, wk->dsig, &pol_kkt);
 #ifdef POLISH_DEBUG
     if (stop != 1) fprintf(stderr, "POL stop %d newton %d best_m %.2e pol_m %.2e\n", stop, S->newton, best_m, pol_m);
 #endif

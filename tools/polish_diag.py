@@ -35,7 +35,7 @@ def main():
         torch.cuda.synchronize()
         st = R.status.cpu().numpy()
         smp = np.sort(rng.choice(R.B, 128, replace=False)) if k >= 2 else np.zeros(0, int)
-        sel = np.union1d(np.flatnonzero(st == 2), smp)
+        sel = np.union1d(np.flatnonzero((st == 2) | (st == -10)), smp)
         if len(sel):
             prm = bp.prm
             rows = R.last_rows
@@ -50,7 +50,7 @@ def main():
             zc, kc, ic, sc = CO.solve_batch_rescue(P, nthreads=16, polish=True)
             zg, sg, kg = R.z.cpu().numpy()[sel], st[sel], R.kkt.cpu().numpy()[sel]
             err = np.abs(zg - zc).max(1)
-            pick = (sg == 2) | ((sg == 1) & (sc == 1) & (err > 1e-7))
+            pick = (sg == 2) | (sg == -10) | ((sg == 1) & (sc == 1) & (err > 1e-7))
             print(f"round {k}: status 2 {int((st == 2).sum())}; C status on them {sc[sg == 2].tolist()}; "
                   f"sample both-solved max err {err[(sg == 1) & (sc == 1)].max() if ((sg == 1) & (sc == 1)).any() else 0:.2e}",
                   flush=True)
