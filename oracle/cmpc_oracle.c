@@ -88,6 +88,9 @@ static double nmax(double a, double b) { return (a > b || a != a) ? a : b; }
 #ifdef DD_COUNT
 long cmpc_dd_iters = 0; /* lab: double-double iterations */
 #endif
+#ifdef POLISH_AT
+long lab_pol_tried = 0, lab_pol_ok = 0; /* lab: polish attempts at iteration POLISH_AT, successes */
+#endif
 #ifdef GONDZIO
 long cmpc_gz_solves = 0; /* lab: corrector solves performed */
 #endif
@@ -1648,6 +1651,24 @@ static int solve_one(const shared_t* S, const agent_t* a, double tol, int max_it
                 nrd / gscale, nrs / qs_max, nrp / scale_p, merit);
 #endif
         if (merit < tol) { stop = 1; break; }
+#ifdef POLISH_AT
+        /* lab: one polish attempt from the iterate of iteration POLISH_AT (the condensed method) */
+        if (!S->newton && it == POLISH_AT) {
+            double pk;
+            const double pm = polish_one(S, a, wk, tol, U, sig, t, lam, wk->dU, wk->dsig, &pk);
+#pragma omp atomic
+            lab_pol_tried += 1;
+            if (pm < tol) {
+#pragma omp atomic
+                lab_pol_ok += 1;
+                memcpy(U, wk->dU, sizeof(double) * n);
+                memcpy(sig, wk->dsig, sizeof(double) * N * ns);
+                kkt = pk;
+                stop = 1;
+                break;
+            }
+        }
+#endif
         /* near-converged but no progress for STALL_ITERS iterations: rounding floor reached */
         if (best_m < 1e3 * tol && it - best_it >= STALL_ITERS) {
             stop = 3;
