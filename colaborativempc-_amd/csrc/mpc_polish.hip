@@ -36,7 +36,7 @@ constexpr int kPolishPasses = 2;
 
 struct PolLayout {
     int cst, Lh, Y, S, G0, G1, sA, sB, sC, sp, U, sig, Uc, sc, Ub, sb, X, ybar, w, lamp, tp, rp, rd, gU, rsig, zv,
-        gz, lA, rA, dl, red, in, Ar;
+        gz, rdH, rdS, lA, rA, dl, red, in, Ar;
     int amax, total;
 };
 
@@ -53,7 +53,8 @@ __host__ __device__ inline PolLayout pol_layout_for(const MpcConst& c, int amax)
     L.cst = take(mpc_const_used_doubles(c));
     const int mc = c.mc, nu = c.nu;
     L.Lh = take(n * (n + 1) / 2);                       // packed lower triangle
-    L.Y = take(amax * n > nx * n ? amax * n : nx * n);  // also 2Q Gamma while H is built
+    const int sY = N * nx * nx;                         // also S_k while H is built
+    L.Y = take(amax * (n | 1) > sY ? amax * (n | 1) : sY);  // rows at an odd stride (LDS banks)
     const int sS = amax * (amax + 1) / 2;
     L.S = take(sS > 2 * nx * n ? sS : 2 * nx * n);      // also Gamma's ping-pong while H is built
     L.G0 = L.S;
@@ -79,6 +80,8 @@ __host__ __device__ inline PolLayout pol_layout_for(const MpcConst& c, int amax)
     L.rsig = take(N * ns);
     L.zv = take(n);
     L.gz = take(n);
+    L.rdH = take(n);
+    L.rdS = take(amax);
     L.lA = take(amax);
     L.rA = take(amax);
     L.dl = take(amax);
@@ -130,42 +133,103 @@ __device__ bool wave_chol(double* M, int n, Idx idx) {
         if (l == 0) M[idx(j, j)] = s;
         for (int i = j + 1 + l; i < n; i += kWave) M[idx(i, j)] *= inv;
         wsync();
+        // row i's entries j+1..i are contiguous (packed lower storage): eight at a time, every load
+        // of a group issued before its stores (a column-in-registers variant with readlane broadcasts
+        // measured 2.4x slower)
         for (int i = j + 1 + l; i < n; i += kWave) {
             const double lij = M[idx(i, j)];
-            for (int p = j + 1; p <= i; ++p) M[idx(i, p)] -= lij * M[idx(p, j)];
+            double* r = M + idx(i, 0);
+            int p = j + 1;
+            for (; p + 8 <= i + 1; p += 8) {
+                double cv[8], rv[8];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) cv[u] = M[idx(p + u, j)];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) rv[u] = r[p + u];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) r[p + u] = rv[u] - lij * cv[u];
+            }
+            for (; p <= i; ++p) r[p] -= lij * M[idx(p, j)];
         }
         wsync();
     }
     return true;
 }
 
-// forward substitution L x = b in place (x overwrites b), wave 0 only (n <= 128: two rows a lane)
-template <class Idx>
-__device__ void wave_fsub(const double* M, int n, Idx idx, double* x) {
-    const int l = threadIdx.x;
-    for (int p = 0; p < n; ++p) {
-        const double xp = x[p] / M[idx(p, p)];
-        wsync();
-        if (l == 0) x[p] = xp;
-        for (int i = p + 1 + l; i < n; i += kWave) x[i] -= M[idx(i, p)] * xp;
-        wsync();
+// the same factorisation by the whole workgroup (packed lower storage, rows contiguous): the trailing
+// update of step j as (row, 8-column chunk) work items over the 256 threads, three barriers a step
+__device__ bool block_chol_packed(double* M, int n) {
+    const int tid = threadIdx.x;
+    auto idx = [](int i, int j) { return i * (i + 1) / 2 + j; };
+    for (int j = 0; j < n; ++j) {
+        const double d = M[idx(j, j)];
+        if (!(d > 0.0)) return false;  // uniform: every thread read the same value
+        const double s = sqrt(d);
+        const double inv = 1.0 / s;
+        __syncthreads();
+        if (tid == 0) M[idx(j, j)] = s;
+        for (int i = j + 1 + tid; i < n; i += kPT) M[idx(i, j)] *= inv;
+        __syncthreads();
+        const int rows = n - 1 - j, chunks = (rows + 7) >> 3;
+        for (int item = tid; item < rows * chunks; item += kPT) {
+            const int i = j + 1 + item / chunks, p0 = j + 1 + 8 * (item % chunks);
+            if (p0 > i) continue;
+            const double lij = M[idx(i, j)];
+            double* r = M + idx(i, 0);
+            const int pe = i + 1 < p0 + 8 ? i + 1 : p0 + 8;
+            if (pe - p0 == 8) {
+                double cv[8], rv[8];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) cv[u] = M[idx(p0 + u, j)];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) rv[u] = r[p0 + u];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) r[p0 + u] = rv[u] - lij * cv[u];
+            } else {
+                for (int p = p0; p < pe; ++p) r[p] -= lij * M[idx(p, j)];
+            }
+        }
+        __syncthreads();
     }
+    return true;
 }
-// backward substitution L' x = b in place, wave 0 only
+
+// forward substitution L x = b in place (x overwrites b), wave 0 only, n <= 128: lane l keeps rows
+// l and l + 64 in registers; the solved entry is broadcast by readlane (no LDS round trip in the
+// chain); rd = the reciprocal diagonal
 template <class Idx>
-__device__ void wave_bsub(const double* M, int n, Idx idx, double* x) {
+__device__ void wave_fsub(const double* M, const double* rd, int n, Idx idx, double* x) {
     const int l = threadIdx.x;
-    for (int p = n - 1; p >= 0; --p) {
-        const double xp = x[p] / M[idx(p, p)];
-        wsync();
-        if (l == 0) x[p] = xp;
-        for (int i = l; i < p; i += kWave) x[i] -= M[idx(p, i)] * xp;
-        wsync();
+    double x0 = l < n ? x[l] : 0.0, x1 = l + kWave < n ? x[l + kWave] : 0.0;
+    for (int p = 0; p < n; ++p) {
+        const double xp = (p < kWave ? readlane_d(x0, p) : readlane_d(x1, p - kWave)) * rd[p];
+        if (l == p) x0 = xp;
+        if (l + kWave == p) x1 = xp;
+        if (l > p && l < n) x0 -= M[idx(l, p)] * xp;
+        if (l + kWave > p && l + kWave < n) x1 -= M[idx(l + kWave, p)] * xp;
     }
+    if (l < n) x[l] = x0;
+    if (l + kWave < n) x[l + kWave] = x1;
+}
+// backward substitution L' x = b in place, wave 0 only (as above)
+template <class Idx>
+__device__ void wave_bsub(const double* M, const double* rd, int n, Idx idx, double* x) {
+    const int l = threadIdx.x;
+    double x0 = l < n ? x[l] : 0.0, x1 = l + kWave < n ? x[l + kWave] : 0.0;
+    for (int p = n - 1; p >= 0; --p) {
+        const double xp = (p < kWave ? readlane_d(x0, p) : readlane_d(x1, p - kWave)) * rd[p];
+        if (l == p) x0 = xp;
+        if (l + kWave == p) x1 = xp;
+        if (l < p) x0 -= M[idx(p, l)] * xp;
+        if (l + kWave < p) x1 -= M[idx(p, l + kWave)] * xp;
+    }
+    if (l < n) x[l] = x0;
+    if (l + kWave < n) x[l + kWave] = x1;
 }
 
 struct PolCtx {
     const MpcConst& c;
+    int nx;  // the state dimension (a compile-time constant in the NX instantiations)
     const PolLayout& L;
     double* sm;
     const double* A;
@@ -177,9 +241,9 @@ struct PolCtx {
 };
 
 // X = simulation of (x0, U) (wave 0; the other waves wait at the caller's barrier)
-__device__ void pol_fwd(const PolCtx& q, const double* U, double* X) {
+__device__ __forceinline__ void pol_fwd(const PolCtx& q, const double* U, double* X) {
     const MpcConst& c = q.c;
-    const int nx = c.nx, nu = c.nu, N = c.N, l = threadIdx.x;
+    const int nx = q.nx, nu = c.nu, N = c.N, l = threadIdx.x;
     if (l >= kWave) return;
     if (l < nx) X[l] = q.x0[l];
     wsync();
@@ -198,9 +262,9 @@ __device__ void pol_fwd(const PolCtx& q, const double* U, double* X) {
 
 // out_k = B_k' psi_{k+1}, psi_N = y_N, psi_k = y_k + A_k' psi_{k+1} (wave 0; psi kept in y's slots,
 // y is overwritten)
-__device__ void pol_adjoint(const PolCtx& q, double* y, double* out) {
+__device__ __forceinline__ void pol_adjoint(const PolCtx& q, double* y, double* out) {
     const MpcConst& c = q.c;
-    const int nx = c.nx, nu = c.nu, N = c.N, l = threadIdx.x;
+    const int nx = q.nx, nu = c.nu, N = c.N, l = threadIdx.x;
     if (l >= kWave) return;
     for (int k = N - 1; k >= 0; --k) {
         const double* psi = y + (k + 1) * nx;
@@ -220,9 +284,9 @@ __device__ void pol_adjoint(const PolCtx& q, double* y, double* out) {
     }
 }
 
-__device__ double pol_row(const PolCtx& q, const double* X, const double* U, const double* sg, int r) {
+__device__ __forceinline__ double pol_row(const PolCtx& q, const double* X, const double* U, const double* sg, int r) {
     const MpcConst& c = q.c;
-    const int nx = c.nx, mc = c.mc, ms = c.ms;
+    const int nx = q.nx, mc = c.mc, ms = c.ms;
     if (r < ms) {
         const int k = r / mc, rr = r - k * mc;
         const double* cr = q.C + (size_t)r * nx;
@@ -238,12 +302,12 @@ __device__ double pol_row(const PolCtx& q, const double* X, const double* U, con
 
 // The interior-point residuals at (U, sigma, t, lambda) into rd / rsig / rp (cmpc_oracle.c merit_at);
 // X is re-simulated.  With `full`, returns the merit max(res, 1e4 mu) and *kkt = max(res, mu).
-__device__ double pol_residuals(const PolCtx& q, const double* U, const double* sg, const double* t,
+__device__ __forceinline__ double pol_residuals(const PolCtx& q, const double* U, const double* sg, const double* t,
                                 const double* lam, const int* act_w, bool full, double* kkt) {
     const MpcConst& c = q.c;
     const PolLayout& L = q.L;
     double* sm = q.sm;
-    const int nx = c.nx, nu = c.nu, N = c.N, ns = c.ns, mc = c.mc, ms = c.ms, m = c.m, n = c.n;
+    const int nx = q.nx, nu = c.nu, N = c.N, ns = c.ns, mc = c.mc, ms = c.ms, m = c.m, n = c.n;
     const int tid = threadIdx.x;
     double *X = sm + L.X, *ybar = sm + L.ybar, *rd = sm + L.rd, *gU = sm + L.gU, *rsig = sm + L.rsig,
            *rp = sm + L.rp, *red = sm + L.red;
@@ -327,6 +391,8 @@ __device__ double pol_residuals(const PolCtx& q, const double* U, const double* 
     return nmax(res, 1e4 * mu);
 }
 
+// NXT: the state dimension as a compile-time constant (0: the runtime c.nx)
+template <int NXT>
 __global__ __launch_bounds__(kPT) void mpc_polish_kernel(const MpcConst c_arg, const MpcPtrs P) {
     extern __shared__ __attribute__((aligned(16))) double sm[];
     const int b = blockIdx.x;
@@ -344,8 +410,8 @@ __global__ __launch_bounds__(kPT) void mpc_polish_kernel(const MpcConst c_arg, c
     }
     __syncthreads();
     const MpcConst& c = *reinterpret_cast<const MpcConst*>(sm + L.cst);
-    const int nx = c.nx, nu = c.nu, N = c.N, ns = c.ns, mc = c.mc, ms = c.ms, m = c.m, n = c.n;
-    const int amax = L.amax;
+    const int nx = NXT ? NXT : c.nx, nu = c.nu, N = c.N, ns = c.ns, mc = c.mc, ms = c.ms, m = c.m, n = c.n;
+    const int amax = L.amax, ldY = n | 1;
     // the stage data (A, B, C rows, linear cost) staged in LDS once: every recursion below reads it
     {
         const double* gA = P.A + (size_t)b * N * nx * nx;
@@ -357,7 +423,7 @@ __global__ __launch_bounds__(kPT) void mpc_polish_kernel(const MpcConst c_arg, c
         for (int i = tid; i < N * mc * nx; i += kPT) sm[L.sC + i] = gC[i];
         for (int i = tid; i < (N + 1) * nx; i += kPT) sm[L.sp + i] = gp[i];
     }
-    const PolCtx q{c, L, sm, sm + L.sA, sm + L.sB, P.x0 + (size_t)b * nx, P.up + (size_t)b * nu, sm + L.sp, sm + L.sC};
+    const PolCtx q{c, nx, L, sm, sm + L.sA, sm + L.sB, P.x0 + (size_t)b * nx, P.up + (size_t)b * nu, sm + L.sp, sm + L.sC};
     const double* hC = P.h + (size_t)b * N * mc;
     const double best_m = flag == 2.0 ? hd[1] : c_arg.tol;  // (flag 1: slot 1 holds the iterations done)
     const int ht = (int)hand_t(c);
@@ -386,45 +452,89 @@ __global__ __launch_bounds__(kPT) void mpc_polish_kernel(const MpcConst c_arg, c
     for (int i = tid; i < n * (n + 1) / 2; i += kPT) Lh[i] = 0.0;
     for (int i = tid; i < nx * n; i += kPT) sm[L.G0 + i] = 0.0;
     __syncthreads();
+    // diagnostic section clocks (MpcPtrs::stamps slots 9..15, thread 0): init, H build, H factor,
+    // active rows (Y), S build + factor, Newton steps + evaluation, output
+    unsigned long long tsum[7] = {0, 0, 0, 0, 0, 0, 0}, t_a = P.stamps ? clock64_() : 0;
+#define PSTAMP(slot)                         \
+    if (P.stamps && tid == 0) {              \
+        const unsigned long long t_b = clock64_(); \
+        tsum[slot] += t_b - t_a;             \
+        t_a = t_b;                           \
+    }
+    PSTAMP(0);
     // ---- H = sum_k Gamma_{k+1}' 2Q Gamma_{k+1} + the 2R / 2dR band (lower triangle), H = L L' ----
+    // by the backward recursion S_N = 2Q, S_k = 2Q + A_k' S_{k+1} A_k (S_{i+1} = the cost-to-go
+    // weight of the state after input stage i): for i >= j the block
+    //     H_ij = B_i' S_{i+1} A_i A_{i-1} ... A_{j+1} B_j,
+    // one thread per row of H carrying r = B_i[:, a]' S_{i+1} Phi back over the stages
     {
-        double* G = sm + L.G0;
-        double* Gn = sm + L.G1;
-        double* WG = Y;
-        for (int k = 0; k < N; ++k) {
-            const double* Ak = q.A + k * nx * nx;
-            const double* Bk = q.B + k * nx * nu;
-            const int ncol = (k + 1) * nu;
-            for (int e = tid; e < nx * n; e += kPT) {
-                const int s = e / n, col = e - s * n;
-                double v = 0.0;
-                if (col < ncol) {
-                    for (int t2 = 0; t2 < nx; ++t2) v += Ak[s * nx + t2] * G[t2 * n + col];
-                    if (col >= k * nu) v += Bk[s * nu + col - k * nu];
+        double* Sk = Y;                  // S_1 .. S_N (N nx^2)
+        double* T = sm + L.G0;           // S_{k+1} A_k
+        if (tid < kWave) {               // wave 0 alone: compiler fences instead of barriers
+            const int l = tid;
+            for (int e = l; e < nx * nx; e += kWave) Sk[(N - 1) * nx * nx + e] = 2.0 * c.Q[e];
+            wsync();
+            for (int k = N - 1; k >= 1; --k) {
+                const double* Ak = q.A + k * nx * nx;
+                const double* Sn = Sk + k * nx * nx;
+                for (int e = l; e < nx * nx; e += kWave) {
+                    const int r = e / nx, cc = e - r * nx;
+                    double v = 0.0;
+                    for (int u = 0; u < nx; ++u) v += Sn[r * nx + u] * Ak[u * nx + cc];
+                    T[e] = v;
                 }
-                Gn[e] = v;
+                wsync();
+                for (int e = l; e < nx * nx; e += kWave) {
+                    const int r = e / nx, cc = e - r * nx;
+                    double v = 2.0 * c.Q[e];
+                    for (int u = 0; u < nx; ++u) v += Ak[u * nx + r] * T[u * nx + cc];
+                    Sk[(k - 1) * nx * nx + e] = v;
+                }
+                wsync();
             }
-            __syncthreads();
-            for (int e = tid; e < nx * n; e += kPT) {
-                const int s = e / n, col = e - s * n;
-                double v = 0.0;
-                if (col < ncol)
-                    for (int u = 0; u < nx; ++u) v += 2.0 * c.Q[s * nx + u] * Gn[u * n + col];
-                WG[e] = v;
+            // lane `row` (n <= 64) carries r = B_i[:, a]' S_{i+1} A_i ... back over the stages, every lane
+            // at the same stage (broadcast reads of A_j, B_j)
+            const int row = l, i2 = row / nu, a = row - i2 * nu;
+            double v[CMPC_MAX_NX], w2[CMPC_MAX_NX];
+            double* Hrow = Lh + row * (row + 1) / 2;
+            for (int j2 = N - 1; j2 >= 0; --j2) {
+                const double* Bj = q.B + j2 * nx * nu;
+                if (row < n && i2 == j2) {  // r = B_i[:, a]' S_{i+1}
+                    const double* S1 = Sk + i2 * nx * nx;
+#pragma unroll
+                    for (int cc = 0; cc < CMPC_MAX_NX; ++cc) {
+                        double h = 0.0;
+                        if (cc < nx)
+                            for (int u = 0; u < nx; ++u) h += Bj[u * nu + a] * S1[u * nx + cc];
+                        v[cc] = h;
+                    }
+                }
+                if (row < n && i2 >= j2) {
+                    for (int b2 = 0; b2 < nu; ++b2) {
+                        const int col = j2 * nu + b2;
+                        double h = 0.0;
+#pragma unroll
+                        for (int u = 0; u < CMPC_MAX_NX; ++u)
+                            if (u < nx) h += v[u] * Bj[u * nu + b2];
+                        if (col <= row) Hrow[col] = h;
+                    }
+                    if (j2 > 0) {  // r <- r A_j
+                        const double* Aj = q.A + j2 * nx * nx;
+#pragma unroll
+                        for (int t2 = 0; t2 < CMPC_MAX_NX; ++t2) {
+                            double h = 0.0;
+#pragma unroll
+                            for (int u = 0; u < CMPC_MAX_NX; ++u)
+                                if (u < nx && t2 < nx) h += v[u] * Aj[u * nx + t2];
+                            w2[t2] = h;
+                        }
+#pragma unroll
+                        for (int u = 0; u < CMPC_MAX_NX; ++u) v[u] = w2[u];
+                    }
+                }
             }
-            __syncthreads();
-            for (int e = tid; e < ncol * ncol; e += kPT) {
-                const int c1 = e / ncol, c2 = e - c1 * ncol;
-                if (c2 > c1) continue;
-                double v = 0.0;
-                for (int s = 0; s < nx; ++s) v += Gn[s * n + c1] * WG[s * n + c2];
-                Lh[c1 * (c1 + 1) / 2 + c2] += v;
-            }
-            __syncthreads();
-            double* tmp = G;
-            G = Gn;
-            Gn = tmp;
         }
+        __syncthreads();
         for (int ci = tid; ci < n; ci += kPT) {
             const int k = ci / nu, i = ci - k * nu;
             for (int j = 0; j < nu; ++j) {
@@ -436,15 +546,19 @@ __global__ __launch_bounds__(kPT) void mpc_polish_kernel(const MpcConst c_arg, c
         }
         __syncthreads();
     }
+    PSTAMP(1);
     auto ih = [](int i, int j) { return i * (i + 1) / 2 + j; };
     auto is = [](int i, int j) { return i * (i + 1) / 2 + j; };
     int& flag_s = *reinterpret_cast<int*>(sm + L.red + 14);
-    if (tid < kWave) {
-        const bool ok = wave_chol(Lh, n, ih);
+    {
+        const bool ok = block_chol_packed(Lh, n);
         if (tid == 0) flag_s = ok ? 1 : 0;
+        if (ok)
+            for (int i = tid; i < n; i += kPT) sm[L.rdH + i] = 1.0 / Lh[ih(i, i)];
     }
     __syncthreads();
     const bool h_ok = flag_s != 0;
+    PSTAMP(2);
     __syncthreads();
     double best = INFINITY, best_kkt = INFINITY;
     int& nA_s = *reinterpret_cast<int*>(sm + L.red + 12);
@@ -472,7 +586,7 @@ __global__ __launch_bounds__(kPT) void mpc_polish_kernel(const MpcConst c_arg, c
         // G_A rows by adjoint recursions (one thread a row), then Y rows = L^-1 g (in place)
         for (int qa = tid; qa < nA; qa += kPT) {
             const int r = Ar[qa];
-            double* g = Y + (size_t)qa * n;
+            double* g = Y + (size_t)qa * ldY;
             for (int i = 0; i < n; ++i) g[i] = 0.0;
             if (r < ms) {
                 const int k = r / mc;
@@ -499,13 +613,22 @@ __global__ __launch_bounds__(kPT) void mpc_polish_kernel(const MpcConst c_arg, c
                 const int qq = r - ms;
                 g[qq >> 1] = (qq & 1) ? -1.0 : 1.0;
             }
-            for (int i = 0; i < n; ++i) {
-                double v = g[i];
-                for (int p2 = 0; p2 < i; ++p2) v -= Lh[i * (i + 1) / 2 + p2] * g[p2];
-                g[i] = v / Lh[i * (i + 1) / 2 + i];
+            for (int i = 0; i < n; ++i) {  // four partial sums: the loads of a group go out together
+                const double* Li = Lh + i * (i + 1) / 2;
+                double v0 = g[i], v1 = 0.0, v2 = 0.0, v3 = 0.0;
+                int p2 = 0;
+                for (; p2 + 4 <= i; p2 += 4) {
+                    v0 -= Li[p2] * g[p2];
+                    v1 -= Li[p2 + 1] * g[p2 + 1];
+                    v2 -= Li[p2 + 2] * g[p2 + 2];
+                    v3 -= Li[p2 + 3] * g[p2 + 3];
+                }
+                for (; p2 < i; ++p2) v0 -= Li[p2] * g[p2];
+                g[i] = ((v0 + v1) + (v2 + v3)) / Li[i];
             }
         }
         __syncthreads();
+        PSTAMP(3);
         // S = Y Y' + E (packed lower)
         for (int e = tid; e < nA * (nA + 1) / 2; e += kPT) {
             int a = (int)((sqrt(8.0 * e + 1.0) - 1.0) * 0.5);
@@ -513,7 +636,7 @@ __global__ __launch_bounds__(kPT) void mpc_polish_kernel(const MpcConst c_arg, c
             while ((a + 1) * (a + 2) / 2 <= e) ++a;
             const int b2 = e - a * (a + 1) / 2;
             double v = 0.0;
-            for (int i = 0; i < n; ++i) v += Y[(size_t)a * n + i] * Y[(size_t)b2 * n + i];
+            for (int i = 0; i < n; ++i) v += Y[(size_t)a * ldY + i] * Y[(size_t)b2 * ldY + i];
             const int r = Ar[a], r2 = Ar[b2];
             if (r < ms && r2 < ms && r / mc == r2 / mc) {
                 const int j = c.row_slack[r % mc];
@@ -522,11 +645,14 @@ __global__ __launch_bounds__(kPT) void mpc_polish_kernel(const MpcConst c_arg, c
             Sm[e] = v;
         }
         __syncthreads();
-        if (tid < kWave) {
-            const bool ok = wave_chol(Sm, nA, is);
+        {
+            const bool ok = block_chol_packed(Sm, nA);
             if (tid == 0) flag_s = ok ? 1 : 0;
+            if (ok)
+                for (int i = tid; i < nA; i += kPT) sm[L.rdS + i] = 1.0 / Sm[is(i, i)];
         }
         __syncthreads();
+        PSTAMP(4);
         if (!flag_s) break;
         // Newton steps from (U, sigma, lambda_A)
         for (int i = tid; i < n; i += kPT) Uc[i] = U[i];
@@ -555,26 +681,26 @@ __global__ __launch_bounds__(kPT) void mpc_polish_kernel(const MpcConst c_arg, c
             }
             for (int i = tid; i < n; i += kPT) zv[i] = rd[i];
             __syncthreads();
-            if (tid < kWave) wave_fsub(Lh, n, ih, zv);  // z = L^-1 rU
+            if (tid < kWave) wave_fsub(Lh, sm + L.rdH, n, ih, zv);  // z = L^-1 rU
             __syncthreads();
             for (int qa = tid; qa < nA; qa += kPT) {
                 double v = rA[qa];
-                for (int i = 0; i < n; ++i) v -= Y[(size_t)qa * n + i] * zv[i];
+                for (int i = 0; i < n; ++i) v -= Y[(size_t)qa * ldY + i] * zv[i];
                 dl[qa] = v;
             }
             __syncthreads();
             if (tid < kWave) {
-                wave_fsub(Sm, nA, is, dl);
-                wave_bsub(Sm, nA, is, dl);
+                wave_fsub(Sm, sm + L.rdS, nA, is, dl);
+                wave_bsub(Sm, sm + L.rdS, nA, is, dl);
             }
             __syncthreads();
             for (int i = tid; i < n; i += kPT) {  // z + Y dlam
                 double v = zv[i];
-                for (int qa = 0; qa < nA; ++qa) v += Y[(size_t)qa * n + i] * dl[qa];
+                for (int qa = 0; qa < nA; ++qa) v += Y[(size_t)qa * ldY + i] * dl[qa];
                 gz[i] = v;
             }
             __syncthreads();
-            if (tid < kWave) wave_bsub(Lh, n, ih, gz);  // H^-1 (rU + G_A' dlam)
+            if (tid < kWave) wave_bsub(Lh, sm + L.rdH, n, ih, gz);  // H^-1 (rU + G_A' dlam)
             __syncthreads();
             for (int i = tid; i < n; i += kPT) Uc[i] -= gz[i];
             for (int e = tid; e < N * ns; e += kPT) {
@@ -606,6 +732,7 @@ __global__ __launch_bounds__(kPT) void mpc_polish_kernel(const MpcConst c_arg, c
             mp = pol_residuals(q, Uc, sc, tp, lamp, in, true, &kk);
             if (mp < c.tol) break;
         }
+        PSTAMP(5);
         if (mp < best) {
             best = mp;
             best_kkt = kk;
@@ -638,6 +765,7 @@ __global__ __launch_bounds__(kPT) void mpc_polish_kernel(const MpcConst c_arg, c
         st[3] = (unsigned long long)__double_as_longlong(best_m);
         st[4] = h_ok ? 1ull : 0ull;
         for (int i = 0; i < 3; ++i) st[5 + i] = (unsigned long long)__double_as_longlong(sm[L.red + 8 + i]);
+        for (int i = 0; i < 6; ++i) st[9 + i] = tsum[i];
     }
     if (!(best < best_m)) {
         if (tid == 0 && flag == 2.0) hd[0] = 0.0;  // (flag 1 stays: the Riccati rescue takes the agent)
@@ -674,15 +802,25 @@ __global__ __launch_bounds__(kPT) void mpc_polish_kernel(const MpcConst c_arg, c
 
 size_t mpc_polish_lds_bytes(const MpcConst& c) { return sizeof(double) * (size_t)pol_layout(c).total; }
 
+template <int NXT>
+static hipError_t polish_launch_t(const MpcConst& c, const MpcPtrs& p, int batch, hipStream_t s, size_t lds) {
+    hipError_t e = hipFuncSetAttribute((const void*)mpc_polish_kernel<NXT>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       (int)lds);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(mpc_polish_kernel<NXT>, dim3(batch), dim3(kPT), lds, s, c, p);
+    return hipGetLastError();
+}
+
 hipError_t mpc_polish_launch(const MpcConst& c, const MpcPtrs& p, int batch, hipStream_t s) {
     if (batch == 0) return hipSuccess;
     const size_t lds = mpc_polish_lds_bytes(c);
     if (lds > kMaxLdsBytes) return hipErrorInvalidValue;
-    hipError_t e = hipFuncSetAttribute((const void*)mpc_polish_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                       (int)lds);
-    if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(mpc_polish_kernel, dim3(batch), dim3(kPT), lds, s, c, p);
-    return hipGetLastError();
+    switch (c.nx) {  // the reference's agent (9), the BASELINE double-integrator families (4, 6)
+        case 9: return polish_launch_t<9>(c, p, batch, s, lds);
+        case 4: return polish_launch_t<4>(c, p, batch, s, lds);
+        case 6: return polish_launch_t<6>(c, p, batch, s, lds);
+        default: return polish_launch_t<0>(c, p, batch, s, lds);
+    }
 }
 
 }  // namespace cmpc
