@@ -118,46 +118,10 @@ __device__ double block_sum(double v, double* red) {
     return (red[4] + red[5]) + (red[6] + red[7]);
 }
 
-// in-place Cholesky of an n x n matrix (lower triangle, element (i, j) at M[idx(i, j)]), right-looking,
-// by wave 0 alone (a wave's LDS operations execute in order: compiler fences, no barriers); lane l
-// owns rows l, l + 64, ...; returns false (on every lane) when a pivot is not positive
-template <class Idx>
-__device__ bool wave_chol(double* M, int n, Idx idx) {
-    const int l = threadIdx.x;
-    for (int j = 0; j < n; ++j) {
-        const double d = M[idx(j, j)];
-        if (!(d > 0.0)) return false;
-        const double s = sqrt(d);
-        const double inv = 1.0 / s;
-        wsync();
-        if (l == 0) M[idx(j, j)] = s;
-        for (int i = j + 1 + l; i < n; i += kWave) M[idx(i, j)] *= inv;
-        wsync();
-        // row i's entries j+1..i are contiguous (packed lower storage): eight at a time, every load
-        // of a group issued before its stores (a column-in-registers variant with readlane broadcasts
-        // measured 2.4x slower)
-        for (int i = j + 1 + l; i < n; i += kWave) {
-            const double lij = M[idx(i, j)];
-            double* r = M + idx(i, 0);
-            int p = j + 1;
-            for (; p + 8 <= i + 1; p += 8) {
-                double cv[8], rv[8];
-#pragma unroll
-                for (int u = 0; u < 8; ++u) cv[u] = M[idx(p + u, j)];
-#pragma unroll
-                for (int u = 0; u < 8; ++u) rv[u] = r[p + u];
-#pragma unroll
-                for (int u = 0; u < 8; ++u) r[p + u] = rv[u] - lij * cv[u];
-            }
-            for (; p <= i; ++p) r[p] -= lij * M[idx(p, j)];
-        }
-        wsync();
-    }
-    return true;
-}
-
-// the same factorisation by the whole workgroup (packed lower storage, rows contiguous): the trailing
-// update of step j as (row, 8-column chunk) work items over the 256 threads, three barriers a step
+// in-place Cholesky of an n x n matrix by the whole workgroup (packed lower storage, rows contiguous):
+// the trailing update of step j as (row, 8-column chunk) work items over the 256 threads, three
+// barriers a step; returns false when a pivot is not positive.  (Tried: one wave with fences, 8-wide
+// chunks — 10 % slower; the column in registers with readlane broadcasts — 2.4x slower.)
 __device__ bool block_chol_packed(double* M, int n) {
     const int tid = threadIdx.x;
     auto idx = [](int i, int j) { return i * (i + 1) / 2 + j; };

@@ -54,3 +54,27 @@ def test_gpu_polish_matches_c_restatement(gpu_ctx):
     assert (st == cmpc.CMPC_SOLVED).all(), st
     assert (kkt < 1e-9).all(), kkt
     assert np.abs(z - z1).max() < 1e-6
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,N,nb,dim,tol", [(64, 20, 2, 2, 1e-13), (64, 10, 2, 3, 1e-15)])
+def test_gpu_polish_double_integrator_families(gpu_ctx, n, N, nb, dim, tol):
+    """The polish kernel's nx = 4 and nx = 6 instantiations (the BASELINE double-integrator families):
+    at a tolerance below the rounding floor (1e-13, 1e-15) the solves stop at the floor, so rescue + polish
+    runs on them; statuses and z match the C restatement of the same policy (to 1e-6), and the
+    polished solves' KKT residuals are no worse than without the polish."""
+    import cmpc
+    from cmpc import scenarios as S
+    from oracle import cmpc_oracle as CO
+    from oracle import synth
+
+    sc = S.make_di(n, N, nb, dim)
+    P = synth.structured(sc.shared, sc.params, sc.A, sc.B, sc.x0, sc.u_prev, sc.lane, sc.nbr, sc.traj, np.arange(n))
+    z0, k0, i0, s0 = cmpc.solve_mpc(P, gpu_ctx, tol=tol, rescue=True)
+    z1, k1, i1, s1 = cmpc.solve_mpc(P, gpu_ctx, tol=tol, rescue=True, polish=True)
+    zc, kc, ic, sc_ = CO.solve_batch_rescue(P, tol=tol, nthreads=4, polish=True)
+    print(f"dim {dim}: status without polish {np.unique(s0, return_counts=True)}, with {np.unique(s1, return_counts=True)}, "
+          f"C {np.unique(sc_, return_counts=True)}; kkt {k0.max():.1e} -> {k1.max():.1e}; |z - z_cpu| {np.abs(z1 - zc).max():.1e}")
+    assert np.isin(s1, (cmpc.CMPC_SOLVED, cmpc.CMPC_SOLVED_INACCURATE)).all()
+    assert np.abs(z1 - zc).max() < 1e-6
+    assert k1.max() <= max(k0.max(), 1e-12)
