@@ -766,7 +766,11 @@ int mpc_prepare(const cmpc_mpc_dims* d, const cmpc_mpc_weights* wt, const cmpc_o
                     ? 1 : 0;
     c->finish = (c->rescue && (o->flags & CMPC_FLAG_FINISH)) ? 1 : 0;
     c->polish = 0;
-    c->polish = (c->rescue && (o->flags & CMPC_FLAG_POLISH) && mpc_polish_lds_bytes(*c) <= kMaxLdsBytes) ? 1 : 0;
+    // (mpc_polish.hip: one lane per condensed variable in its H build, so n <= 64 — every condensed
+    // solve, which is what carries the rescue image)
+    c->polish = (c->rescue && (o->flags & CMPC_FLAG_POLISH) && c->n <= kWave &&
+                 mpc_polish_lds_bytes(*c) <= kMaxLdsBytes)
+                    ? 1 : 0;
     for (int i = 0; i < d->nu; ++i) {
         c->u_ub[i] = wt->u_ub[i];
         c->u_lb[i] = wt->u_lb[i];

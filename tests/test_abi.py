@@ -54,6 +54,9 @@ def test_plan_occupancy_of_the_bench_configs():
     assert plan(S.di_shared(2, 30, 2), 1024, generic=True)["solver"] == "condensed"
     with pytest.raises(cmpc.CmpcError):   # no fp32 path for nb = 3 at these dimensions
         plan(S.di_shared(2, 20, 3), 16, fp32=True)
+    # CMPC_FLAG_POLISH (with CMPC_FLAG_RESCUE) is a known option bit: the condensed plan is unchanged
+    pp = plan(S.di_shared(2, 30, 2), 1024, rescue=True, polish=True)
+    assert pp["solver"] == "condensed_v3" and pp["wg_per_cu"] == 4, pp
 
 
 def test_no_cpu_fallback_without_device():
