@@ -326,7 +326,7 @@ def test_fused_round_bit_equal_to_build_then_solve(gpu_ctx, n, N, nb, dim):
         torch.cuda.synchronize()
         for a in ("z", "kkt", "iters", "status", "traj_all", "x0", "u_prev"):
             assert torch.equal(getattr(F, a), getattr(U, a)), (rnd, a)
-    assert (U.status.cpu().numpy() == 1).mean() > 0.9
+    assert (U.status.cpu().numpy() == 1).mean() >= 0.99
 
 
 def test_deterministic_and_permutation_invariant(gpu_ctx):
@@ -685,8 +685,8 @@ def test_lane_kernel_fp64_vs_c_restatement(gpu_ctx):
     zc, kc, ic, stc = CO.solve_batch(P, nthreads=8, newton=1)
     same = st == stc
     both = (st == 1) & (stc == 1)
-    print(f"lane fp64: status agree {same.mean():.3f}, iterations agree {np.mean(it == ic):.3f}")
-    assert same.mean() >= 0.95 and both.mean() >= 0.85
+    print(f"lane fp64: status agree {same.mean():.3f}, both solved {both.mean():.3f}, iterations agree {np.mean(it == ic):.3f}")
+    assert same.mean() >= 0.97 and both.mean() >= 0.95   # measured 0.984 agree (r04c)
     assert np.abs(z[both] - zc[both]).max() < Z_TOL
 
 
