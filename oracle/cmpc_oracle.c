@@ -1576,6 +1576,24 @@ static int solve_one(const shared_t* S, const agent_t* a, double tol, int max_it
 #endif
 #endif
     for (it = 1; it <= max_iter; ++it) {
+#ifdef POLISH_AT
+        /* lab: one polish attempt from the iterate of iteration POLISH_AT (the condensed method) */
+        if (!S->newton && it == POLISH_AT + 1) {  /* before this iteration's residuals */
+            double pk;
+            const double pm = polish_one(S, a, wk, tol, U, sig, t, lam, wk->dU, wk->dsig, &pk);
+#pragma omp atomic
+            lab_pol_tried += 1;
+            if (pm < tol) {
+#pragma omp atomic
+                lab_pol_ok += 1;
+                memcpy(U, wk->dU, sizeof(double) * n);
+                memcpy(sig, wk->dsig, sizeof(double) * N * ns);
+                kkt = pk;
+                stop = 1;
+                break;
+            }
+        }
+#endif
         /* ---- residuals ---- */
         double* ybar = wk->ybar;
         double gscale = 1.0;
@@ -1651,24 +1669,6 @@ static int solve_one(const shared_t* S, const agent_t* a, double tol, int max_it
                 nrd / gscale, nrs / qs_max, nrp / scale_p, merit);
 #endif
         if (merit < tol) { stop = 1; break; }
-#ifdef POLISH_AT
-        /* lab: one polish attempt from the iterate of iteration POLISH_AT (the condensed method) */
-        if (!S->newton && it == POLISH_AT) {
-            double pk;
-            const double pm = polish_one(S, a, wk, tol, U, sig, t, lam, wk->dU, wk->dsig, &pk);
-#pragma omp atomic
-            lab_pol_tried += 1;
-            if (pm < tol) {
-#pragma omp atomic
-                lab_pol_ok += 1;
-                memcpy(U, wk->dU, sizeof(double) * n);
-                memcpy(sig, wk->dsig, sizeof(double) * N * ns);
-                kkt = pk;
-                stop = 1;
-                break;
-            }
-        }
-#endif
         /* near-converged but no progress for STALL_ITERS iterations: rounding floor reached */
         if (best_m < 1e3 * tol && it - best_it >= STALL_ITERS) {
             stop = 3;
