@@ -6,7 +6,7 @@ reference optimum / the C restatement; builder outputs to fp64 rounding.
 import numpy as np
 import pytest
 
-from conftest import KKT_TOL, LPV_CASES, assert_matches_optimum, golden, lpv_qps, reference_kkt
+from conftest import LPV_CASES, assert_matches_optimum, golden, lpv_qps
 
 pytestmark = pytest.mark.gpu
 
@@ -53,17 +53,12 @@ def test_lpv_batch_matches_reference_optimum(gpu_ctx, name):
         res = bp.solve(np.stack([c["x0"] for c in cs]), np.stack([c["x_last"] for c in cs]),
                        np.stack([c["u_last"] for c in cs]), np.stack([c["u_old"] for c in cs]),
                        xa if xa.shape[2] else None, np.stack([c["pose"] for c in cs]))
-        # solved; or, at the rounding floor of the hardest agents, "solved inaccurate" (OSQP's
-        # status 2, which the reference counts as feasible, LPV_Planner.py:243-249) — then the
-        # returned z must carry its own certificate: reference-form KKT residual <= 1e-6
-        assert np.isin(res["status"], (cmpc.CMPC_SOLVED, cmpc.CMPC_SOLVED_INACCURATE)).all(), res["status"]
+        # every captured QP solved to tol: PlannerLPVBatch runs the rescue + polish policy (OSQP's
+        # polish=True), which finishes the hardest agents' rounding-floor exits (round 3 allowed
+        # status 2 here with a reference-form KKT certificate)
+        assert (res["status"] == cmpc.CMPC_SOLVED).all(), res["status"]
         for a, c in enumerate(cs):
             assert_matches_optimum(res["z"][a], c, Z_TOL)
-            if res["status"][a] != cmpc.CMPC_SOLVED:
-                kkt, cert = reference_kkt(c["P"], c["q"], c["A"], c["l"], c["u"], res["z"][a])
-                print(f"{name}: agent {a} status {res['status'][a]} (rounding floor): reference-form KKT {kkt:.2e}, "
-                      f"|z - z*| {np.abs(res['z'][a] - c['z']).max():.1e}")
-                assert kkt <= KKT_TOL, cert
         if xa.shape[2]:
             np.testing.assert_allclose(res["planes"], np.stack([c["planes"] for c in cs]), rtol=0, atol=1e-14)
 
