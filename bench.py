@@ -459,7 +459,13 @@ def lpv_check_round(bp, R, sample):
              u_prev=R.u_old.cpu().numpy()[sample], qlin=b["qlin"], C=b["C"], h=b["h"])
     finish = bool(bp.opts.flags & 64)   # CMPC_FLAG_FINISH
     polish = bool(bp.opts.flags & 256)  # CMPC_FLAG_POLISH
-    zc, _, _, sc = CO.solve_batch_rescue(P, nthreads=min(16, os.cpu_count() or 1), finish=finish, polish=polish)
+    amax = 0
+    if polish:  # the polish kernel's active-set capacity for this shape (both sides polish the same agents)
+        from cmpc.solver import plan
+
+        amax = plan(P, 1, rescue=True, polish=True)["polish_max_active"]
+    zc, _, _, sc = CO.solve_batch_rescue(P, nthreads=min(16, os.cpu_count() or 1), finish=finish, polish=polish,
+                                         polish_amax=amax)
     return zc, sc, P
 
 
@@ -519,10 +525,11 @@ def lpv_rounds(ctx, replicas=341, rounds=20, warmup=2, rescue=True, check=True, 
     if check:
         R = LPVRounds(bp, *args, **kw)
         rng = np.random.default_rng(11)
-        err, both, n = 0.0, 0, 0
+        err, err_nd, both, n = 0.0, 0.0, 0, 0
         # agents both sides solve whose z differ by more than 1e-6: an interior-point endpoint against a
         # polished one on a degenerate optimum (a weakly active row: the IPM approaches it like sqrt(mu));
-        # each is certified instead by the GPU point's reference-form KKT residual and objective
+        # each is certified in addition by the GPU point's reference-form KKT residual and objective, and
+        # counted; max_abs_err_vs_cpu stays over every both-solved agent
         deg = {"count": 0, "max_ref_kkt_gpu": 0.0, "max_ref_kkt_cpu": 0.0, "max_obj_gap_rel": -np.inf,
                "max_abs_err": 0.0}
         for k in range(warmup + rounds):
@@ -535,6 +542,8 @@ def lpv_rounds(ctx, replicas=341, rounds=20, warmup=2, rescue=True, check=True, 
                 zg, sg = R.z.cpu().numpy()[smp], R.status.cpu().numpy()[smp]
                 ok = (sc == 1) & (sg == 1)
                 e = np.abs(zg - zc).max(1)
+                if ok.any():
+                    err = max(err, float(e[ok].max()))
                 for a in np.flatnonzero(ok & (e > 1e-6)):
                     kg, fg = reference_certificate(Pc, a, zg[a])
                     kc, fc = reference_certificate(Pc, a, zc[a])
@@ -545,13 +554,14 @@ def lpv_rounds(ctx, replicas=341, rounds=20, warmup=2, rescue=True, check=True, 
                     deg["max_abs_err"] = max(deg["max_abs_err"], float(e[a]))
                     ok[a] = False
                 if ok.any():
-                    err = max(err, float(e[ok].max()))
+                    err_nd = max(err_nd, float(e[ok].max()))
                 both += int(((sc == 1) & (sg == 1)).sum())
                 n += sample
             R.advance()
             R.exchange()
         out["oracle_sample"] = {"agents_per_round": sample, "checked": n, "both_solved": both,
-                                "max_abs_err_vs_cpu": err, "degenerate": deg}
+                                "max_abs_err_vs_cpu": err, "max_abs_err_vs_cpu_non_degenerate": err_nd,
+                                "degenerate": deg}
     return out
 
 

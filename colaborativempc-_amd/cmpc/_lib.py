@@ -64,7 +64,8 @@ CMPC_SOLVER_CONDENSED_V3, CMPC_SOLVER_CONDENSED, CMPC_SOLVER_RICCATI, CMPC_SOLVE
 
 
 class cmpc_plan_info(ct.Structure):
-    _fields_ = [(k, ct.c_int) for k in ("solver", "lds_bytes", "wg_per_cu", "agents_per_wg")]
+    _fields_ = [(k, ct.c_int) for k in ("solver", "lds_bytes", "wg_per_cu", "agents_per_wg", "waves_per_agent",
+                                        "polish_lds_bytes", "polish_max_active")]
 
 
 class cmpc_mpc_data(ct.Structure):

@@ -59,7 +59,9 @@ def _flags(fp32=False, riccati=False, generic=False, rescue=False, lane=False, p
 
 def plan(shared, batch=1, fp32=False, riccati=False, generic=False, lane=False, rescue=False, polish=False):
     """Which solver cmpc_solve_mpc_batch would run for this problem shape, and its occupancy
-    (cmpc_plan_mpc, host only): dict(solver=name, lds_bytes, wg_per_cu, agents_per_wg)."""
+    (cmpc_plan_mpc, host only): dict(solver=name, lds_bytes, wg_per_cu, agents_per_wg, waves_per_agent,
+    polish_lds_bytes, polish_max_active) — the last two describe the rescue policy's polish launch (0 without
+    ``rescue`` and ``polish``)."""
     w, keep = _weights(shared)
     d = _dims(shared, batch)
     o = L.opts(None, None, _flags(fp32, riccati, generic, rescue, lane, polish))
@@ -71,7 +73,8 @@ def plan(shared, batch=1, fp32=False, riccati=False, generic=False, lane=False, 
              L.CMPC_SOLVER_RICCATI: "riccati", L.CMPC_SOLVER_LANE: "lane"}
     del keep
     return dict(solver=names[info.solver], lds_bytes=info.lds_bytes, wg_per_cu=info.wg_per_cu,
-                agents_per_wg=info.agents_per_wg)
+                agents_per_wg=info.agents_per_wg, waves_per_agent=info.waves_per_agent,
+                polish_lds_bytes=info.polish_lds_bytes, polish_max_active=info.polish_max_active)
 
 
 def solve_mpc(p, ctx=None, tol=None, max_iter=None, fp32=False, riccati=False, generic=False, rescue=False,

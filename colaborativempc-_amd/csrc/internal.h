@@ -107,6 +107,16 @@ constexpr double kT0Floor = 0.5;
 // 43 iterations); the cfg3 rounds and every captured reference QP never trigger it (identical
 // iterates, tools/ipm_lab.py).
 constexpr double kShortStep = 0.02;
+
+// Degenerate endpoints (CMPC_FLAG_POLISH).  A solve that converges (merit < tol) with a weakly active row
+// — t_r and lambda_r both of order sqrt(mu) instead of one of them ~0 — is fixed only to ~sqrt(mu) ~ 3e-7
+// along that row's direction: on bench.py's lpv_rounds population the GPU and the C restatement, each at
+// its own ulp-different endpoint, land 5e-7 .. 1e-6 apart there (tools/lpv_margin.py, round 5: every
+// such agent had one row, the last stage's input bound, with min(t, lambda) ~ 2-4e-7 and the next row
+// below 1e-11).  Those agents join the polish launch (rescue image flag 2 with their merit): the active
+// set's equality-constrained QP gives the optimum to ~1e-13 in KKT, and it replaces the endpoint only
+// when its merit is lower.  The threshold sits orders of magnitude from both populations.
+constexpr double kPolishDegenerate = 1e-9;
 constexpr double kSigmaMin = 0.5;
 enum { kStopMaxIter = 0, kStopConverged = 1, kStopBreakdown = 2, kStopStalled = 3, kStopNonFinite = 4 };
 
@@ -146,6 +156,7 @@ __host__ __device__ inline bool hand_over(int stop, double best_m, const MpcCons
 
 // Active-set polish (mpc_polish.hip): agents whose rescue image carries flag 2.
 size_t mpc_polish_lds_bytes(const MpcConst& c);
+int mpc_polish_max_active(const MpcConst& c);  // the layout's active-set capacity (LDS-limited)
 hipError_t mpc_polish_launch(const MpcConst& c, const MpcPtrs& p, int batch, hipStream_t s);
 // Stage-wise Riccati kernel (mpc_riccati.hip): any horizon whose per-agent rows fit LDS.
 size_t mpc_riccati_lds_bytes(const MpcConst& c);

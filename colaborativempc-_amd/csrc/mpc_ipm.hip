@@ -632,10 +632,20 @@ __global__ __launch_bounds__(kWave) void mpc_ipm_kernel(const MpcConst c, const 
     if (it > c.max_iter) it = c.max_iter;
     bar();
     int status = CMPC_SOLVED;
+    // a converged endpoint with a weakly active row (kPolishDegenerate) is polished as well
+    bool degen = false;
+    if (c.polish && P.ws && stop == kStopConverged) {
+        double dg_l = 0.0;
+        for (int r = l; r < m; r += kWave)
+            if (isfinite(w[r])) dg_l = fmax(dg_l, fmin(t[r], lam[r]));
+        degen = wave_max(dg_l) > kPolishDegenerate;
+    }
     // polish (CMPC_FLAG_POLISH): a stall or max-iteration exit at the rounding floor leaves its last iterate
     // in the rescue image too (a breakdown wrote it above)
-    if (c.polish && P.ws && stop != kStopConverged && stop != kStopBreakdown && stop != kStopNonFinite &&
-        (best_m < 1e3 * c.tol || stop == kStopMaxIter)) {
+    if (c.polish && P.ws &&
+        ((stop != kStopConverged && stop != kStopBreakdown && stop != kStopNonFinite &&
+          (best_m < 1e3 * c.tol || stop == kStopMaxIter)) ||
+         degen)) {
         double* hd = P.ws + (size_t)b * c.ws_stride;
         const size_t ht = hand_t(c);
         for (int i = l; i < n; i += kWave) hd[2 + i] = U[i];
@@ -679,8 +689,10 @@ __global__ __launch_bounds__(kWave) void mpc_ipm_kernel(const MpcConst c, const 
             double* hd = P.ws + (size_t)b * c.ws_stride;
             const bool ho = hand_over(stop, best_m, c);
             // polished: a final exit short of tol (status 2 or -2; CMPC_UNSOLVED goes on to the Riccati rescue)
-            const bool pol = !ho && c.polish && stop != kStopConverged && stop != kStopNonFinite &&
-                             (best_m < 1e3 * c.tol || stop == kStopMaxIter);
+            const bool pol = !ho && c.polish &&
+                             ((stop != kStopConverged && stop != kStopNonFinite &&
+                               (best_m < 1e3 * c.tol || stop == kStopMaxIter)) ||
+                              degen);
             hd[0] = ho ? 1.0 : (pol ? 2.0 : 0.0);
             if (pol) hd[1] = best_m;
         }

@@ -1607,10 +1607,21 @@ __global__ __launch_bounds__(64, 1) void mpc_ipm3_kernel(const MpcConst c, const
     if (it > c.max_iter) it = c.max_iter;
     wsync();
     int status = CMPC_SOLVED;
+    // a converged endpoint with a weakly active row (kPolishDegenerate) is polished as well
+    bool degen = false;
+    if (c.polish && P.ws && stop == kStopConverged) {
+        double dg_l = 0.0;
+#pragma unroll
+        for (int r = 0; r < RX; ++r)
+            if (ACT(r)) dg_l = fmax(dg_l, fmin(t[r], lam[r]));
+        degen = wave_max(dg_l) > kPolishDegenerate;
+    }
     // polish (CMPC_FLAG_POLISH): a stall or max-iteration exit at the rounding floor leaves its last iterate
     // too (a breakdown wrote it above)
-    if (c.polish && P.ws && stop != kStopConverged && stop != kStopBreakdown && stop != kStopNonFinite &&
-        (best_m < 1e3 * c.tol || stop == kStopMaxIter))
+    if (c.polish && P.ws &&
+        ((stop != kStopConverged && stop != kStopBreakdown && stop != kStopNonFinite &&
+          (best_m < 1e3 * c.tol || stop == kStopMaxIter)) ||
+         degen))
         write_image();
     if (stop != kStopConverged) {
         if (best_it > 0) {  // restore the best iterate
@@ -1652,8 +1663,10 @@ __global__ __launch_bounds__(64, 1) void mpc_ipm3_kernel(const MpcConst c, const
             double* hd = P.ws + (size_t)b * c.ws_stride;
             const bool ho = hand_over(stop, best_m, c);
             // polished: a final exit short of tol (status 2 or -2; CMPC_UNSOLVED goes on to the Riccati rescue)
-            const bool pol = !ho && c.polish && stop != kStopConverged && stop != kStopNonFinite &&
-                             (best_m < 1e3 * c.tol || stop == kStopMaxIter);
+            const bool pol = !ho && c.polish &&
+                             ((stop != kStopConverged && stop != kStopNonFinite &&
+                               (best_m < 1e3 * c.tol || stop == kStopMaxIter)) ||
+                              degen);
             hd[0] = ho ? 1.0 : (pol ? 2.0 : 0.0);
             if (pol) hd[1] = best_m;
         }

@@ -750,7 +750,11 @@ __global__ __launch_bounds__(kPT) void mpc_polish_kernel(const MpcConst c_arg, c
         for (int i = 0; i < 3; ++i) st[5 + i] = (unsigned long long)__double_as_longlong(sm[L.red + 8 + i]);
         for (int i = 0; i < 6; ++i) st[9 + i] = tsum[i];
     }
-    if (!(best < best_m)) {
+    // kept only when it beats the method's best AND lands at the rounding floor at least (stop_status's
+    // 1e3 tol): below tol it is solved (1), below the floor solved-inaccurate (2).  A polish of a solve
+    // that ended far from the floor (a cold-pass stall, a max-iteration exit) never turns it into a 2,
+    // which the reference would count as feasible (LPV_Planner.py:243-249): status and z stay as they were
+    if (!(best < best_m) || !(best < 1e3 * c.tol)) {
         if (tid == 0 && flag == 2.0) hd[0] = 0.0;  // (flag 1 stays: the Riccati rescue takes the agent)
         return;
     }
@@ -784,6 +788,7 @@ __global__ __launch_bounds__(kPT) void mpc_polish_kernel(const MpcConst c_arg, c
 }  // namespace
 
 size_t mpc_polish_lds_bytes(const MpcConst& c) { return sizeof(double) * (size_t)pol_layout(c).total; }
+int mpc_polish_max_active(const MpcConst& c) { return pol_layout(c).amax; }
 
 template <int NXT>
 static hipError_t polish_launch_t(const MpcConst& c, const MpcPtrs& p, int batch, hipStream_t s, size_t lds) {

@@ -42,8 +42,9 @@
 extern "C" {
 #endif
 
-#define CMPC_ABI_VERSION 5   /* 2: cmpc_lpv_advance_dev status / infeasible, cmpc_lpv_rounds_*; 3: cmpc_opts.order;
-                                4: cmpc_comm_sum_i32, cmpc_plan_mpc; 5: CMPC_FLAG_POLISH */
+#define CMPC_ABI_VERSION 6   /* 2: cmpc_lpv_advance_dev status / infeasible, cmpc_lpv_rounds_*; 3: cmpc_opts.order;
+                                4: cmpc_comm_sum_i32, cmpc_plan_mpc; 5: CMPC_FLAG_POLISH;
+                                6: cmpc_plan_info waves_per_agent / polish_lds_bytes / polish_max_active */
 
 /* API error codes */
 #define CMPC_OK 0
@@ -112,7 +113,11 @@ typedef struct {
                          behaviour: a missing agent is left unsolved, and a duplicated one is solved by
                          two workgroups (lanes) at once into the same scratch and outputs (a data race).
                          The library does not check it (the device array is read by the kernels only);
-                         cmpc.rounds.DIRounds builds it by argsort, always a permutation. */
+                         cmpc.rounds.DIRounds builds it by argsort, always a permutation.
+                         Exception: a lane-per-agent batch whose scratch reaches 2 GiB runs as consecutive
+                         sub-launches in agent order (mpc_lane.hip) and ignores both `order` and `stamps`
+                         (same results; only the wavefront packing is lost).  cfg5 (8192 agents) stays
+                         below that size; the bound is ~19.7k agents at N = 50. */
 } cmpc_opts;
 
 int cmpc_abi_version(void);
@@ -190,6 +195,15 @@ typedef struct {
     int lds_bytes;     /* dynamic LDS per workgroup */
     int wg_per_cu;     /* workgroups resident per CU */
     int agents_per_wg; /* 1, or 32 (lane solver) */
+    int waves_per_agent;   /* wavefronts of one agent's workgroup (1; 2: the condensed kernel's small-batch mode) */
+    /* The rescue policy (CMPC_FLAG_RESCUE [| CMPC_FLAG_POLISH]) adds launches the fields above do not
+     * describe: the polish kernel (before the Riccati hand-over and after the Riccati passes; one
+     * 256-thread workgroup per agent, agents without a flag return at once) and two Riccati passes.
+     * polish_lds_bytes: the polish workgroup's LDS (0 when the polish does not run); polish_max_active:
+     * the largest active set it polishes (kPolishMaxActive = 96, lowered in steps of 8 until the image
+     * fits 160 KB; larger active sets keep the interior-point result) */
+    int polish_lds_bytes;
+    int polish_max_active;
 } cmpc_plan_info;
 int cmpc_plan_mpc(const cmpc_mpc_dims* dims, const cmpc_mpc_weights* w, const cmpc_opts* opts,
                   cmpc_plan_info* out);

@@ -17,7 +17,7 @@
  * (oracle/qp_ipm.py) on QPs captured from the reference (tests/golden).
  */
 #include <math.h>
-#if defined(ORACLE_TRACE) || defined(POLISH_DEBUG) || defined(RIC_DEBUG) || defined(LAB_THDUMP) || defined(DIRCHECK) || defined(LAB_STOPDUMP)
+#if defined(ORACLE_TRACE) || defined(POLISH_DEBUG) || defined(RIC_DEBUG) || defined(LAB_THDUMP) || defined(DIRCHECK) || defined(LAB_STOPDUMP) || defined(LAB_DEGEN)
 #include <stdio.h>
 #endif
 #include <stdlib.h>
@@ -34,6 +34,7 @@ typedef struct {
     int refine_dd;      /* refinement steps of a double-double iteration (RIC_REFINE_MAX; continued
                            rescue solves RIC_REFINE_WARM, the kernels' kRefineMaxWarm) */
     int polish;         /* CMPC_FLAG_POLISH: active-set polish of a breakdown at the rounding floor */
+    int polish_amax;    /* largest polished active set (0: POLISH_MAX_ACTIVE) */
     /* newton: 0 condensed Cholesky; 1 Riccati (P = Qyy + A'PA + Hvy'K); 2 Riccati, Joseph form */
 } shared_t;
 
@@ -1226,7 +1227,13 @@ static double merit_at(const shared_t* S, const agent_t* a, work_t* wk, const do
 }
 
 #ifndef POLISH_MAX_ACTIVE
-#define POLISH_MAX_ACTIVE 128 /* kPolishMaxActive (internal.h): larger active sets are not polished */
+#define POLISH_MAX_ACTIVE 96  /* kPolishMaxActive (mpc_polish.hip): larger active sets are not polished.  The
+                                 kernel lowers it in steps of 8 until its LDS image fits (pol_layout); the
+                                 caller passes that value in (newton bits 16..23, cmpc_plan_info's
+                                 polish_max_active) so both sides polish the same agents */
+#endif
+#ifndef POLISH_DEGENERATE
+#define POLISH_DEGENERATE 1e-9 /* kPolishDegenerate (internal.h) */
 #endif
 #ifndef POLISH_STEPS
 #define POLISH_STEPS 3        /* kPolishSteps: Newton steps on the (linear) equality-constrained KKT system */
@@ -1254,7 +1261,7 @@ static double polish_one(const shared_t* S, const agent_t* a, work_t* wk, double
                          const double* t, const double* lam, double* Up, double* sigp, double* kkt) {
     const int nx = S->nx, nu = S->nu, N = S->N, ns = S->ns, mc = S->mc;
     const int n = N * nu, ms = N * mc, m = ms + 2 * nu * N;
-    const int amax = POLISH_MAX_ACTIVE;
+    const int amax = S->polish_amax > 0 ? S->polish_amax : POLISH_MAX_ACTIVE;
     unsigned char* in = malloc((size_t)m);
     int* Ar = malloc(sizeof(int) * amax);
     double* GA = malloc(sizeof(double) * (2 * (size_t)amax * n + (size_t)amax * amax + 3 * (size_t)amax +
@@ -1551,7 +1558,7 @@ static int solve_one(const shared_t* S, const agent_t* a, double tol, int max_it
     /* best iterate by merit max(res, 1e4 mu) (< tol <=> converged): returned when the
        method stops short of convergence (max_iter, factorisation breakdown, stagnation) */
     double best_m = INFINITY, best_kkt = INFINITY;
-    int best_it = 0, stop = 0; /* stop: 0 max_iter, 1 converged, 2 breakdown, 3 stagnation, 4 non-finite */
+    int best_it = 0, stop = 0, pol_done = 0; /* stop: 0 max_iter, 1 converged, 2 breakdown, 3 stagnation, 4 non-finite */
     double *bU = wk->bU, *bsig = wk->bsig;
     int it;
     double kkt = INFINITY;
@@ -1667,6 +1674,13 @@ static int solve_one(const shared_t* S, const agent_t* a, double tol, int max_it
 #ifdef ORACLE_TRACE
         fprintf(stderr, "it %2d mu %.3e res %.3e (rd %.2e rs %.2e rp %.2e) merit %.3e\n", it, mu, res,
                 nrd / gscale, nrs / qs_max, nrp / scale_p, merit);
+#endif
+#ifdef LAB_DEGEN
+        if (merit < tol) {
+            double v1 = 0, v2 = 0, v3 = 0; int r1 = -1;
+            for (int r = 0; r < m; ++r) if (wk->act[r]) { double v = fmin(t[r], lam[r]); if (v > v1) { v3 = v2; v2 = v1; v1 = v; r1 = r; } else if (v > v2) { v3 = v2; v2 = v; } else if (v > v3) v3 = v; }
+            fprintf(stderr, "DEGEN it %d mu %.2e top min(t,lam) %.2e (row %d t %.2e lam %.2e) %.2e %.2e\n", it, mu, v1, r1, r1 >= 0 ? t[r1] : 0., r1 >= 0 ? lam[r1] : 0., v2, v3);
+        }
 #endif
         if (merit < tol) { stop = 1; break; }
         /* near-converged but no progress for STALL_ITERS iterations: rounding floor reached */
@@ -1854,6 +1868,7 @@ static int solve_one(const shared_t* S, const agent_t* a, double tol, int max_it
                         memcpy(sig, wk->dsig, sizeof(double) * N * ns);
                         kkt = pk;
                         stop = 1;
+                        pol_done = 1;
                         break;
                     }
                 }
@@ -2225,15 +2240,24 @@ static int solve_one(const shared_t* S, const agent_t* a, double tol, int max_it
        last iterate (the kernels' rescue image, flag 2) */
     double pol_m = INFINITY, pol_kkt = INFINITY;
     const int final_solve = !warm_rescue || best_m < 1e3 * tol || stop == 0;
-    if (S->polish && stop != 1 && stop != 4 && final_solve)
+    /* ... and a condensed solve that converged with a weakly active row (kPolishDegenerate, internal.h:
+       t_r and lambda_r both ~sqrt(mu); the endpoint is then fixed only to ~3e-7 along that row) */
+    int degen = 0;
+    if (S->polish && stop == 1 && !S->newton && !pol_done) {
+        double dg = 0.0;
+        for (int r = 0; r < m; ++r)
+            if (wk->act[r]) dg = fmax(dg, fmin(t[r], lam[r]));
+        degen = dg > POLISH_DEGENERATE;
+    }
+    if (S->polish && ((stop != 1 && stop != 4 && final_solve) || degen))
         pol_m = polish_one(S, a, wk, tol, U, sig, t, lam, wk->dU, wk->dsig, &pol_kkt);
 #ifdef POLISH_DEBUG
     if (stop != 1) fprintf(stderr, "POL stop %d newton %d best_m %.2e pol_m %.2e\n", stop, S->newton, best_m, pol_m);
 #endif
     int status;
-    if (stop == 1) {
+    if (stop == 1 && !(degen && pol_m < best_m)) {
         status = 1;
-    } else if (pol_m < best_m) {
+    } else if (pol_m < best_m && pol_m < 1e3 * tol) { /* (mpc_polish.hip: never promotes past the floor) */
         memcpy(U, wk->dU, sizeof(double) * n);
         memcpy(sig, wk->dsig, sizeof(double) * N * ns);
         kkt = pol_kkt;
@@ -2278,9 +2302,10 @@ int cmpc_oracle_solve_ex(int nx, int nu, int N, int ns, int mc, int batch,
                          double tol, int max_iter, int nthreads, int newton, int refine, const double* U0,
                          double* z, double* kkt, int* iters, int* status) {
     const int polish = (newton >> 8) & 1; /* newton | 0x100: CMPC_FLAG_POLISH */
+    const int polish_amax = (newton >> 16) & 0xff; /* newton | amax << 16: the kernel's active-set capacity */
     newton &= 0xff;
     shared_t S = {nx, nu, N, ns, mc, Q, R, dR, Qs, u_ub, u_lb, row_slack, row_sign, newton, refine, RIC_REFINE_MAX,
-                  polish};
+                  polish, polish_amax};
     if (newton && (nx + nu > NA_MAX || nu > NU_MAX)) return -1;
     const int n = N * nu, m = N * mc + 2 * nu * N;
     const size_t nz = (size_t)(nx + ns) * (N + 1) + 2 * (size_t)nu * N;

@@ -51,20 +51,23 @@ def nz_of(p):
     return (p["nx"] + p["ns"]) * (p["N"] + 1) + 2 * p["nu"] * p["N"]
 
 
-def solve_batch_rescue(p, tol=1e-9, max_iter=60, nthreads=0, finish=False, polish=False):
+def solve_batch_rescue(p, tol=1e-9, max_iter=60, nthreads=0, finish=False, polish=False, polish_amax=0):
     """The product's CMPC_FLAG_RESCUE policy restated: the condensed method; an agent whose
     factorisation breaks down short of the rounding floor (best merit >= 1e3 tol; with ``finish``,
     CMPC_FLAG_FINISH, every breakdown) continues from that iterate with the Riccati method in the
     kernel's double-double mode, its best-iterate bookkeeping restarted (newton 5 / 4, the kernels'
     hand-over); an agent that still ends CMPC_UNSOLVED is re-solved by that Riccati method from a
-    cold start (newton 3, the second rescue pass)."""
-    z, kkt, it, st = solve_batch(p, tol, max_iter, nthreads, newton=(4 if finish else 5) | (0x100 if polish else 0))
+    cold start (newton 3, the second rescue pass).  ``polish_amax``: the polish kernel's active-set
+    capacity for this shape (cmpc.solver.plan(..., rescue=True, polish=True)["polish_max_active"]; 0:
+    kPolishMaxActive = 96), so both sides polish the same agents."""
+    pol = (0x100 | (int(polish_amax) & 0xff) << 16) if polish else 0
+    z, kkt, it, st = solve_batch(p, tol, max_iter, nthreads, newton=(4 if finish else 5) | pol)
     bad = np.flatnonzero(st == -10)
     if len(bad):
         q = dict(p)
         for k in ("A", "B", "x0", "u_prev", "qlin", "C", "h"):
             q[k] = p[k][bad]
-        z[bad], kkt[bad], it[bad], st[bad] = solve_batch(q, tol, max_iter, nthreads, newton=3 | (0x100 if polish else 0))
+        z[bad], kkt[bad], it[bad], st[bad] = solve_batch(q, tol, max_iter, nthreads, newton=3 | pol)
     return z, kkt, it, st
 
 

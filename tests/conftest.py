@@ -17,6 +17,14 @@ def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (gfx950) device and the built libcmpc.so")
 
 
+def polish_amax(P):
+    """The polish kernel's active-set capacity for this problem shape (cmpc_plan_info.polish_max_active,
+    host only), handed to the C restatement so both sides polish the same agents."""
+    from cmpc.solver import plan
+
+    return plan(P, 1, rescue=True, polish=True)["polish_max_active"]
+
+
 def golden(name):
     return np.load(os.path.join(GOLDEN, name + ".npz"), allow_pickle=False)
 

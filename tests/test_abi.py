@@ -33,7 +33,7 @@ def test_library_exports_every_declared_symbol():
 
 
 def test_abi_version():
-    assert L.load().cmpc_abi_version() == 5
+    assert L.load().cmpc_abi_version() == 6
 
 
 def test_plan_occupancy_of_the_bench_configs():

@@ -6,7 +6,7 @@ reference optimum / the C restatement; builder outputs to fp64 rounding.
 import numpy as np
 import pytest
 
-from conftest import LPV_CASES, assert_matches_optimum, golden, lpv_qps
+from conftest import LPV_CASES, assert_matches_optimum, golden, lpv_qps, polish_amax
 
 pytestmark = pytest.mark.gpu
 
@@ -207,7 +207,8 @@ def test_rescue_pass_resolves_factorisation_breakdowns(gpu_ctx, finish, polish):
                      u_ub=np.array([0.3, 5.0]), u_lb=np.array([-0.3, -10.0]), row_slack=np.array([-1, 0, 1, 1, 2, 2]),
                      row_sign=np.array([1, 1, 1, 1, -1, -1]), A=b["A"], B=b["B"], x0=R.x0.cpu().numpy(),
                      u_prev=R.u_old.cpu().numpy(), qlin=b["qlin"], C=b["C"], h=b["h"])
-            zc, kc, ic, sc = CO.solve_batch_rescue(P, nthreads=8, finish=finish, polish=polish)
+            zc, kc, ic, sc = CO.solve_batch_rescue(P, nthreads=8, finish=finish, polish=polish,
+                                                   polish_amax=polish_amax(P) if polish else 0)
             both = (sc == 1) & (st1 == 1)
             floor = ~both
             err = np.abs(zc - z1).max(1)
@@ -412,6 +413,13 @@ def test_edge_cases(gpu_ctx):
     z, kkt, it, st = cmpc.solve_mpc(H, gpu_ctx, max_iter=40)
     assert st[0] != cmpc.CMPC_SOLVED and st[1] != cmpc.CMPC_SOLVED
     zc, _, _, _ = CO.solve_batch(P)
+    assert (st[2:] == 1).all() and np.abs(z[2:] - zc[2:]).max() < Z_TOL
+    # ... and through the whole rescue policy (condensed -> polish -> Riccati warm / cold -> polish): the
+    # polish never promotes the hard-infeasible agent to 1 or 2, which the reference would count as
+    # feasible (LPV_Planner.py:243-249); the regular agents are still solved
+    z, kkt, it, st = cmpc.solve_mpc(H, gpu_ctx, max_iter=40, rescue=True, polish=True)
+    assert st[0] not in (cmpc.CMPC_SOLVED, cmpc.CMPC_SOLVED_INACCURATE), st[:2]
+    assert st[1] not in (cmpc.CMPC_SOLVED, cmpc.CMPC_SOLVED_INACCURATE), st[:2]
     assert (st[2:] == 1).all() and np.abs(z[2:] - zc[2:]).max() < Z_TOL
 
 

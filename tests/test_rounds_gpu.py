@@ -174,10 +174,12 @@ def test_lpv_rounds_at_scale_against_c_restatement(gpu_ctx):
     smp = out["oracle_sample"]
     assert smp["checked"] == 20 * 128, smp
     assert smp["both_solved"] >= 0.99 * smp["checked"], smp
-    assert smp["max_abs_err_vs_cpu"] <= 1e-6, smp
+    assert smp["max_abs_err_vs_cpu_non_degenerate"] <= 1e-6, smp
     # both solved but farther apart than 1e-6: an interior-point endpoint against a polished one on a
     # degenerate optimum; the GPU point certifies itself (reference-form KKT, objective not above the
-    # C restatement's)
+    # C restatement's), and such agents stay rare (<= 0.5 % of the sample; max_abs_err_vs_cpu, over every
+    # both-solved agent, includes them)
     dg = smp["degenerate"]
+    assert dg["count"] <= 0.005 * smp["checked"], dg
     if dg["count"]:
         assert dg["max_ref_kkt_gpu"] <= 1e-6 and dg["max_obj_gap_rel"] <= 1e-10, dg
