@@ -100,6 +100,13 @@ constexpr int kStallIters = 3;
 // slowest agent's iteration count drops 1951 -> 1801 (the kernel time follows the slowest
 // agent) with no max-iteration agent (floors 0.4 and 0.7 each had one); mean 9.39 -> 9.32.
 constexpr double kT0Floor = 0.5;
+// ... for the condensed kernels (mpc_ipm3, mpc_ipm) since round 5: 0.1.  Measured again on the current
+// method (tools/ipm_lab.py, 100 cfg3 rounds of 1024 agents): the sum of the per-round slowest agent's
+// iterations 1801 -> 1621 (floors 0.04 .. 0.15 all give 1566 .. 1621; 0.02 and below fail agents), mean
+// 9.32 -> 9.13; reference-model rounds (tools/lpv_lab.py, 22 rounds of 1023 agents, rescue policy): 553 ->
+// 500, max 45 -> 38, mean 14.5 -> 13.6.  The stage-wise kernels keep 0.5: on cfg5 (N = 50, Riccati) the
+// total iterations, which set that launch, rose 2 % with 0.1.
+constexpr double kT0FloorCond = 0.1;
 // Stall guard: after an iteration whose step was below kShortStep, the corrector's centring
 // parameter is at least kSigmaMin.  On the BASELINE cfg5 population (N=50, nx=6 nu=3) about 1
 // agent in 10^4 otherwise stalls at steps ~1e-3, blocked by a terminal collision row, and runs

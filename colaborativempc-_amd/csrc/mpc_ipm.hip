@@ -277,7 +277,7 @@ __global__ __launch_bounds__(kWave) void mpc_ipm_kernel(const MpcConst c, const 
     for (int r = l; r < m; r += kWave) {
         if (isfinite(w[r])) {
             const double g = row_value(c, C, r, X, U, sig);
-            t[r] = fmax(w[r] - g, kT0Floor);
+            t[r] = fmax(w[r] - g, kT0FloorCond);
             lam[r] = 1.0;
             mact_l += 1.0;
             sp_l = fmax(sp_l, fabs(w[r]));

@@ -725,7 +725,7 @@ __global__ __launch_bounds__(64, 1) void mpc_ipm3_kernel(const MpcConst c, const
     for (int r = 0; r < RX; ++r) {
         if (ACT(r)) {
             const double w = wv(r);
-            t[r] = fmax(w - rowval(r, X, U, true), kT0Floor);
+            t[r] = fmax(w - rowval(r, X, U, true), kT0FloorCond);
             lam[r] = 1.0;
             mact_l += 1.0;
             sp_l = fmax(sp_l, fabs(w));

@@ -124,7 +124,10 @@ long cmpc_gz_solves = 0; /* lab: corrector solves performed */
 #define MU_FACTOR 1e4   /* merit max(res, MU_FACTOR mu); lab: the fp32 kernels use 10 */
 #endif
 #ifndef T0_FLOOR
-#define T0_FLOOR 0.5    /* starting slacks t_r = max(w_r - g_r, T0_FLOOR) (internal.h kT0Floor) */
+#define T0_FLOOR 0.5    /* starting slacks t_r = max(w_r - g_r, T0_FLOOR) (internal.h kT0Floor): stage-wise methods */
+#endif
+#ifndef T0_FLOOR_COND
+#define T0_FLOOR_COND 0.1 /* ... the condensed method (newton 0; kT0FloorCond) */
 #endif
 
 static int chol(double* K, int n) {
@@ -1232,6 +1235,14 @@ static double merit_at(const shared_t* S, const agent_t* a, work_t* wk, const do
                                  caller passes that value in (newton bits 16..23, cmpc_plan_info's
                                  polish_max_active) so both sides polish the same agents */
 #endif
+#ifdef LAB_SIGMA2
+#ifndef LAB_SIGMA2_RULE
+#define LAB_SIGMA2_RULE(s) fmax(10.0 * (s), 0.1)
+#endif
+#ifndef LAB_SIGMA2_MARGIN
+#define LAB_SIGMA2_MARGIN 1.0
+#endif
+#endif
 #ifndef POLISH_DEGENERATE
 #define POLISH_DEGENERATE 1e-9 /* kPolishDegenerate (internal.h) */
 #endif
@@ -1534,7 +1545,8 @@ static int solve_one(const shared_t* S, const agent_t* a, double tol, int max_it
         if (!wk->act[r]) { t[r] = 1.0; lam[r] = 0.0; continue; }
         double g; ROWVAL(X, U, sig, r, g);
         double s0 = wk->w[r] - g;
-        t[r] = s0 > T0_FLOOR ? s0 : T0_FLOOR; /* kT0Floor of the kernels (internal.h) */
+        const double fl = S->newton ? T0_FLOOR : T0_FLOOR_COND; /* kT0Floor / kT0FloorCond (internal.h) */
+        t[r] = s0 > fl ? s0 : fl;
 #ifdef LAM0_CENTRE
         lam[r] = LAM0_CENTRE / t[r]; /* lab: centred start, t lambda equal on every row */
 #else
@@ -1570,6 +1582,11 @@ static int solve_one(const shared_t* S, const agent_t* a, double tol, int max_it
 #define DD_STALL 2           /* kDdStall of mpc_riccati.hip */
 #endif
     int dd_on = 0;           /* newton 3: this solve has switched to double-double near the solution */
+#ifdef LAB_SIGMA2
+    /* lab: a second corrector with another centring parameter per iteration (a second wavefront's
+       work in a two-wave kernel); the longer step wins, ties to the first */
+    double* s2_save = malloc(sizeof(double) * ((size_t)n + (size_t)(N + 1) * nx + (size_t)N * ns + 2 * (size_t)m));
+#endif
 #ifdef GONDZIO
     /* lab: Gondzio centrality correctors (up to GONDZIO per iteration) on the Mehrotra direction */
     long gz_used = 0;
@@ -1919,6 +1936,9 @@ static int solve_one(const shared_t* S, const agent_t* a, double tol, int max_it
 
         /* ---- predictor / corrector ---- */
         double sig_c = 0.0, mu_aff = 0.0;
+#ifdef LAB_SIGMA2
+        int s2_stage = 0; double s2_al = 0.0, s2_sig1 = 0.0;
+#endif
 #ifdef RETRY_SIGMA
         int retried = 0;
 #endif
@@ -2201,6 +2221,35 @@ static int solve_one(const shared_t* S, const agent_t* a, double tol, int max_it
                     if (blk >= 0)
                         fprintf(stderr, "      step al %.3e sigma %.2e mu_aff/mu %.2e blocking %d (t %.2e lam %.2e)\n",
                                 al, sig_c, mu > 0 ? mu_aff / mu : 0.0, blk, t[blk % 10000], lam[blk % 10000]);
+                }
+#endif
+#ifdef LAB_SIGMA2
+                {
+                    const size_t nX = (size_t)(N + 1) * nx, nS = (size_t)N * ns;
+                    if (s2_stage == 0) {
+                        double* sv = s2_save;
+                        memcpy(sv, wk->dU, sizeof(double) * n); sv += n;
+                        memcpy(sv, wk->dX, sizeof(double) * nX); sv += nX;
+                        memcpy(sv, wk->dsig, sizeof(double) * nS); sv += nS;
+                        memcpy(sv, dt, sizeof(double) * m); sv += m;
+                        memcpy(sv, dl, sizeof(double) * m);
+                        s2_al = al;
+                        s2_sig1 = sig_c;
+                        s2_stage = 1;
+                        sig_c = LAB_SIGMA2_RULE(sig_c);
+                        pass = 0;
+                        continue;
+                    }
+                    if (!(al > s2_al * LAB_SIGMA2_MARGIN)) { /* the first corrector's step */
+                        double* sv = s2_save;
+                        memcpy(wk->dU, sv, sizeof(double) * n); sv += n;
+                        memcpy(wk->dX, sv, sizeof(double) * nX); sv += nX;
+                        memcpy(wk->dsig, sv, sizeof(double) * nS); sv += nS;
+                        memcpy(dt, sv, sizeof(double) * m); sv += m;
+                        memcpy(dl, sv, sizeof(double) * m);
+                        al = s2_al;
+                        sig_c = s2_sig1;
+                    }
                 }
 #endif
 #ifdef RETRY_SIGMA
