@@ -25,7 +25,7 @@ sys.path.insert(0, os.path.join(ROOT, "colaborativempc-_amd"))
 sys.path.insert(0, ROOT)
 
 METRIC = "agent-QP solves/sec (whole node) at N=30, nx=4 nu=2; max KKT residual vs ref"
-FP64_PEAK_TFLOPS = 78.6   # MI355X dense FP64 (vector == matrix), spec
+FP64_PEAK_TFLOPS = 78.6   # MI355X dense FP64 (vector == matrix): AMD's datasheet figure; the MI355X guide has no FP64 line
 FP32_PEAK_TFLOPS = 157.3  # MI355X FP32 vector, spec
 HBM_PEAK_GBS = 8000.0
 
@@ -209,7 +209,8 @@ def main():
                 "counters": sq_profile(pmc_kind or "cfg3"),
                 "achieved": achieved_tf,
                 "peak": peak,
-                "peak_note": "fp32 vector (the factorisation's precision)" if args.fp32 else "fp64 vector = matrix",
+                "peak_note": "fp32 vector (the factorisation's precision)" if args.fp32 else
+                             "fp64 vector = matrix, AMD datasheet figure (not in the MI355X guide)",
                 "unit": "TFLOP/s",
                 "frac": achieved_tf / peak,
                 "traffic": traffic,
@@ -717,6 +718,8 @@ def cpu_baseline(R, seconds, rounds=4, newton=0, label="cfg3"):
     solved = passes * rounds * B
     return ({"value": solved / el, "unit": "agent-QP/s", "cores": threads, "kind": "port",
              "nproc": nproc, "cpu_model": model,
+             "cores_note": f"{threads}-thread job share (affinity mask) of a {nproc}-thread host: a baseline "
+                           f"against those threads, not against the whole node",
              "sample": f"{passes} pass(es) over {rounds} consecutive full {label} rounds of {B} agents "
                        f"(device-built problems copied to the host), oracle/cmpc_oracle.c fp64, OpenMP "
                        f"{threads} threads, {el:.1f} s"}, err)

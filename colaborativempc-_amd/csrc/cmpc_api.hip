@@ -101,7 +101,10 @@ int lpv_solver_const(cmpc_ctx* ctx, const cmpc_lpv_params* prm, const cmpc_lpv_d
     for (int i = 0; i < 9; ++i)
         for (int j = 0; j < 9; ++j)
             if (i != j && prm->Q[i * 9 + j] != 0.0) qdiag = false;
-    mc->lpv = (qdiag && !(o && (o->flags & CMPC_FLAG_GENERIC))) ? 1 : 0;
+    // 2: Q also zero on states 1, 2, 5, 6 (the reference's config_LPV.py:7): the v3 kernel's L5 contraction
+    const bool q5 = prm->Q[1 * 9 + 1] == 0.0 && prm->Q[2 * 9 + 2] == 0.0 && prm->Q[5 * 9 + 5] == 0.0 &&
+                    prm->Q[6 * 9 + 6] == 0.0;
+    mc->lpv = (qdiag && !(o && (o->flags & CMPC_FLAG_GENERIC))) ? (q5 ? 2 : 1) : 0;
     return CMPC_OK;
 }
 

@@ -24,7 +24,8 @@ struct MpcConst {
     int max_iter;
     int riccati;  // 1: stage-wise Riccati kernel (fp64, N*nu > 64 or CMPC_FLAG_RICCATI)
     int rescue;   // 1: CMPC_FLAG_RESCUE on a condensed solve (Riccati re-solve of broken-down agents)
-    int lpv;      // 1: data made by lpv_build.hip with Q diagonal (the v3 kernel's LS layout applies)
+    int lpv;      // 1: data made by lpv_build.hip with Q diagonal (the v3 kernel's LS layout applies); 2: and Q zero
+                  // on states 1, 2, 5, 6 (the LS kernel's L5 contraction, the reference's config_LPV.py:7)
     int finish;   // 1: CMPC_FLAG_FINISH (rescue also continues breakdowns at the rounding floor)
     int lane;     // lane-per-agent kernel (mpc_lane.hip): 1 fp64 (CMPC_FLAG_LANE), 2 mixed fp32 (CMPC_FLAG_FP32 | LANE,
                   // or CMPC_FLAG_FP32 on dimensions without an fp32 Riccati instantiation)

@@ -612,20 +612,55 @@ __global__ __launch_bounds__(kPT) void mpc_polish_kernel(const MpcConst c_arg, c
         }
         __syncthreads();
         PSTAMP(3);
-        // S = Y Y' + E (packed lower)
-        for (int e = tid; e < nA * (nA + 1) / 2; e += kPT) {
-            int a = (int)((sqrt(8.0 * e + 1.0) - 1.0) * 0.5);
-            while (a * (a + 1) / 2 > e) --a;
-            while ((a + 1) * (a + 2) / 2 <= e) ++a;
-            const int b2 = e - a * (a + 1) / 2;
-            double v = 0.0;
-            for (int i = 0; i < n; ++i) v += Y[(size_t)a * ldY + i] * Y[(size_t)b2 * ldY + i];
-            const int r = Ar[a], r2 = Ar[b2];
-            if (r < ms && r2 < ms && r / mc == r2 / mc) {
-                const int j = c.row_slack[r % mc];
-                if (j >= 0 && c.row_slack[r2 % mc] == j) v += c.row_sign[r % mc] * c.row_sign[r2 % mc] / (2.0 * c.Qs[j]);
+        // S = Y Y' + E (packed lower): the active rows' Gram matrix on V_MFMA_F64_16X16X4_F64.  16 x 16
+        // tiles (I, J), I >= J, over nA padded to 16, dealt round-robin to the four waves, two tiles in
+        // flight per wave (independent accumulator chains); k-steps of 4 over the n columns.  Both
+        // operands of a k-step are the same fragment pattern: lane l holds Y[16 I + (l & 15)][4 s + (l >> 4)]
+        // (A: 16 x 4 row block of Y; B: its transpose); D[i][j] sits at lane j + 16 (i & 3), register i >> 2.
+        // (Was one thread per packed entry with an n-term LDS dot product: 0.15 M clocks at nA ~ 80.)
+        {
+            const int TA = (nA + 15) >> 4, NTt = TA * (TA + 1) / 2, KS = (n + 3) >> 2;
+            const int wv = tid >> 6, l = tid & 63, i16 = l & 15, kq = l >> 4;
+            auto tile_ij = [](int t, int& I, int& J) {
+                I = 0;
+                while ((I + 1) * (I + 2) / 2 <= t) ++I;
+                J = t - I * (I + 1) / 2;
+            };
+            auto frag = [&](int blk, int s) {
+                const int row = 16 * blk + i16, col = 4 * s + kq;
+                const double v = Y[(size_t)(row < nA ? row : 0) * ldY + (col < n ? col : 0)];
+                return (row < nA && col < n) ? v : 0.0;
+            };
+            auto store = [&](int I, int J, const v4d& acc) {
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int a = 16 * I + kq + 4 * r, b2 = 16 * J + i16;
+                    if (a < nA && b2 <= a) {
+                        double v = acc[r];
+                        const int ra = Ar[a], rb = Ar[b2];
+                        if (ra < ms && rb < ms && ra / mc == rb / mc) {
+                            const int j = c.row_slack[ra % mc];
+                            if (j >= 0 && c.row_slack[rb % mc] == j)
+                                v += c.row_sign[ra % mc] * c.row_sign[rb % mc] / (2.0 * c.Qs[j]);
+                        }
+                        Sm[a * (a + 1) / 2 + b2] = v;
+                    }
+                }
+            };
+            for (int t0 = 2 * wv; t0 < NTt; t0 += 2 * (kPT / kWave)) {
+                int I0, J0, I1, J1;
+                tile_ij(t0, I0, J0);
+                const bool two = t0 + 1 < NTt;
+                tile_ij(two ? t0 + 1 : t0, I1, J1);
+                v4d a0 = {0.0, 0.0, 0.0, 0.0}, a1 = {0.0, 0.0, 0.0, 0.0};
+                for (int s = 0; s < KS; ++s) {
+                    const double yi0 = frag(I0, s), yj0 = frag(J0, s), yi1 = frag(I1, s), yj1 = frag(J1, s);
+                    a0 = __builtin_amdgcn_mfma_f64_16x16x4f64(yi0, yj0, a0, 0, 0, 0);
+                    a1 = __builtin_amdgcn_mfma_f64_16x16x4f64(yi1, yj1, a1, 0, 0, 0);
+                }
+                store(I0, J0, a0);
+                if (two) store(I1, J1, a1);
             }
-            Sm[e] = v;
         }
         __syncthreads();
         {
