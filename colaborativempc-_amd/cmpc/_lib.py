@@ -44,6 +44,8 @@ CMPC_FLAG_RESCUE = 32   # Riccati continuation of agents whose condensed factori
 CMPC_FLAG_FINISH = 64   # ... also of breakdowns already at the rounding floor (status 2)
 CMPC_FLAG_LANE = 128    # lane-per-agent stage-wise kernel, fp64
 CMPC_FLAG_POLISH = 256  # with RESCUE: active-set polish of breakdowns at the rounding floor (OSQP polish=True)
+CMPC_FLAG_ONE_WAVE = 512   # fused DS round: one wavefront per agent (the default)
+CMPC_FLAG_TWO_WAVES = 1024  # ... two wavefronts per agent (opt-in: bit-identical, no faster at 512 agents)
 
 
 class cmpc_opts(ct.Structure):

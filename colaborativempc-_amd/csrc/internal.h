@@ -31,6 +31,7 @@ struct MpcConst {
                   // or CMPC_FLAG_FP32 on dimensions without an fp32 Riccati instantiation)
     int f32;      // 1: CMPC_FLAG_FP32 on the stage-wise Riccati kernel (Cfg::F32; riccati = 1 as well)
     int polish;   // 1: CMPC_FLAG_POLISH (with rescue): active-set polish of breakdowns at the rounding floor
+    int waves;    // fused DS instantiation of the v3 kernel: wavefronts per agent (0, 1: one; 2: CMPC_FLAG_TWO_WAVES)
     unsigned long long ws_stride;  // doubles of MpcPtrs::ws per agent (set by mpc_launch; 0: no scratch)
     double tol;
     double qs_max;  // max(1, 2*max(Qs)) — slack residual scale
@@ -161,6 +162,9 @@ constexpr int kWarmStall = 3;
 __host__ __device__ inline bool hand_over(int stop, double best_m, const MpcConst& c) {
     return stop == kStopBreakdown && (c.finish || !(best_m < 1e3 * c.tol));
 }
+
+// v3 kernel, fused double-integrator round: two wavefronts per agent (MpcConst::waves == 2)
+bool mpc3_two_waves(const MpcConst& c, int batch);
 
 // Active-set polish (mpc_polish.hip): agents whose rescue image carries flag 2.
 size_t mpc_polish_lds_bytes(const MpcConst& c);

@@ -777,6 +777,7 @@ int mpc_prepare(const cmpc_mpc_dims* d, const cmpc_mpc_weights* wt, const cmpc_o
                  mpc_riccati_lds_bytes(*c) <= kMaxLdsBytes)
                     ? 1 : 0;
     c->finish = (c->rescue && (o->flags & CMPC_FLAG_FINISH)) ? 1 : 0;
+    c->waves = (o && (o->flags & CMPC_FLAG_TWO_WAVES)) ? 2 : ((o && (o->flags & CMPC_FLAG_ONE_WAVE)) ? 1 : 0);
     c->polish = 0;
     // (mpc_polish.hip: one lane per condensed variable in its H build, so n <= 64 — every condensed
     // solve, which is what carries the rescue image)

@@ -40,7 +40,39 @@ __host__ __device__ constexpr double sgn(int r) { return r < 4 ? 1.0 : -1.0; }
 
 struct Lds3 {
     int cst, A, B, C, H, Pq, x0, up, W, Gb, Yb, X, dX, yb, U, dU, rd, vb, thin, bU, Ld, red, stamps, Phi, Pst, total;
+    // two-wave mode (W2): the fields from W to stamps are each wave's private copy (wave 1's at + psz);
+    // exchange areas: wave 1's K tiles (xk), the predictor's rho and vb (xr, xv), dU of the two passes
+    // (xu0, xu1), flags (xf)
+    int psz, xk, xr, xv, xu0, xu1, xf;
 };
+
+// Two-wave mode (W2, the DS instantiation at <= 2 agents per CU): the K build's MFMA tiles split between
+// the waves (the VALU Gamma recursion runs on both); wave 1 hands its tiles to wave 0.  Wave 0 owns the
+// tiles below (balanced by the number of stages that touch each tile: 70 of 140 MFMAs at cfg3).
+__host__ __device__ constexpr bool w2_own0(int T, int ti, int tj) {
+    return T >= 4 ? (ti == 0 || (ti == 1 && tj == 0) || (ti == 3 && tj < 3))
+                  : (T == 3 ? (ti == 0 || (ti == 1 && tj == 0)) : ti == 0);
+}
+#ifndef CMPC_W2_RHS
+#define CMPC_W2_RHS 1
+#endif
+constexpr bool kW2Rhs = CMPC_W2_RHS != 0;  // (lab switch: the predictor right-hand side on wave 1)
+__host__ __device__ constexpr int w2_tiles1(int T) {
+    int c = 0;
+    for (int ti = 0; ti < T; ++ti)
+        for (int tj = 0; tj <= ti; ++tj) c += w2_own0(T, ti, tj) ? 0 : 1;
+    return c;
+}
+// slot of wave-1 tile (ti, tj) in the exchange (tiles in ascending (ti, tj) order)
+__host__ __device__ constexpr int w2_slot1(int T, int ti, int tj) {
+    int c = 0;
+    for (int a = 0; a < T; ++a)
+        for (int b = 0; b <= a; ++b) {
+            if (a == ti && b == tj) return c;
+            c += w2_own0(T, a, b) ? 0 : 1;
+        }
+    return c;
+}
 
 // LS (the reference's own agent, nx 9 / nu 2, built by lpv_build.hip): the model's structure is
 // fixed by LPV_Planner.py:493-585 and :279-380, and the images shrink to it —
@@ -82,10 +114,10 @@ __host__ __device__ constexpr bool seg_on() {
     return !LS && NX <= 4 && NU <= 2 && T >= 2;
 }
 
-template <int T, int NX, int NU, int NB, bool LS = false, bool DS = false>
+template <int T, int NX, int NU, int NB, bool LS = false, bool DS = false, bool W2 = false>
 __host__ __device__ inline Lds3 lds3_layout(int N) {
     constexpr int NP = 16 * T, MC = 4 + NB;
-    Lds3 L;
+    Lds3 L{};
     int o = 0;
     auto take = [&](int cnt) {
         int r = o;
@@ -100,6 +132,12 @@ __host__ __device__ inline Lds3 lds3_layout(int N) {
     L.Pq = take((N + 1) * NX);
     L.x0 = take(NX);
     L.up = take(NU);
+    // segmented forward simulation (kSeg): the transitions Phi_k of stages (a_1, N] (fwd3seg); 352
+    // doubles at N = 30, NX = 4
+    L.Phi = take(seg_on<T, NX, NU, LS>() ? (N - seg_a(1, N)) * NX * NX : 0);
+    // ... and the transposed transitions Psi'_k of the segmented adjoint (psi3seg): 352 doubles at N = 30
+    L.Pst = take(seg_on<T, NX, NU, LS>() ? (seg_b(3, N) - 1) * NX * NX : 0);
+    const int pbeg = o;
     // the Cholesky panel scratch ((T-1) x 16 x 17) aliases W | dX | yb after the K build (the stage
     // weights are consumed by then, and the residuals' adjoints are done while the passes' have not
     // begun); Gb extends them only where they are smaller than that (short horizons, small NX).  At
@@ -122,11 +160,17 @@ __host__ __device__ inline Lds3 lds3_layout(int N) {
     L.Ld = take(T * 16 * 17);
     L.red = take(16);
     L.stamps = take(kStampSlots);
-    // segmented forward simulation (kSeg): the transitions Phi_k of stages (a_1, N] (fwd3seg); 352
-    // doubles at N = 30, NX = 4
-    L.Phi = take(seg_on<T, NX, NU, LS>() ? (N - seg_a(1, N)) * NX * NX : 0);
-    // ... and the transposed transitions Psi'_k of the segmented adjoint (psi3seg): 352 doubles at N = 30
-    L.Pst = take(seg_on<T, NX, NU, LS>() ? (seg_b(3, N) - 1) * NX * NX : 0);
+    L.psz = o - pbeg;
+    if (W2) {
+        constexpr int RX = (4 + NB) > 2 * NU ? (4 + NB) : 2 * NU;
+        o += L.psz;  // wave 1's private copy
+        L.xk = take(w2_tiles1(T) * 256);
+        L.xr = take(64 * RX);
+        L.xv = take(NP);
+        L.xu0 = take(NP);
+        L.xu1 = take(NP);
+        L.xf = take(2);
+    }
     L.total = o;
     return L;
 }
@@ -511,18 +555,36 @@ __device__ __forceinline__ double bpsi3(const double* B, const double* psi, int 
 
 }  // namespace
 
-template <int T, int NX, int NU, int NB, bool LS = false, bool DS = false>
-__global__ __launch_bounds__(64, 1) void mpc_ipm3_kernel(const MpcConst c, const MpcPtrs P) {
+// L5 (with LS): Q's diagonal is zero on states 1, 2, 5, 6 (the reference's Q = diag(10, 0, 0, 25, 10, 0, 0,
+// 0, 0), config_LPV.py:7), so W_k = 2Q + the rows' weights is nonzero only on states {0, 3, 4, 7, 8}: the
+// K build's MFMA contraction runs over those five (two k-steps of 4) instead of all nine (three).
+// W2: two wavefronts per agent (a 128-lane workgroup, one wave per SIMD, two agents per CU): for batches
+// that leave SIMDs idle at one wave per agent (<= 512 agents on 256 CUs: BASELINE cfg4's shard).  Both waves
+// run the whole iteration on private copies of the mutable images (the same arithmetic in the same order, so
+// they hold bit-identical values and take the same wave-uniform decisions), except:
+//   * the K build's MFMAs: each wave accumulates its own tiles (w2_own0); wave 1 hands its tiles to wave 0
+//     through LDS (each tile keeps its accumulation order: bit-identical to one wave);
+//   * while wave 0 factors K and inverts the diagonal blocks, wave 1 forms the predictor's right-hand side
+//     (rho, C' rho~, the adjoint recursion, vb) and hands rho and vb over;
+//   * the triangular solves run on wave 0 only; wave 1 takes each pass's dU from LDS.
+// Wave 0 alone writes the outputs.
+template <int T, int NX, int NU, int NB, bool LS = false, bool DS = false, bool L5 = false, bool W2 = false>
+__global__ __launch_bounds__(W2 ? 128 : 64, 1) void mpc_ipm3_kernel(const MpcConst c, const MpcPtrs P) {
     constexpr int MC = 4 + NB, NS = 3, NT = T * (T + 1) / 2, NP = 16 * T, NXP = (NX + 3) & ~3;
     constexpr int NI = 2 * NU, RX = MC > NI ? MC : NI;
     constexpr int CW = ls_cw<NB>();  // LS: row coefficients per stage
     static_assert(!LS || (NX == 9 && NU == 2), "LS: the reference's agent model");
     static_assert(!DS || (NX == 4 && NU == 2 && !LS), "DS: the 2-D double integrator");
+    static_assert(!L5 || LS, "L5: a variant of LS");
     constexpr int CWD = ds_cw<NB>();  // DS: plane coefficients per stage
     extern __shared__ __attribute__((aligned(16))) double sm[];
-    const int l0 = threadIdx.x, b = blockIdx.x, N = c.N, n = N * NU, ms = N * MC;
+    static_assert(!W2 || DS, "W2: the fused double-integrator instantiation");
+    const int l0 = threadIdx.x & 63, b = blockIdx.x, N = c.N, n = N * NU, ms = N * MC;
     const int l = l0;
-    const Lds3 L = lds3_layout<T, NX, NU, NB, LS, DS>(N);
+    // the wave index as a scalar (wave-uniform: the branches on it are scalar, never exec-masked)
+    const int wvi = W2 ? __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)) : 0;
+    const Lds3 L = lds3_layout<T, NX, NU, NB, LS, DS, W2>(N);
+    const int po = wvi * L.psz;  // this wave's private images
     double* Q2 = sm + L.cst;          // 2Q
     double* R2 = Q2 + NX * NX;        // 2R
     double* dR2 = R2 + NU * NU;       // 2dR
@@ -536,22 +598,22 @@ __global__ __launch_bounds__(64, 1) void mpc_ipm3_kernel(const MpcConst c, const
     double* sP = sm + L.Pq;
     double* sx0 = sm + L.x0;
     double* sup = sm + L.up;
-    double* sW = sm + L.W;
-    double* X = sm + L.X;
-    double* dX = sm + L.dX;
-    double* yb = sm + L.yb;
-    double* U = sm + L.U;
-    double* dU = sm + L.dU;
-    double* rd = sm + L.rd;
-    double* vb = sm + L.vb;
-    double* thin = sm + L.thin;
-    double* bU = sm + L.bU;
-    double* Ld = sm + L.Ld;
-    double* red = sm + L.red;
+    double* sW = sm + po + L.W;
+    double* X = sm + po + L.X;
+    double* dX = sm + po + L.dX;
+    double* yb = sm + po + L.yb;
+    double* U = sm + po + L.U;
+    double* dU = sm + po + L.dU;
+    double* rd = sm + po + L.rd;
+    double* vb = sm + po + L.vb;
+    double* thin = sm + po + L.thin;
+    double* bU = sm + po + L.bU;
+    double* Ld = sm + po + L.Ld;
+    double* red = sm + po + L.red;
     double* SP = sW;  // Cholesky panel scratch (aliases W | Gb after the K build)
     const bool stamp = P.stamps != nullptr;
     // diagnostic per-section clock sums live in LDS (registers stay with the solver)
-    unsigned long long* tsum = reinterpret_cast<unsigned long long*>(sm + L.stamps);
+    unsigned long long* tsum = reinterpret_cast<unsigned long long*>(sm + po + L.stamps);
     if (l < kStampSlots) tsum[l] = 0;
     unsigned long long t_a = stamp ? clock64_() : 0, t_b = 0;
 #define STAMP(slot)                                \
@@ -562,7 +624,9 @@ __global__ __launch_bounds__(64, 1) void mpc_ipm3_kernel(const MpcConst c, const
     }
 
     // ---------------- stage the agent's data and the shared weights into LDS ----------------
-    {
+    // (W2: the shared images by wave 0 alone — the fused row build accumulates into the linear cost, so two
+    // writers would race — then a barrier before their first use below)
+    if (wvi == 0) {
         const double* gA = P.A + (size_t)b * N * NX * NX;
         const double* gB = P.B + (size_t)b * N * NX * NU;
         const double* gC = P.C + (size_t)b * N * MC * NX;
@@ -618,6 +682,8 @@ __global__ __launch_bounds__(64, 1) void mpc_ipm3_kernel(const MpcConst c, const
             ub[l] = c.u_ub[l];
             lb[l] = c.u_lb[l];
         }
+    }
+    {
         for (int i = l; i < NP; i += 64) {
             U[i] = 0.0;
             dU[i] = 0.0;
@@ -666,6 +732,7 @@ __global__ __launch_bounds__(64, 1) void mpc_ipm3_kernel(const MpcConst c, const
         }
     };
     wsync();
+    if constexpr (W2) __syncthreads();  // wave 0's shared images
     if (own) {
 #pragma unroll
         for (int r = 0; r < RX; ++r)
@@ -683,10 +750,13 @@ __global__ __launch_bounds__(64, 1) void mpc_ipm3_kernel(const MpcConst c, const
     };
     double* sPst = sm + L.Pst;
     if constexpr (kSeg) {
-        phi_build<NX>(l, N, sA, sPhi);
-        psi_build<NX>(l, N, sA, sPst);
+        if (wvi == 0) {
+            phi_build<NX>(l, N, sA, sPhi);
+            psi_build<NX>(l, N, sA, sPst);
+        }
         wsync();
     }
+    if constexpr (W2) __syncthreads();  // wave 0's transitions
     fwd(l, sx0, U, X);
     wsync();
 
@@ -866,6 +936,36 @@ __global__ __launch_bounds__(64, 1) void mpc_ipm3_kernel(const MpcConst c, const
         kkt = nmax(res, mu);
         STAMP(2);
         const double merit = nmax(res, 1e4 * mu);
+#ifdef CMPC_DBG_MERIT  // lab: the merit of iterations 1..15 (instead of the section clocks)
+        if (l == 0 && wvi == 0 && P.stamps && it < kStampSlots)
+            P.stamps[(size_t)b * kStampSlots + it] = (unsigned long long)__double_as_longlong(merit);
+#endif
+        if constexpr (W2) {
+            // wave 0 decides for the pair: the waves hold identical values, and taking wave 0's verdict at a
+            // barrier keeps any divergence from leaving one wave waiting at a barrier the other never reaches
+            int dec = 0;
+            if (!isfinite(merit)) {
+                dec = kStopNonFinite;
+            } else {
+                if (merit < best_m) {
+                    best_m = merit;
+                    best_kkt = kkt;
+                    best_it = it;
+                    for (int i = l; i < NP; i += 64) bU[i] = U[i];
+#pragma unroll
+                    for (int j = 0; j < NS; ++j) bsg[j] = sg[j];
+                }
+                if (merit < c.tol) dec = kStopConverged;
+                else if (best_m < 1e3 * c.tol && it - best_it >= kStallIters) dec = kStopStalled;
+            }
+            if (wvi == 0 && l == 0) sm[L.xf + 1] = (double)dec;
+            __syncthreads();
+            dec = (int)sm[L.xf + 1];
+            if (dec) {
+                stop = dec;
+                break;
+            }
+        } else {
         if (!isfinite(merit)) {
             stop = kStopNonFinite;
             break;
@@ -885,6 +985,7 @@ __global__ __launch_bounds__(64, 1) void mpc_ipm3_kernel(const MpcConst c, const
         if (best_m < 1e3 * c.tol && it - best_it >= kStallIters) {
             stop = kStopStalled;
             break;
+        }
         }
 
         // ================= Newton matrix K = Gamma' W Gamma + Hc + diag =================
@@ -1081,23 +1182,26 @@ __global__ __launch_bounds__(64, 1) void mpc_ipm3_kernel(const MpcConst c, const
                 }
 #pragma unroll
                 for (int s2 = 0; s2 < NX; ++s2) g[s2] = gn[s2];
-                double gf[NXP], yf[NXP];
-                static_for<0, NXP>([&](auto s_c) __attribute__((always_inline)) {
-                    constexpr int s2 = decltype(s_c)::value;
+                // contraction slot j -> state s2 (L5: the five states W_k weights, zero padding after)
+                constexpr int KP = L5 ? 8 : NXP;
+                double gf[KP], yf[KP];
+                static_for<0, KP>([&](auto j_c) __attribute__((always_inline)) {
+                    constexpr int j = decltype(j_c)::value;
+                    constexpr int s2 = L5 ? (j == 0 ? 0 : j == 1 ? 3 : j == 2 ? 4 : j == 3 ? 7 : j == 4 ? 8 : NX) : j;
                     if constexpr (s2 < NX) {
-                        gf[s2] = g[s2];
-                        if constexpr (s2 == 0) yf[s2] = w5[0] * g[0];
-                        else if constexpr (s2 == 3) yf[s2] = w5[1] * g[3];
-                        else if constexpr (s2 == 7) yf[s2] = fma(w5[3], g[8], w5[2] * g[7]);
-                        else if constexpr (s2 == 8) yf[s2] = fma(w5[4], g[8], w5[3] * g[7]);
-                        else yf[s2] = q2d[s2] * g[s2];
+                        gf[j] = g[s2];
+                        if constexpr (s2 == 0) yf[j] = w5[0] * g[0];
+                        else if constexpr (s2 == 3) yf[j] = w5[1] * g[3];
+                        else if constexpr (s2 == 7) yf[j] = fma(w5[3], g[8], w5[2] * g[7]);
+                        else if constexpr (s2 == 8) yf[j] = fma(w5[4], g[8], w5[3] * g[7]);
+                        else yf[j] = q2d[s2] * g[s2];
                     } else {
-                        gf[s2] = 0.0;
-                        yf[s2] = 0.0;
+                        gf[j] = 0.0;
+                        yf[j] = 0.0;
                     }
                 });
 #pragma unroll
-                for (int q = 0; q < NXP; q += 4) {
+                for (int q = 0; q < KP; q += 4) {
                     transpose_rows4(gf[q], gf[q + 1], gf[q + 2], gf[q + 3]);
                     transpose_rows4(yf[q], yf[q + 1], yf[q + 2], yf[q + 3]);
 #pragma unroll
@@ -1142,8 +1246,11 @@ __global__ __launch_bounds__(64, 1) void mpc_ipm3_kernel(const MpcConst c, const
             fetchA(0, a0);
             // W_k is loaded first, then the next stage's A (pf): LDS returns in order, so W_k's wait
             // (after the Gamma chain) does not include the prefetch
-            auto stage = [&](auto tau_c, int kk, const double* av, auto pf) __attribute__((always_inline)) {
+            // role: 2 every tile (one wave per agent); W2: 0 / 1 the tiles of wave 0 / 1 (w2_own0), each
+            // wave's K build a copy of its own with a static MFMA set (no branch between accumulations)
+            auto stage = [&](auto tau_c, auto role_c, int kk, const double* av, auto pf) __attribute__((always_inline)) {
                 constexpr int tau = decltype(tau_c)::value;
+                constexpr int role = decltype(role_c)::value;
                 const double* Ak = sA + kk * NX * NX;
                 const double* Wk = sW + kk * (DS ? kDsW : NX * NX);
                 constexpr int PW = DS ? kDsW : PA;
@@ -1195,14 +1302,18 @@ __global__ __launch_bounds__(64, 1) void mpc_ipm3_kernel(const MpcConst c, const
                 for (int q = 0; q < NXP; q += 4) {
                     transpose_rows4(gf[q], gf[q + 1], gf[q + 2], gf[q + 3]);
                     transpose_rows4(yf[q], yf[q + 1], yf[q + 2], yf[q + 3]);
-#pragma unroll
-                    for (int ti = 0; ti <= tau; ++ti)
-#pragma unroll
-                        for (int tj = 0; tj <= ti; ++tj)
-                            acc[ti * (ti + 1) / 2 + tj] = __builtin_amdgcn_mfma_f64_16x16x4f64(
-                                gf[q + ti], yf[q + tj], acc[ti * (ti + 1) / 2 + tj], 0, 0, 0);
+                    static_for<0, tau + 1>([&](auto ti_c) __attribute__((always_inline)) {
+                        constexpr int ti = decltype(ti_c)::value;
+                        static_for<0, ti + 1>([&](auto tj_c) __attribute__((always_inline)) {
+                            constexpr int tj = decltype(tj_c)::value;
+                            if constexpr (role == 2 || w2_own0(T, ti, tj) == (role == 0))
+                                acc[ti * (ti + 1) / 2 + tj] = __builtin_amdgcn_mfma_f64_16x16x4f64(
+                                    gf[q + ti], yf[q + tj], acc[ti * (ti + 1) / 2 + tj], 0, 0, 0);
+                        });
+                    });
                 }
             };
+            auto kbuild = [&](auto role_c) __attribute__((always_inline)) {
             static_for<0, T>([&](auto tau_c) __attribute__((always_inline)) {
                 constexpr int tau = decltype(tau_c)::value;
                 // stages whose Gamma_{k+1} has tiles 0..tau nonzero (last column (k+1)NU-1 in tile tau)
@@ -1211,19 +1322,57 @@ __global__ __launch_bounds__(64, 1) void mpc_ipm3_kernel(const MpcConst c, const
                 const int ke = ke0 < N ? ke0 : N;
                 int kk = kb;
                 for (; kk + 1 < ke; kk += 2) {
-                    stage(tau_c, kk, a0, [&]() __attribute__((always_inline)) { fetchA(kk + 1, a1); });
-                    stage(tau_c, kk + 1, a1,
+                    stage(tau_c, role_c, kk, a0, [&]() __attribute__((always_inline)) { fetchA(kk + 1, a1); });
+                    stage(tau_c, role_c, kk + 1, a1,
                           [&]() __attribute__((always_inline)) { fetchA(kk + 2 < N ? kk + 2 : N - 1, a0); });
                 }
                 if (kk < ke) {
-                    stage(tau_c, kk, a0,
+                    stage(tau_c, role_c, kk, a0,
                           [&]() __attribute__((always_inline)) { fetchA(kk + 1 < N ? kk + 1 : N - 1, a1); });
 #pragma unroll
                     for (int i = 0; i < PA; ++i) a0[i] = a1[i];
                 }
             });
+            };
+            if constexpr (!W2) {
+                kbuild(std::integral_constant<int, 2>{});
+            } else if (wvi == 0) {
+                kbuild(std::integral_constant<int, 0>{});
+            } else {
+                kbuild(std::integral_constant<int, 1>{});
+            }
         }
         STAMP(4);
+        if constexpr (W2) {  // wave 1's tiles to wave 0 (slot-major, [register][lane]: conflict-free)
+            double* xk = sm + L.xk;
+            if (wvi != 0) {
+                static_for<0, T>([&](auto ti_c) __attribute__((always_inline)) {
+                    constexpr int ti = decltype(ti_c)::value;
+                    static_for<0, ti + 1>([&](auto tj_c) __attribute__((always_inline)) {
+                        constexpr int tj = decltype(tj_c)::value;
+                        if constexpr (!w2_own0(T, ti, tj)) {
+#pragma unroll
+                            for (int r = 0; r < 4; ++r)
+                                xk[(w2_slot1(T, ti, tj) * 4 + r) * 64 + l] = acc[ti * (ti + 1) / 2 + tj][r];
+                        }
+                    });
+                });
+            }
+            __syncthreads();
+            if (wvi == 0) {
+                static_for<0, T>([&](auto ti_c) __attribute__((always_inline)) {
+                    constexpr int ti = decltype(ti_c)::value;
+                    static_for<0, ti + 1>([&](auto tj_c) __attribute__((always_inline)) {
+                        constexpr int tj = decltype(tj_c)::value;
+                        if constexpr (!w2_own0(T, ti, tj)) {
+#pragma unroll
+                            for (int r = 0; r < 4; ++r)
+                                acc[ti * (ti + 1) / 2 + tj][r] = xk[(w2_slot1(T, ti, tj) * 4 + r) * 64 + l];
+                        }
+                    });
+                });
+            }
+        }
         // + 2R + 2D'dR D (block tridiagonal) + input-row curvature; identity on the padding.
         // The band half-width 2NU - 1 < 16 touches only the diagonal and first sub-diagonal tiles;
         // branch-free: unconditional (clamped) LDS reads and selects.
@@ -1250,6 +1399,32 @@ __global__ __launch_bounds__(64, 1) void mpc_ipm3_kernel(const MpcConst c, const
 
         // ================= blocked Cholesky in the accumulator registers =================
         bool chol_ok = true;
+        // diagonal blocks L_JJ -> L_JJ^{-1} in place (LDS, lower triangle; zeros above): row q of the
+        // wave inverts block q, lane (q, j) forms column j by forward substitution.  Done once per
+        // factorisation, it turns every in-block substitution of the four triangular solves per
+        // iteration (16 dependent broadcast -> multiply -> fma steps) into a 16-term mat-vec
+        auto invert_diag = [&]() __attribute__((always_inline)) {
+            const int q = l >> 4, j = l & 15;
+            double* Lq = Ld + (q < T ? q : 0) * 272;
+            double x[16];
+            static_for<0, 16>([&](auto i_c) __attribute__((always_inline)) {
+                constexpr int i = decltype(i_c)::value;
+                double s0 = (j == i) ? 1.0 : 0.0, s1 = 0.0;
+#pragma unroll
+                for (int c = 0; c < i; ++c) {
+                    if (c & 1) s1 = fma(-Lq[i * 17 + c], x[c], s1);
+                    else s0 = fma(-Lq[i * 17 + c], x[c], s0);
+                }
+                x[i] = (s0 + s1) * rcp_d(Lq[i * 17 + i]);
+            });
+            wsync();
+            if (q < T) {
+#pragma unroll
+                for (int i = 0; i < 16; ++i) Lq[i * 17 + j] = x[i];
+            }
+            wsync();
+        };
+        if (!W2 || wvi == 0) {
 #pragma unroll
         for (int J = 0; J < T; ++J) {
             const int JJ = J * (J + 1) / 2 + J;
@@ -1343,50 +1518,12 @@ __global__ __launch_bounds__(64, 1) void mpc_ipm3_kernel(const MpcConst c, const
             }
             STAMP(7);
         }
-        if (!chol_ok) {
-            stop = kStopBreakdown;
-            if (c.rescue && P.ws) {  // hand the iterate to the Riccati rescue (hand_doubles, internal.h)
-                write_image();
-                if (l == 0) P.ws[(size_t)b * c.ws_stride + 1] = it - 1;
-            }
-            break;
         }
-        // diagonal blocks L_JJ -> L_JJ^{-1} in place (LDS, lower triangle; zeros above): row q of the
-        // wave inverts block q, lane (q, j) forms column j by forward substitution.  Done once per
-        // factorisation, it turns every in-block substitution of the four triangular solves per
-        // iteration (16 dependent broadcast -> multiply -> fma steps) into a 16-term mat-vec
-        {
-            const int q = l >> 4, j = l & 15;
-            double* Lq = Ld + (q < T ? q : 0) * 272;
-            double x[16];
-            static_for<0, 16>([&](auto i_c) __attribute__((always_inline)) {
-                constexpr int i = decltype(i_c)::value;
-                double s0 = (j == i) ? 1.0 : 0.0, s1 = 0.0;
-#pragma unroll
-                for (int c = 0; c < i; ++c) {
-                    if (c & 1) s1 = fma(-Lq[i * 17 + c], x[c], s1);
-                    else s0 = fma(-Lq[i * 17 + c], x[c], s0);
-                }
-                x[i] = (s0 + s1) * rcp_d(Lq[i * 17 + i]);
-            });
-            wsync();
-            if (q < T) {
-#pragma unroll
-                for (int i = 0; i < 16; ++i) Lq[i * 17 + j] = x[i];
-            }
-            wsync();
-        }
-        // this lane's diagonal block (J = lane >> 4) of L^{-1}: row / column (l & 15)
-        const double* Lme = Ld + ((l >> 4) < T ? (l >> 4) : 0) * 272;
-
         // ================= predictor / corrector =================
-        {
-            int ozi;
-            asm volatile("v_mov_b32 %0, 0" : "=v"(ozi));
-            theta((double)ozi);
-        }
         double sig_c = 0.0, alpha = 0.0;
-        for (int pass = 0; pass < 2; ++pass) {
+        // the right-hand side of a pass: rho (pass 1: Mehrotra's second-order term from the predictor still
+        // in (rho, gdu, dsg)), C' rho~ into yb, the adjoint recursion, vb
+        auto pass_rhs = [&](int pass) __attribute__((always_inline)) {
             // pass 1: Mehrotra's second-order term dt_aff * dl_aff from the predictor still in (rho, gdu, dsg)
 #pragma unroll
             for (int r = 0; r < RX; ++r) {
@@ -1460,6 +1597,50 @@ __global__ __launch_bounds__(64, 1) void mpc_ipm3_kernel(const MpcConst c, const
                 }
             }
             wsync();
+        };
+        if constexpr (W2) {
+            // wave 1 forms the predictor's right-hand side while wave 0 factors; then rho (per lane) and vb
+            // change hands, with wave 0's factorisation verdict
+            if (kW2Rhs && wvi != 0) {
+                int ozi;
+                asm volatile("v_mov_b32 %0, 0" : "=v"(ozi));
+                theta((double)ozi);
+                pass_rhs(0);
+#pragma unroll
+                for (int r = 0; r < RX; ++r) sm[L.xr + r * 64 + l] = rho[r];
+                for (int i = l; i < NP; i += 64) sm[L.xv + i] = vb[i];
+            } else if (l == 0) {
+                sm[L.xf] = chol_ok ? 1.0 : 0.0;
+            }
+            __syncthreads();
+            chol_ok = sm[L.xf] != 0.0;
+        }
+        if (!chol_ok) {
+            stop = kStopBreakdown;
+            if (wvi == 0 && c.rescue && P.ws) {  // hand the iterate to the Riccati rescue (hand_doubles, internal.h)
+                write_image();
+                if (l == 0) P.ws[(size_t)b * c.ws_stride + 1] = it - 1;
+            }
+            break;
+        }
+        if (wvi == 0) invert_diag();  // (W2: after the hand-over; before it, its registers spilled)
+        // this lane's diagonal block (J = lane >> 4) of L^{-1}: row / column (l & 15)
+        const double* Lme = Ld + ((l >> 4) < T ? (l >> 4) : 0) * 272;
+        if (wvi == 0) {
+            int ozi;
+            asm volatile("v_mov_b32 %0, 0" : "=v"(ozi));
+            theta((double)ozi);
+        }
+        for (int pass = 0; pass < 2; ++pass) {
+            if (!W2 || !kW2Rhs || pass) {
+                pass_rhs(pass);
+            } else if (wvi == 0) {  // W2, pass 0: wave 1's rho and vb
+#pragma unroll
+                for (int r = 0; r < RX; ++r) rho[r] = sm[L.xr + r * 64 + l];
+                for (int i = l; i < NP; i += 64) vb[i] = sm[L.xv + i];
+                wsync();
+            }
+            if (wvi == 0) {  // (W2: the triangular solves on wave 0, which holds L)
             // ---- forward solve L y = vb (block rows; L_JI tiles in acc, L_JJ in LDS) ----
             // this lane's row of its row group's inverted diagonal block: the same for every J
             // (only row group J's result is kept), so it is loaded once, not per block row
@@ -1523,6 +1704,15 @@ __global__ __launch_bounds__(64, 1) void mpc_ipm3_kernel(const MpcConst c, const
                 wsync();
             }
             for (int i = l; i < NP; i += 64) dU[i] = (i < n) ? vb[i] : 0.0;
+            }
+            if constexpr (W2) {  // each pass's dU to wave 1 (one slot per pass)
+                double* xu = sm + (pass ? L.xu1 : L.xu0);
+                if (wvi == 0)
+                    for (int i = l; i < NP; i += 64) xu[i] = dU[i];
+                __syncthreads();
+                if (wvi != 0)
+                    for (int i = l; i < NP; i += 64) dU[i] = xu[i];
+            }
             wsync();
             STAMP(10);
             fwd(l, nullptr, dU, dX);
@@ -1605,6 +1795,9 @@ __global__ __launch_bounds__(64, 1) void mpc_ipm3_kernel(const MpcConst c, const
         STAMP(13);
     }
     if (it > c.max_iter) it = c.max_iter;
+    if constexpr (W2) {  // wave 0 holds everything wave 1 has (bit-identical) and writes the outputs
+        if (wvi != 0) return;
+    }
     wsync();
     int status = CMPC_SOLVED;
     // a converged endpoint with a weakly active row (kPolishDegenerate) is polished as well
@@ -1670,33 +1863,36 @@ __global__ __launch_bounds__(64, 1) void mpc_ipm3_kernel(const MpcConst c, const
             hd[0] = ho ? 1.0 : (pol ? 2.0 : 0.0);
             if (pol) hd[1] = best_m;
         }
+#ifndef CMPC_DBG_MERIT
         if (stamp) {
             unsigned long long* st = P.stamps + (size_t)b * kStampSlots;
             for (int i = 0; i < kStampSlots - 1; ++i) st[i] = tsum[i];
             st[kStampSlots - 1] = it;
         }
+#endif
     }
 #undef STAMP
 #undef ACT
 }
 
-template <int T, int NX, int NU, int NB, bool LS, bool DS>
+template <int T, int NX, int NU, int NB, bool LS, bool DS, bool L5, bool W2 = false>
 static hipError_t launch3(const MpcConst& c, const MpcPtrs& p, int batch, hipStream_t s) {
-    const size_t lds = sizeof(double) * (size_t)lds3_layout<T, NX, NU, NB, LS, DS>(c.N).total;
-    hipError_t e = hipFuncSetAttribute((const void*)mpc_ipm3_kernel<T, NX, NU, NB, LS, DS>,
+    const size_t lds = sizeof(double) * (size_t)lds3_layout<T, NX, NU, NB, LS, DS, W2>(c.N).total;
+    hipError_t e = hipFuncSetAttribute((const void*)mpc_ipm3_kernel<T, NX, NU, NB, LS, DS, L5, W2>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL((mpc_ipm3_kernel<T, NX, NU, NB, LS, DS>), dim3(batch), dim3(64), lds, s, c, p);
+    hipLaunchKernelGGL((mpc_ipm3_kernel<T, NX, NU, NB, LS, DS, L5, W2>), dim3(batch), dim3(W2 ? 128 : 64), lds, s,
+                       c, p);
     return hipGetLastError();
 }
 
-template <int NX, int NU, int NB, bool LS = false, bool DS = false>
+template <int NX, int NU, int NB, bool LS = false, bool DS = false, bool L5 = false, bool W2 = false>
 static hipError_t launch3_t(const MpcConst& c, const MpcPtrs& p, int batch, hipStream_t s) {
     switch (c.npad / 16) {
-        case 1: return launch3<1, NX, NU, NB, LS, DS>(c, p, batch, s);
-        case 2: return launch3<2, NX, NU, NB, LS, DS>(c, p, batch, s);
-        case 3: return launch3<3, NX, NU, NB, LS, DS>(c, p, batch, s);
-        default: return launch3<4, NX, NU, NB, LS, DS>(c, p, batch, s);
+        case 1: return launch3<1, NX, NU, NB, LS, DS, L5, W2>(c, p, batch, s);
+        case 2: return launch3<2, NX, NU, NB, LS, DS, L5, W2>(c, p, batch, s);
+        case 3: return launch3<3, NX, NU, NB, LS, DS, L5, W2>(c, p, batch, s);
+        default: return launch3<4, NX, NU, NB, LS, DS, L5, W2>(c, p, batch, s);
     }
 }
 
@@ -1719,18 +1915,31 @@ static bool q_diagonal(const MpcConst& c) {
         return true;                                        \
     }
 // the reference's agent as built by lpv_build.hip (MpcConst::lpv; the fused DI rows never apply)
-#define CASE_LS(NB_)                                                        \
-    if (c.lpv && c.nx == 9 && c.nu == 2 && nb == NB_ && !p.fuse.on) {       \
-        *err = launch3_t<9, 2, NB_, true>(c, p, batch, s);                  \
-        return true;                                                        \
+#define CASE_LS(NB_)                                                                              \
+    if (c.lpv && c.nx == 9 && c.nu == 2 && nb == NB_ && !p.fuse.on) {                             \
+        *err = c.lpv == 2 ? launch3_t<9, 2, NB_, true, false, true>(c, p, batch, s)               \
+                          : launch3_t<9, 2, NB_, true>(c, p, batch, s);                           \
+        return true;                                                                              \
     }
-// the fused double-integrator round with a diagonal Q (DS images; the dense form gives the same bits)
+// the fused double-integrator round with a diagonal Q (DS images; the dense form gives the same bits);
+// two wavefronts per agent where one per agent would leave SIMDs idle (mpc3_two_waves)
 #define CASE_DS(NB_)                                                                   \
     if (p.fuse.on && c.nx == 4 && c.nu == 2 && nb == NB_ && q_diagonal(c)) {           \
-        *err = launch3_t<4, 2, NB_, false, true>(c, p, batch, s);                      \
+        *err = mpc3_two_waves(c, batch) ? launch3_t<4, 2, NB_, false, true, false, true>(c, p, batch, s) \
+                                        : launch3_t<4, 2, NB_, false, true>(c, p, batch, s); \
         return true;                                                                   \
     }
 #if CMPC_V3_SET == 1
+// Two-wave mode: opt-in (CMPC_FLAG_TWO_WAVES).  Measured at 512 agents on one MI355X (tools/w2_ab.py, 20 cfg3
+// rounds, bit-identical results): 0.646 ms per launch against 0.640 ms with one wave.  Wave 0's K build
+// shrinks 19.9k -> 15.8k clk per iteration and the predictor's right-hand side leaves its path, but the five
+// barriers per iteration, the second wave's LDS traffic on the same CU and a few spilled registers take
+// the gain back (tools/stamps.py --two-waves).
+bool mpc3_two_waves(const MpcConst& c, int batch) {
+    (void)batch;
+    return c.waves == 2;
+}
+
 // host: the LDS image of the instantiation mpc3_try_launch picks (the same coverage rules)
 size_t mpc3_lds_bytes(const MpcConst& c) {
     if (c.ns != 3 || c.N > 32 || c.mc < 4 || c.n > 64) return 0;

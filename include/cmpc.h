@@ -93,8 +93,14 @@ typedef struct cmpc_ctx cmpc_ctx;
                                its active set {lambda_r > t_r} as exact, solves that equality-constrained QP
                                (range-space KKT, two active-set corrections) and returns it when its merit
                                is lower (status 1 below tol) */
+#define CMPC_FLAG_ONE_WAVE 512  /* the condensed kernel's fused double-integrator instantiation: one wavefront per
+                                   agent (the default) */
+#define CMPC_FLAG_TWO_WAVES 1024 /* ... two wavefronts per agent (a 128-lane workgroup: split K build, the
+                                   predictor's right-hand side on the second wave); bit-identical results, no
+                                   faster at 512 agents on one MI355X, so opt-in */
 #define CMPC_FLAG_ALL (CMPC_FLAG_GENERIC | CMPC_FLAG_FP32 | CMPC_FLAG_RICCATI | CMPC_FLAG_RESCUE | CMPC_FLAG_FINISH | \
-                       CMPC_FLAG_LANE | CMPC_FLAG_POLISH)  /* other bits: CMPC_ERR_ARG */
+                       CMPC_FLAG_LANE | CMPC_FLAG_POLISH | CMPC_FLAG_ONE_WAVE | CMPC_FLAG_TWO_WAVES)
+                       /* other bits: CMPC_ERR_ARG */
 
 typedef struct {
     double tol;    /* relative stationarity/feasibility tolerance (complementarity: 1e-4*tol); <= 0 selects 1e-9 */
@@ -195,7 +201,9 @@ typedef struct {
     int lds_bytes;     /* dynamic LDS per workgroup */
     int wg_per_cu;     /* workgroups resident per CU */
     int agents_per_wg; /* 1, or 32 (lane solver) */
-    int waves_per_agent;   /* wavefronts of one agent's workgroup (1; 2: the condensed kernel's small-batch mode) */
+    int waves_per_agent;   /* wavefronts of one agent's workgroup (1; 2: the condensed kernel's small-batch mode,
+                              CMPC_FLAG_ONE_WAVE / CMPC_FLAG_TWO_WAVES); agents of a fused double-integrator round
+                              only (cmpc_di_solve_dev), so the plan of a structured batch reports 1 */
     /* The rescue policy (CMPC_FLAG_RESCUE [| CMPC_FLAG_POLISH]) adds launches the fields above do not
      * describe: the polish kernel (before the Riccati hand-over and after the Riccati passes; one
      * 256-thread workgroup per agent, agents without a flag return at once) and two Riccati passes.

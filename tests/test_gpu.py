@@ -325,6 +325,41 @@ def test_fused_round_bit_equal_to_build_then_solve(gpu_ctx, n, N, nb, dim):
     assert (U.status.cpu().numpy() == 1).mean() >= 0.99
 
 
+@pytest.mark.parametrize("n,N", [(512, 30), (96, 20)])
+def test_two_wave_mode_bit_equal_and_matches_c_restatement(gpu_ctx, n, N):
+    """The v3 kernel's two-wavefront mode (CMPC_FLAG_TWO_WAVES: split K build, the predictor's right-hand
+    side on the second wave) on BASELINE cfg4's per-GPU shard (512 agents, N = 30) and a T = 3 shape: four
+    consecutive fused rounds bit-equal to one wavefront per agent (z, kkt, iterations, status, exchanged
+    trajectories), and each round's solution within 1e-6 of the C restatement on a 64-agent sample."""
+    import torch
+
+    from cmpc import _lib as L
+    from cmpc import scenarios as S
+    from cmpc.rounds import DIRounds
+    from oracle import cmpc_oracle as CO
+
+    sc = S.make_di(n, N, 2, 2)
+    R1 = DIRounds(sc, ctx=gpu_ctx)
+    R2 = DIRounds(sc, ctx=gpu_ctx)
+    R1.opts = L.opts(flags=L.CMPC_FLAG_ONE_WAVE)
+    R2.opts = L.opts(flags=L.CMPC_FLAG_TWO_WAVES)
+    smp = np.sort(np.random.default_rng(2).choice(n, 64, replace=False))
+    for rnd in range(4):
+        R2.build()
+        P = {k: (v[smp] if isinstance(v, np.ndarray) and v.ndim and v.shape[0] == n else v)
+             for k, v in R2.snapshot().items()}
+        R1.step()
+        R2.step()
+        torch.cuda.synchronize()
+        for a in ("z", "kkt", "iters", "status", "traj_all"):
+            assert torch.equal(getattr(R1, a), getattr(R2, a)), (rnd, a)
+        zc, _, _, sc_ = CO.solve_batch(P, nthreads=8)
+        st = R2.status.cpu().numpy()[smp]
+        ok = (st == 1) & (sc_ == 1)
+        assert ok.mean() >= 0.95, (rnd, st, sc_)
+        assert np.abs(R2.z.cpu().numpy()[smp][ok] - zc[ok]).max() < Z_TOL, rnd
+
+
 def test_deterministic_and_permutation_invariant(gpu_ctx):
     import cmpc
     from cmpc import scenarios as S

@@ -26,6 +26,11 @@ NAMES = {14: "setup", 0: "residual: Q X, C'lam", 1: "residual: 2 adjoints", 2: "
 UNFUSED = "--unfused" in sys.argv
 if UNFUSED:
     sys.argv.remove("--unfused")
+WAVES = 0  # --one-wave / --two-waves: CMPC_FLAG_ONE_WAVE / CMPC_FLAG_TWO_WAVES (default: the library's choice)
+for a_, f_ in (("--one-wave", L.CMPC_FLAG_ONE_WAVE), ("--two-waves", L.CMPC_FLAG_TWO_WAVES)):
+    if a_ in sys.argv:
+        sys.argv.remove(a_)
+        WAVES = f_
 LPV = len(sys.argv) > 1 and sys.argv[1] == "--lpv"
 if LPV:
     import bench
@@ -52,7 +57,7 @@ else:
     if not UNFUSED:
         R.solve = R.build_solve
 st = torch.zeros((n, SLOTS), dtype=torch.int64, device="cuda")
-R.opts = L.opts(stamps=st.data_ptr())
+R.opts = L.opts(stamps=st.data_ptr(), flags=WAVES)
 for _ in range(3):
     R.solve()
 torch.cuda.synchronize()
@@ -71,7 +76,7 @@ print(f"agents {n} N {N}: kernel {ev[0].elapsed_time(ev[1]):.3f} ms (with stamps
 for i in sorted(NAMES, key=lambda i: (i != 14, i)):
     print(f"  {NAMES[i]:24s} {a[:, i].mean() / it.mean():10.0f} clk/iter   {100 * a[:, i].sum() / tot.sum():5.1f} %")
 print(f"  total                    {tot.mean() / it.mean():10.0f} clk/iter ; slowest agent {tot.max():.0f} clk")
-R.opts = L.opts()
+R.opts = L.opts(flags=WAVES)
 ev[0].record()
 R.solve()
 ev[1].record()
