@@ -269,9 +269,15 @@ def cfg5_line(ctx, steps=5, warmup=2):
         peak = FP32_PEAK_TFLOPS if fp32 else FP64_PEAK_TFLOPS
         kind = "cfg5fp32" if fp32 else "cfg5"
         traffic, src = pmc_traffic(kind)
+        stn, kkn = st.cpu().numpy(), kk.cpu().numpy()
+        k2 = np.sort(kkn[stn == 2])[::-1]  # the rounding-floor solves' KKT residuals (scaled), largest first
         line = {"value": R.B * steps / el, "unit": "agent-QP/s", "ms_per_step": el / steps * 1e3,
                 "mean_ipm_iters": mean_it, "max_kkt": float(kk.max()),
-                "status_counts": {int(a): int(b) for a, b in zip(*np.unique(st.cpu().numpy(), return_counts=True))},
+                "max_kkt_status1": float(kkn[stn == 1].max()) if (stn == 1).any() else None,
+                "status2_kkt": {"count": int(len(k2)), "max": float(k2[0]) if len(k2) else None,
+                                "values": [float(v) for v in k2[:40]],
+                                "over_1e-6": int((k2 > 1e-6).sum())},
+                "status_counts": {int(a): int(b) for a, b in zip(*np.unique(stn, return_counts=True))},
                 "roofline": {"kernel": f"mpc_riccati_kernel<Cfg<2,6,3,6,GR{',F32' if fp32 else ''}>>",
                              "bound": "latency", "achieved": ach, "peak": peak, "unit": "TFLOP/s", "frac": ach / peak,
                              "traffic": traffic, "traffic_source": src, "kernel_ms_per_launch": kern,

@@ -109,6 +109,11 @@ constexpr double kT0Floor = 0.5;
 // 500, max 45 -> 38, mean 14.5 -> 13.6.  The stage-wise kernels keep 0.5: on cfg5 (N = 50, Riccati) the
 // total iterations, which set that launch, rose 2 % with 0.1.
 constexpr double kT0FloorCond = 0.1;
+// Mehrotra's centring parameter sigma = (mu_aff / mu)^e: e = 3 in the stage-wise kernels, e = 2 in the condensed
+// ones since round 5 (tools/ipm_lab.py, 100 cfg3 rounds: sum of the per-round slowest agent's iterations 1621 ->
+// 1580; tools/lpv_lab.py, 22 reference-model rounds: 500 -> 490 and 23 % fewer rounding-floor exits, 718 -> 554;
+// on cfg5's Riccati solves e = 2 cost 1.5 % more iterations, so those keep 3; a warm Riccati continuation of a
+// condensed solve, CMPC_FLAG_RESCUE, keeps the e = 2 of the solve it continues).
 // Stall guard: after an iteration whose step was below kShortStep, the corrector's centring
 // parameter is at least kSigmaMin.  On the BASELINE cfg5 population (N=50, nx=6 nu=3) about 1
 // agent in 10^4 otherwise stalls at steps ~1e-3, blocked by a terminal collision row, and runs

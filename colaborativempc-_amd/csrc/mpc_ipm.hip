@@ -599,7 +599,7 @@ __global__ __launch_bounds__(kWave) void mpc_ipm_kernel(const MpcConst c, const 
                     if (isfinite(w[r])) mua_l += (t[r] + a * dta[r]) * (lam[r] + a * dla[r]);
                 const double mu_aff = wave_sum(mua_l) / mact;
                 const double ratio = mu > 0.0 ? mu_aff / mu : 0.0;
-                sig_c = ratio * ratio * ratio;
+                sig_c = ratio * ratio;  // (the condensed kernels: e = 2, internal.h)
                 if (alpha_prev < kShortStep) sig_c = fmax(sig_c, kSigmaMin);
             } else {
                 alpha = fmin(1.0, 0.995 * amax);

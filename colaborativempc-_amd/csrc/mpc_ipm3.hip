@@ -1756,7 +1756,7 @@ __global__ __launch_bounds__(W2 ? 128 : 64, 1) void mpc_ipm3_kernel(const MpcCon
                 }
                 const double mu_aff = wave_sum(mua_l) / mact;
                 const double ratio = mu > 0.0 ? mu_aff / mu : 0.0;
-                sig_c = ratio * ratio * ratio;
+                sig_c = ratio * ratio;  // (the condensed kernels: e = 2, internal.h)
                 if (alpha_prev < kShortStep) sig_c = fmax(sig_c, kSigmaMin);
                 STAMP(12);
             } else {

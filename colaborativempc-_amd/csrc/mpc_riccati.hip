@@ -2083,7 +2083,8 @@ __global__ __launch_bounds__(kWave) void mpc_riccati_kernel(const MpcConst c_arg
                     if (isfinite(w[r])) mua_l += (t[r] + a * dta[r]) * (lam[r] + a * dla[r]);
                 const double mu_aff = wave_sum(mua_l) / mact;
                 const double ratio = mu > 0.0 ? mu_aff / mu : 0.0;
-                sig_c = ratio * ratio * ratio;
+                // e = 3; a warm continuation of a condensed solve keeps that method's e = 2 (internal.h)
+                sig_c = warm ? ratio * ratio : ratio * ratio * ratio;
                 if (alpha_prev < kShortStep) sig_c = fmax(sig_c, kSigmaMin);
             } else {
                 alpha = fmin(1.0, 0.995 * amax);

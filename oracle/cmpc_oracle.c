@@ -2144,7 +2144,9 @@ static int solve_one(const shared_t* S, const agent_t* a, double tol, int max_it
 #ifdef SIGMA_EXP
                 sig_c = mu > 0 ? pow(mu_aff / mu, SIGMA_EXP) : 0.0;
 #else
-                sig_c = mu > 0 ? pow(mu_aff / mu, 3.0) : 0.0;
+                /* e = 3 for the stage-wise methods, 2 for the condensed one and its warm Riccati continuation
+                   (internal.h) */
+                sig_c = mu > 0 ? pow(mu_aff / mu, (S->newton && !warm_rescue) ? 3.0 : 2.0) : 0.0;
 #endif
                 if (alpha_prev < SHORT_STEP) sig_c = fmax(sig_c, SIGMA_MIN); /* kShortStep / kSigmaMin */
             } else {

@@ -16,7 +16,7 @@ import sys
 import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-sys.path[:0] = [ROOT, os.path.join(ROOT, "tools")]
+sys.path[:0] = [ROOT, os.path.join(ROOT, "tools"), os.path.join(ROOT, "colaborativempc-_amd")]
 
 ROUND, KEEP_FLOOR, KEEP_PLAIN = 4, 6, 2
 
@@ -42,7 +42,10 @@ def main():
         up = z[:, base: base + 2 * N].reshape(-1, N, 2)
         x0, x_last, u_last, u_old = xp[:, 1].copy(), xp[:, 1:].copy(), up.copy(), up[:, 0].copy()
         traj = xp[:, :, 7:9].copy()
-    zp, kp, ip, sp = CO.solve_batch_rescue(P, nthreads=8, polish=True)
+    from cmpc.solver import plan  # the polish kernel's active-set capacity for this shape (host only)
+
+    amax = plan(P, 1, rescue=True, polish=True)["polish_max_active"]
+    zp, kp, ip, sp = CO.solve_batch_rescue(P, nthreads=8, polish=True, polish_amax=amax)
     floor = np.flatnonzero((st == 2) & (sp == 1))[:KEEP_FLOOR]
     plain = np.flatnonzero((st == 1) & (sp == 1))[:KEEP_PLAIN]
     sel = np.concatenate([floor, plain])
