@@ -53,7 +53,8 @@ __host__ __device__ inline PolLayout pol_layout_for(const MpcConst& c, int amax)
     L.cst = take(mpc_const_used_doubles(c));
     const int mc = c.mc, nu = c.nu;
     L.Lh = take(n * (n + 1) / 2);                       // packed lower triangle
-    const int sY = N * nx * nx;                         // also S_k while H is built
+    // also S_k while H is built, and the one-wave Cholesky's scratch (wave_chol64: 4 x 272 + 3 x 272)
+    const int sY = N * nx * nx > 7 * 272 ? N * nx * nx : 7 * 272;
     L.Y = take(amax * (n | 1) > sY ? amax * (n | 1) : sY);  // rows at an odd stride (LDS banks)
     const int sS = amax * (amax + 1) / 2;
     L.S = take(sS > 2 * nx * n ? sS : 2 * nx * n);      // also Gamma's ping-pong while H is built
@@ -118,12 +119,130 @@ __device__ double block_sum(double v, double* red) {
     return (red[4] + red[5]) + (red[6] + red[7]);
 }
 
+// In-place Cholesky of a packed lower n x n matrix, n <= 64, by wave 0 alone in the MFMA accumulator layout
+// (the v3 kernel's factorisation, mpc_ipm3.hip): 16 x 16 tiles, padding rows the identity; each 16 x 16
+// diagonal factor by DPP row broadcasts and rsq + Newton steps, the panel substitution in the accumulator
+// layout, the trailing update on V_MFMA_F64_16X16X4_F64.  L overwrites M; rd receives 1 / L_ii.  Scratch: 7 x 272
+// doubles of LDS.  Returns false when a pivot is not positive.  (Was the workgroup's four-column blocked
+// factorisation, block_chol_packed, two barriers per block: 0.14 M clocks at n = 60.)
+__device__ __attribute__((noinline)) bool wave_chol64(double* M, double* rd, int n, double* scratch) {
+    constexpr int T = 4;
+    const int l = threadIdx.x & 63;
+    double* Ld = scratch;            // T x 16 x 17: the factored diagonal blocks
+    double* SP = scratch + T * 272;  // (T - 1) x 16 x 17: the panel, for the transposed MFMA operands
+    auto pk = [](int i, int j) { return i * (i + 1) / 2 + j; };
+    v4d acc[T * (T + 1) / 2];
+#pragma unroll
+    for (int I = 0; I < T; ++I)
+#pragma unroll
+        for (int J = 0; J <= I; ++J)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int row = 16 * I + (l >> 4) + 4 * r, col = 16 * J + (l & 15);
+                const int a = row > col ? row : col, b2 = row > col ? col : row;
+                const double v = M[pk(a < n ? a : 0, b2 < n ? b2 : 0)];
+                acc[I * (I + 1) / 2 + J][r] = (row < n && col < n) ? v : (row == col ? 1.0 : 0.0);
+            }
+    bool ok = true;
+#pragma unroll
+    for (int J = 0; J < T; ++J) {
+        const int JJ = J * (J + 1) / 2 + J;
+        double* S0 = Ld + J * 272;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) S0[((l >> 4) + 4 * r) * 17 + (l & 15)] = acc[JJ][r];
+        wsync();
+        double rw[16];
+#pragma unroll
+        for (int cc = 0; cc < 16; ++cc) rw[cc] = S0[(l & 15) * 17 + cc];
+        {
+            double dn = 0.0;
+            static_for<0, 16>([&](auto jc) __attribute__((always_inline)) {
+                constexpr int j = decltype(jc)::value;
+                const double djj = bcast16<j>(j == 0 ? rw[0] : dn);
+                if (!(djj > 0.0)) ok = false;
+                const double y = rsqrt_d(djj);
+                const double lj = rw[j] * y;
+                rw[j] = lj;
+                if constexpr (j + 1 < 16) dn = fma(-lj, lj, rw[j + 1]);
+                static_for<j + 1, 16>([&](auto cc) __attribute__((always_inline)) {
+                    constexpr int c2 = decltype(cc)::value;
+                    rw[c2] = fma(-lj, bcast16<c2>(lj), rw[c2]);
+                });
+            });
+        }
+        if (l < 16) {
+#pragma unroll
+            for (int cc = 0; cc < 16; ++cc) S0[l * 17 + cc] = (cc <= l) ? rw[cc] : 0.0;
+        }
+        wsync();
+        if (J + 1 < T) {
+            // panel: L_IJ = K_IJ L_JJ^-T (lane l: column l & 15 of every panel tile; unscaled form)
+            const int i16 = l & 15;
+            const double inv_own = 1.0 / S0[i16 * 17 + i16];
+            static_for<0, 16>([&](auto jc) __attribute__((always_inline)) {
+                constexpr int cc = decltype(jc)::value;
+                const double dcc = bcast16<cc>(inv_own);
+                const double lcc = (i16 > cc) ? rw[cc] * dcc : 0.0;
+#pragma unroll
+                for (int I = J + 1; I < T; ++I)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        const double v = acc[I * (I + 1) / 2 + J][r];
+                        acc[I * (I + 1) / 2 + J][r] = fma(-bcast16<cc>(v), lcc, v);
+                    }
+            });
+#pragma unroll
+            for (int I = J + 1; I < T; ++I)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) acc[I * (I + 1) / 2 + J][r] *= inv_own;
+#pragma unroll
+            for (int I = J + 1; I < T; ++I)
+#pragma unroll
+                for (int r = 0; r < 4; ++r)
+                    SP[((I - J - 1) * 16 + (l >> 4) + 4 * r) * 17 + (l & 15)] = acc[I * (I + 1) / 2 + J][r];
+            wsync();
+            // trailing update K_IK -= L_IJ L_KJ' (I >= K > J)
+#pragma unroll
+            for (int q = 0; q < 16; q += 4) {
+                double fr[T];
+#pragma unroll
+                for (int I = J + 1; I < T; ++I) fr[I] = SP[((I - J - 1) * 16 + (l & 15)) * 17 + q + (l >> 4)];
+#pragma unroll
+                for (int I = J + 1; I < T; ++I)
+#pragma unroll
+                    for (int K2 = J + 1; K2 <= I; ++K2)
+                        acc[I * (I + 1) / 2 + K2] =
+                            __builtin_amdgcn_mfma_f64_16x16x4f64(-fr[I], fr[K2], acc[I * (I + 1) / 2 + K2], 0, 0, 0);
+            }
+            wsync();
+        }
+    }
+    // L back into the packed storage: the off-diagonal tiles from the accumulators, the diagonal blocks from Ld
+#pragma unroll
+    for (int I = 1; I < T; ++I)
+#pragma unroll
+        for (int J = 0; J < I; ++J)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int row = 16 * I + (l >> 4) + 4 * r, col = 16 * J + (l & 15);
+                if (row < n) M[pk(row, col)] = acc[I * (I + 1) / 2 + J][r];
+            }
+    for (int e = l; e < T * 256; e += kWave) {
+        const int J = e >> 8, i = (e >> 4) & 15, j = e & 15, row = 16 * J + i, col = 16 * J + j;
+        if (row < n && col <= row) M[pk(row, col)] = Ld[J * 272 + i * 17 + j];
+    }
+    wsync();
+    for (int i = l; i < n; i += kWave) rd[i] = 1.0 / M[pk(i, i)];
+    return ok;
+}
+
 // in-place Cholesky of an n x n matrix by the whole workgroup (packed lower storage, rows contiguous),
 // blocked by four columns: wave 0 factors the four-column panel (compiler fences only), then the
 // workgroup applies its rank-4 update to the trailing triangle as (row, 8-column chunk) items — two
 // barriers per block instead of three per column.  Returns false when a pivot is not positive.
 // (Tried: unblocked with three barriers per column, 1.6x slower; one wave with fences; the column
 // in registers with readlane broadcasts, 2.4x slower still.)
+// (Now only S beyond 64 active rows, or without room for wave_chol64's scratch.)
 __device__ bool block_chol_packed(double* M, int n, int* flag) {
     const int tid = threadIdx.x;
     auto idx = [](int i, int j) { return i * (i + 1) / 2 + j; };
@@ -533,11 +652,9 @@ __global__ __launch_bounds__(kPT) void mpc_polish_kernel(const MpcConst c_arg, c
     auto ih = [](int i, int j) { return i * (i + 1) / 2 + j; };
     auto is = [](int i, int j) { return i * (i + 1) / 2 + j; };
     int& flag_s = *reinterpret_cast<int*>(sm + L.red + 14);
-    {
-        const bool ok = block_chol_packed(Lh, n, &flag_s);
+    if (tid < kWave) {  // one wave, in the accumulators (n <= 64: every polished condensed shape)
+        const bool ok = wave_chol64(Lh, sm + L.rdH, n, Y);
         if (tid == 0) flag_s = ok ? 1 : 0;
-        if (ok)
-            for (int i = tid; i < n; i += kPT) sm[L.rdH + i] = 1.0 / Lh[ih(i, i)];
     }
     __syncthreads();
     const bool h_ok = flag_s != 0;
@@ -663,7 +780,12 @@ __global__ __launch_bounds__(kPT) void mpc_polish_kernel(const MpcConst c_arg, c
             }
         }
         __syncthreads();
-        {
+        if (nA <= 64 && (amax - nA) * ldY >= 7 * 272) {  // (Y is live: the scratch is its rows past nA)
+            if (tid < kWave) {
+                const bool ok = wave_chol64(Sm, sm + L.rdS, nA, Y + (size_t)nA * ldY);
+                if (tid == 0) flag_s = ok ? 1 : 0;
+            }
+        } else {
             const bool ok = block_chol_packed(Sm, nA, &flag_s);
             if (tid == 0) flag_s = ok ? 1 : 0;
             if (ok)
