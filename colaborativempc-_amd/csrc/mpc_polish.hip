@@ -33,9 +33,10 @@ constexpr int kPT = 256;           // threads per workgroup (four waves)
 constexpr int kPolishMaxActive = 96;
 constexpr int kPolishSteps = 3;    // Newton steps on the (linear) KKT system: one solve, refinements while above tol
 constexpr int kPolishPasses = 2;
+constexpr int kLdG = 72;           // row stride of the H build's Gamma / 2Q Gamma images (2-way LDS banks)
 
 struct PolLayout {
-    int cst, Lh, Y, S, G0, G1, sA, sB, sC, sp, U, sig, Uc, sc, Ub, sb, X, ybar, w, lamp, tp, rp, rd, gU, rsig, zv,
+    int cst, Lh, Y, S, sA, sB, sC, sp, U, sig, Uc, sc, Ub, sb, X, ybar, w, lamp, tp, rp, rd, gU, rsig, zv,
         gz, rdH, rdS, lA, rA, dl, red, in, Ar;
     int amax, total;
 };
@@ -53,13 +54,12 @@ __host__ __device__ inline PolLayout pol_layout_for(const MpcConst& c, int amax)
     L.cst = take(mpc_const_used_doubles(c));
     const int mc = c.mc, nu = c.nu;
     L.Lh = take(n * (n + 1) / 2);                       // packed lower triangle
-    // also S_k while H is built, and the one-wave Cholesky's scratch (wave_chol64: 4 x 272 + 3 x 272)
-    const int sY = N * nx * nx > 7 * 272 ? N * nx * nx : 7 * 272;
-    L.Y = take(amax * (n | 1) > sY ? amax * (n | 1) : sY);  // rows at an odd stride (LDS banks)
-    const int sS = amax * (amax + 1) / 2;
-    L.S = take(sS > 2 * nx * n ? sS : 2 * nx * n);      // also Gamma's ping-pong while H is built
-    L.G0 = L.S;
-    L.G1 = L.S + nx * n;
+    L.Y = take(amax * (n | 1));  // rows at an odd stride (LDS banks)
+    // S; also Gamma and 2Q Gamma while H is built (4 x KR x kLdG), and the one-wave Cholesky's scratch while
+    // H is factored (wave_chol64: 4 x 272 + 3 x 272)
+    const int sG = 4 * ((nx + 3) & ~3) * kLdG, sS = amax * (amax + 1) / 2;
+    const int sS2 = sG > 7 * 272 ? sG : 7 * 272;
+    L.S = take(sS > sS2 ? sS : sS2);
     L.sA = take(N * nx * nx);                           // the agent's stage data, staged once
     L.sB = take(N * nx * nu);
     L.sC = take(N * mc * nx);
@@ -103,6 +103,13 @@ __host__ __device__ inline PolLayout pol_layout(const MpcConst& c) {
     return L;
 }
 
+// the (I, J) of lower 16 x 16 tile t in row-major order (I >= J)
+__device__ __forceinline__ void tile_ij(int t, int& I, int& J) {
+    I = 0;
+    while ((I + 1) * (I + 2) / 2 <= t) ++I;
+    J = t - I * (I + 1) / 2;
+}
+
 // NaN-propagating block reductions over the four waves (scratch: 4 doubles)
 __device__ double block_nmax(double v, double* red) {
     v = wave_max(v);
@@ -125,11 +132,16 @@ __device__ double block_sum(double v, double* red) {
 // layout, the trailing update on V_MFMA_F64_16X16X4_F64.  L overwrites M; rd receives 1 / L_ii.  Scratch: 7 x 272
 // doubles of LDS.  Returns false when a pivot is not positive.  (Was the workgroup's four-column blocked
 // factorisation, block_chol_packed, two barriers per block: 0.14 M clocks at n = 60.)
-__device__ __attribute__((noinline)) bool wave_chol64(double* M, double* rd, int n, double* scratch) {
+// (Out of line, so its registers stay out of the kernel's other sections; the operands are cast to the LDS
+// address space, or the call's generic pointers would make every access a flat one.)
+typedef __attribute__((address_space(3))) double lds_f64;
+__device__ __attribute__((noinline)) bool wave_chol64(double* M_, double* rd_, int n, double* scratch) {
     constexpr int T = 4;
     const int l = threadIdx.x & 63;
-    double* Ld = scratch;            // T x 16 x 17: the factored diagonal blocks
-    double* SP = scratch + T * 272;  // (T - 1) x 16 x 17: the panel, for the transposed MFMA operands
+    lds_f64* M = (lds_f64*)M_;
+    lds_f64* rd = (lds_f64*)rd_;
+    lds_f64* Ld = (lds_f64*)scratch;  // T x 16 x 17: the factored diagonal blocks
+    lds_f64* SP = Ld + T * 272;       // (T - 1) x 16 x 17: the panel, for the transposed MFMA operands
     auto pk = [](int i, int j) { return i * (i + 1) / 2 + j; };
     v4d acc[T * (T + 1) / 2];
 #pragma unroll
@@ -147,7 +159,7 @@ __device__ __attribute__((noinline)) bool wave_chol64(double* M, double* rd, int
 #pragma unroll
     for (int J = 0; J < T; ++J) {
         const int JJ = J * (J + 1) / 2 + J;
-        double* S0 = Ld + J * 272;
+        lds_f64* S0 = Ld + J * 272;
 #pragma unroll
         for (int r = 0; r < 4; ++r) S0[((l >> 4) + 4 * r) * 17 + (l & 15)] = acc[JJ][r];
         wsync();
@@ -296,34 +308,63 @@ __device__ bool block_chol_packed(double* M, int n, int* flag) {
     return true;
 }
 
-// forward substitution L x = b in place (x overwrites b), wave 0 only, n <= 128: lane l keeps rows
-// l and l + 64 in registers; the solved entry is broadcast by readlane (no LDS round trip in the
-// chain); rd = the reciprocal diagonal
+// forward substitution L x = b in place, wave 0 only: lane l holds x_l and x_{l+64}; the solved entry is
+// broadcast by readlane (no LDS round trip in the chain); rd = the reciprocal diagonal.  The factor's
+// entries and rd of eight pivots are loaded ahead of their eight chain steps (one LDS latency per group
+// instead of one per pivot; the same operations in the same order).
 template <class Idx>
 __device__ void wave_fsub(const double* M, const double* rd, int n, Idx idx, double* x) {
-    const int l = threadIdx.x;
+    const int l = threadIdx.x & (kWave - 1);
     double x0 = l < n ? x[l] : 0.0, x1 = l + kWave < n ? x[l + kWave] : 0.0;
-    for (int p = 0; p < n; ++p) {
-        const double xp = (p < kWave ? readlane_d(x0, p) : readlane_d(x1, p - kWave)) * rd[p];
-        if (l == p) x0 = xp;
-        if (l + kWave == p) x1 = xp;
-        if (l > p && l < n) x0 -= M[idx(l, p)] * xp;
-        if (l + kWave > p && l + kWave < n) x1 -= M[idx(l + kWave, p)] * xp;
+    for (int p0 = 0; p0 < n; p0 += 8) {
+        double m0[8], m1[8], rp[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const int p = p0 + u;
+            rp[u] = rd[p < n ? p : 0];
+            m0[u] = (l > p && l < n) ? M[idx(l, p)] : 0.0;
+            m1[u] = (l + kWave > p && l + kWave < n) ? M[idx(l + kWave, p)] : 0.0;
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const int p = p0 + u;
+            if (p < n) {
+                const double xp = (p < kWave ? readlane_d(x0, p) : readlane_d(x1, p - kWave)) * rp[u];
+                if (l == p) x0 = xp;
+                if (l + kWave == p) x1 = xp;
+                if (l > p && l < n) x0 -= m0[u] * xp;
+                if (l + kWave > p && l + kWave < n) x1 -= m1[u] * xp;
+            }
+        }
     }
     if (l < n) x[l] = x0;
     if (l + kWave < n) x[l + kWave] = x1;
 }
-// backward substitution L' x = b in place, wave 0 only (as above)
+// backward substitution L' x = b in place, wave 0 only (as above; row p of the factor is contiguous)
 template <class Idx>
 __device__ void wave_bsub(const double* M, const double* rd, int n, Idx idx, double* x) {
-    const int l = threadIdx.x;
+    const int l = threadIdx.x & (kWave - 1);
     double x0 = l < n ? x[l] : 0.0, x1 = l + kWave < n ? x[l + kWave] : 0.0;
-    for (int p = n - 1; p >= 0; --p) {
-        const double xp = (p < kWave ? readlane_d(x0, p) : readlane_d(x1, p - kWave)) * rd[p];
-        if (l == p) x0 = xp;
-        if (l + kWave == p) x1 = xp;
-        if (l < p) x0 -= M[idx(p, l)] * xp;
-        if (l + kWave < p) x1 -= M[idx(p, l + kWave)] * xp;
+    for (int p0 = n - 1; p0 >= 0; p0 -= 8) {
+        double m0[8], m1[8], rp[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const int p = p0 - u;
+            rp[u] = rd[p >= 0 ? p : 0];
+            m0[u] = (l < p) ? M[idx(p, l)] : 0.0;
+            m1[u] = (l + kWave < p) ? M[idx(p, l + kWave)] : 0.0;
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const int p = p0 - u;
+            if (p >= 0) {
+                const double xp = (p < kWave ? readlane_d(x0, p) : readlane_d(x1, p - kWave)) * rp[u];
+                if (l == p) x0 = xp;
+                if (l + kWave == p) x1 = xp;
+                if (l < p) x0 -= m0[u] * xp;
+                if (l + kWave < p) x1 -= m1[u] * xp;
+            }
+        }
     }
     if (l < n) x[l] = x0;
     if (l + kWave < n) x[l + kWave] = x1;
@@ -331,7 +372,7 @@ __device__ void wave_bsub(const double* M, const double* rd, int n, Idx idx, dou
 
 struct PolCtx {
     const MpcConst& c;
-    int nx;  // the state dimension (a compile-time constant in the NX instantiations)
+    int nx, nu;  // the state and input dimensions (compile-time constants in the NX / NU instantiations)
     const PolLayout& L;
     double* sm;
     const double* A;
@@ -342,48 +383,176 @@ struct PolCtx {
     const double* C;
 };
 
+// n <= 64 forms of the two substitutions (H's factor, every condensed shape): x in one register, no branch
+// on the pivot's register; the same operations in the same order as wave_fsub / wave_bsub.
+template <class Idx>
+__device__ void wave_fsub64(const double* M, const double* rd, int n, Idx idx, double* x) {
+    const int l = threadIdx.x & (kWave - 1);
+    double x0 = l < n ? x[l] : 0.0;
+    for (int p0 = 0; p0 < n; p0 += 8) {
+        double m0[8], rp[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const int p = p0 + u;
+            rp[u] = rd[p < n ? p : 0];
+            m0[u] = (l > p && l < n) ? M[idx(l, p)] : 0.0;
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const int p = p0 + u;
+            if (p < n) {
+                const double xp = readlane_d(x0, p) * rp[u];
+                if (l == p) x0 = xp;
+                if (l > p && l < n) x0 -= m0[u] * xp;
+            }
+        }
+    }
+    if (l < n) x[l] = x0;
+}
+template <class Idx>
+__device__ void wave_bsub64(const double* M, const double* rd, int n, Idx idx, double* x) {
+    const int l = threadIdx.x & (kWave - 1);
+    double x0 = l < n ? x[l] : 0.0;
+    for (int p0 = n - 1; p0 >= 0; p0 -= 8) {
+        double m0[8], rp[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const int p = p0 - u;
+            rp[u] = rd[p >= 0 ? p : 0];
+            m0[u] = (l < p) ? M[idx(p, l)] : 0.0;
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const int p = p0 - u;
+            if (p >= 0) {
+                const double xp = readlane_d(x0, p) * rp[u];
+                if (l == p) x0 = xp;
+                if (l < p) x0 -= m0[u] * xp;
+            }
+        }
+    }
+    if (l < n) x[l] = x0;
+}
+
+// The stage recursions below run on wave 0 with the state (or costate) in lanes 0..nx-1 of a register and
+// its entries broadcast by readlane: no LDS round trip or fence in the chain, and a stage's A / B entries
+// are loaded before it (one FMA chain per stage).  Same sums in the same order as the LDS forms they
+// replace (0.5-1.1 k clocks per stage: a load latency inside every chain).
+
 // X = simulation of (x0, U) (wave 0; the other waves wait at the caller's barrier)
 __device__ __forceinline__ void pol_fwd(const PolCtx& q, const double* U, double* X) {
     const MpcConst& c = q.c;
-    const int nx = q.nx, nu = c.nu, N = c.N, l = threadIdx.x;
+    const int nx = q.nx, nu = q.nu, N = c.N, l = threadIdx.x;
     if (l >= kWave) return;
-    if (l < nx) X[l] = q.x0[l];
-    wsync();
+    const int lr = l < nx ? l : 0;
+    double x = q.x0[lr];
+    if (l < nx) X[l] = x;
     for (int k = 0; k < N; ++k) {
-        if (l < nx) {
-            const double* Ak = q.A + ((size_t)k * nx + l) * nx;
-            const double* Bk = q.B + ((size_t)k * nx + l) * nu;
-            double v = 0.0;
-            for (int t = 0; t < nx; ++t) v += Ak[t] * X[k * nx + t];
-            for (int i = 0; i < nu; ++i) v += Bk[i] * U[k * nu + i];
-            X[(k + 1) * nx + l] = v;
+        const double* Ak = q.A + ((size_t)k * nx + lr) * nx;
+        const double* Bk = q.B + ((size_t)k * nx + lr) * nu;
+        double a[CMPC_MAX_NX], bu[CMPC_MAX_NU], u[CMPC_MAX_NU];
+#pragma unroll
+        for (int t = 0; t < CMPC_MAX_NX; ++t) a[t] = t < nx ? Ak[t] : 0.0;
+#pragma unroll
+        for (int i = 0; i < CMPC_MAX_NU; ++i) {
+            bu[i] = i < nu ? Bk[i] : 0.0;
+            u[i] = i < nu ? U[k * nu + i] : 0.0;
         }
-        wsync();
+        double v = 0.0;
+#pragma unroll
+        for (int t = 0; t < CMPC_MAX_NX; ++t)
+            if (t < nx) v += a[t] * readlane_d(x, t);
+#pragma unroll
+        for (int i = 0; i < CMPC_MAX_NU; ++i)
+            if (i < nu) v += bu[i] * u[i];
+        x = v;
+        if (l < nx) X[(k + 1) * nx + l] = v;
     }
+    wsync();
 }
 
 // out_k = B_k' psi_{k+1}, psi_N = y_N, psi_k = y_k + A_k' psi_{k+1} (wave 0; psi kept in y's slots,
 // y is overwritten)
 __device__ __forceinline__ void pol_adjoint(const PolCtx& q, double* y, double* out) {
     const MpcConst& c = q.c;
-    const int nx = q.nx, nu = c.nu, N = c.N, l = threadIdx.x;
+    const int nx = q.nx, nu = q.nu, N = c.N, l = threadIdx.x;
     if (l >= kWave) return;
+    const int lr = l < nx ? l : 0, lb = l < nu ? l : 0;
+    double psi = y[N * nx + lr];
     for (int k = N - 1; k >= 0; --k) {
-        const double* psi = y + (k + 1) * nx;
-        if (l < nu) {
-            const double* Bk = q.B + (size_t)k * nx * nu;
-            double v = 0.0;
-            for (int s = 0; s < nx; ++s) v += Bk[s * nu + l] * psi[s];
-            out[k * nu + l] = v;
+        const double* Ak = q.A + (size_t)k * nx * nx;
+        const double* Bk = q.B + (size_t)k * nx * nu;
+        double a[CMPC_MAX_NX], bc[CMPC_MAX_NX], ps[CMPC_MAX_NX];
+#pragma unroll
+        for (int s2 = 0; s2 < CMPC_MAX_NX; ++s2) {
+            a[s2] = s2 < nx ? Ak[s2 * nx + lr] : 0.0;
+            bc[s2] = s2 < nx ? Bk[s2 * nu + lb] : 0.0;
         }
-        if (k > 0 && l < nx) {
-            const double* Ak = q.A + (size_t)k * nx * nx;
-            double v = y[k * nx + l];
-            for (int s = 0; s < nx; ++s) v += Ak[s * nx + l] * psi[s];
-            y[k * nx + l] = v;
+        const double yk = y[k * nx + lr];
+#pragma unroll
+        for (int s2 = 0; s2 < CMPC_MAX_NX; ++s2) ps[s2] = s2 < nx ? readlane_d(psi, s2) : 0.0;
+        double vo = 0.0;
+#pragma unroll
+        for (int s2 = 0; s2 < CMPC_MAX_NX; ++s2)
+            if (s2 < nx) vo += bc[s2] * ps[s2];
+        if (l < nu) out[k * nu + l] = vo;
+        if (k > 0) {
+            double v = yk;
+#pragma unroll
+            for (int s2 = 0; s2 < CMPC_MAX_NX; ++s2)
+                if (s2 < nx) v += a[s2] * ps[s2];
+            psi = v;
+            if (l < nx) y[k * nx + l] = v;
         }
-        wsync();
     }
+    wsync();
+}
+
+// both residual adjoints of pol_residuals in one sweep: chain 0 (lanes 0..31) as pol_adjoint on y (out0 = gU),
+// chain 1 (lanes 32..63) on y2 = y + C' lam on stages 1..N, formed as it goes (out1 = rd).  Same sums in the
+// same order as two pol_adjoint sweeps, y2 built as in pol_residuals.
+__device__ __forceinline__ void pol_adjoint2(const PolCtx& q, double* y, double* out0, double* out1, const double* lam) {
+    const MpcConst& c = q.c;
+    const int nx = q.nx, nu = q.nu, N = c.N, mc = c.mc, l = threadIdx.x;
+    if (l >= kWave) return;
+    const int ch = l >> 5, j = l & 31;
+    const int lr = j < nx ? j : 0, lb = j < nu ? j : 0;
+    auto y2 = [&](int k) {  // this lane's entry of y (chain 0) or y2 (chain 1) at stage k >= 1
+        double v = y[k * nx + lr];
+        if (ch)
+            for (int r = 0; r < mc; ++r) v += lam[(k - 1) * mc + r] * q.C[((size_t)(k - 1) * mc + r) * nx + lr];
+        return v;
+    };
+    double psi = y2(N);
+    for (int k = N - 1; k >= 0; --k) {
+        const double* Ak = q.A + (size_t)k * nx * nx;
+        const double* Bk = q.B + (size_t)k * nx * nu;
+        double a[CMPC_MAX_NX], bc[CMPC_MAX_NX], ps[CMPC_MAX_NX];
+#pragma unroll
+        for (int s2 = 0; s2 < CMPC_MAX_NX; ++s2) {
+            a[s2] = s2 < nx ? Ak[s2 * nx + lr] : 0.0;
+            bc[s2] = s2 < nx ? Bk[s2 * nu + lb] : 0.0;
+        }
+        const double yk = k > 0 ? y2(k) : 0.0;
+#pragma unroll
+        for (int s2 = 0; s2 < CMPC_MAX_NX; ++s2) {
+            const double p0 = s2 < nx ? readlane_d(psi, s2) : 0.0, p1 = s2 < nx ? readlane_d(psi, 32 + s2) : 0.0;
+            ps[s2] = ch ? p1 : p0;
+        }
+        double vo = 0.0;
+#pragma unroll
+        for (int s2 = 0; s2 < CMPC_MAX_NX; ++s2)
+            if (s2 < nx) vo += bc[s2] * ps[s2];
+        if (j < nu) (ch ? out1 : out0)[k * nu + j] = vo;
+        if (k > 0) {
+            double v = yk;
+#pragma unroll
+            for (int s2 = 0; s2 < CMPC_MAX_NX; ++s2)
+                if (s2 < nx) v += a[s2] * ps[s2];
+            psi = v;
+        }
+    }
+    wsync();
 }
 
 __device__ __forceinline__ double pol_row(const PolCtx& q, const double* X, const double* U, const double* sg, int r) {
@@ -403,18 +572,21 @@ __device__ __forceinline__ double pol_row(const PolCtx& q, const double* X, cons
 }
 
 // The interior-point residuals at (U, sigma, t, lambda) into rd / rsig / rp (cmpc_oracle.c merit_at);
-// X is re-simulated.  With `full`, returns the merit max(res, 1e4 mu) and *kkt = max(res, mu).
+// X is re-simulated when `sim` (otherwise X already holds U's states).  With `full`, returns the merit
+// max(res, 1e4 mu) and *kkt = max(res, mu).
 __device__ __forceinline__ double pol_residuals(const PolCtx& q, const double* U, const double* sg, const double* t,
-                                const double* lam, const int* act_w, bool full, double* kkt) {
+                                const double* lam, const int* act_w, bool full, bool sim, double* kkt) {
     const MpcConst& c = q.c;
     const PolLayout& L = q.L;
     double* sm = q.sm;
-    const int nx = q.nx, nu = c.nu, N = c.N, ns = c.ns, mc = c.mc, ms = c.ms, m = c.m, n = c.n;
+    const int nx = q.nx, nu = q.nu, N = c.N, ns = c.ns, mc = c.mc, ms = c.ms, m = c.m, n = c.n;
     const int tid = threadIdx.x;
     double *X = sm + L.X, *ybar = sm + L.ybar, *rd = sm + L.rd, *gU = sm + L.gU, *rsig = sm + L.rsig,
            *rp = sm + L.rp, *red = sm + L.red;
-    pol_fwd(q, U, X);
-    __syncthreads();
+    if (sim) {
+        pol_fwd(q, U, X);
+        __syncthreads();
+    }
     auto ucost = [&](int k, int i) {
         double v = 0.0;
         for (int j = 0; j < nu; ++j) {
@@ -433,13 +605,13 @@ __device__ __forceinline__ double pol_residuals(const PolCtx& q, const double* U
             ybar[e] = v;
         }
         __syncthreads();
-        pol_adjoint(q, ybar, gU);
+        pol_adjoint2(q, ybar, gU, rd, lam);
         __syncthreads();
         double g_l = 0.0;
         for (int e = tid; e < n; e += kPT) g_l = nmax(g_l, fabs(gU[e] + ucost(e / nu, e % nu)));
         gscale = nmax(1.0, block_nmax(g_l, red));
     }
-    for (int e = tid; e < (N + 1) * nx; e += kPT) {
+    for (int e = tid; e < (N + 1) * nx && !full; e += kPT) {
         const int k = e / nx, s = e - k * nx;
         double v = 2.0 * q.pl[e];
         for (int t2 = 0; t2 < nx; ++t2) v += 2.0 * c.Q[s * nx + t2] * X[k * nx + t2];
@@ -447,9 +619,11 @@ __device__ __forceinline__ double pol_residuals(const PolCtx& q, const double* U
             for (int r = 0; r < mc; ++r) v += lam[(k - 1) * mc + r] * q.C[((size_t)(k - 1) * mc + r) * nx + s];
         ybar[e] = v;
     }
-    __syncthreads();
-    pol_adjoint(q, ybar, rd);
-    __syncthreads();
+    if (!full) {
+        __syncthreads();
+        pol_adjoint(q, ybar, rd);
+        __syncthreads();
+    }
     for (int e = tid; e < n; e += kPT) {
         const int k = e / nu, i = e - k * nu, r = ms + 2 * e;
         rd[e] += ucost(k, i) + lam[r] - lam[r + 1];
@@ -493,8 +667,8 @@ __device__ __forceinline__ double pol_residuals(const PolCtx& q, const double* U
     return nmax(res, 1e4 * mu);
 }
 
-// NXT: the state dimension as a compile-time constant (0: the runtime c.nx)
-template <int NXT>
+// NXT, NUT: the state and input dimensions as compile-time constants (0: the runtime c.nx, c.nu)
+template <int NXT, int NUT>
 __global__ __launch_bounds__(kPT) void mpc_polish_kernel(const MpcConst c_arg, const MpcPtrs P) {
     extern __shared__ __attribute__((aligned(16))) double sm[];
     const int b = blockIdx.x;
@@ -512,7 +686,7 @@ __global__ __launch_bounds__(kPT) void mpc_polish_kernel(const MpcConst c_arg, c
     }
     __syncthreads();
     const MpcConst& c = *reinterpret_cast<const MpcConst*>(sm + L.cst);
-    const int nx = NXT ? NXT : c.nx, nu = c.nu, N = c.N, ns = c.ns, mc = c.mc, ms = c.ms, m = c.m, n = c.n;
+    const int nx = NXT ? NXT : c.nx, nu = NUT ? NUT : c.nu, N = c.N, ns = c.ns, mc = c.mc, ms = c.ms, m = c.m, n = c.n;
     const int amax = L.amax, ldY = n | 1;
     // the stage data (A, B, C rows, linear cost) staged in LDS once: every recursion below reads it
     {
@@ -525,7 +699,7 @@ __global__ __launch_bounds__(kPT) void mpc_polish_kernel(const MpcConst c_arg, c
         for (int i = tid; i < N * mc * nx; i += kPT) sm[L.sC + i] = gC[i];
         for (int i = tid; i < (N + 1) * nx; i += kPT) sm[L.sp + i] = gp[i];
     }
-    const PolCtx q{c, nx, L, sm, sm + L.sA, sm + L.sB, P.x0 + (size_t)b * nx, P.up + (size_t)b * nu, sm + L.sp, sm + L.sC};
+    const PolCtx q{c, nx, nu, L, sm, sm + L.sA, sm + L.sB, P.x0 + (size_t)b * nx, P.up + (size_t)b * nu, sm + L.sp, sm + L.sC};
     const double* hC = P.h + (size_t)b * N * mc;
     const double best_m = flag == 2.0 ? hd[1] : c_arg.tol;  // (flag 1: slot 1 holds the iterations done)
     const int ht = (int)hand_t(c);
@@ -552,10 +726,40 @@ __global__ __launch_bounds__(kPT) void mpc_polish_kernel(const MpcConst c_arg, c
     for (int i = tid; i < n; i += kPT) U[i] = hd[2 + i];
     for (int i = tid; i < N * ns; i += kPT) sig[i] = hd[2 + n + i];
     for (int i = tid; i < n * (n + 1) / 2; i += kPT) Lh[i] = 0.0;
-    for (int i = tid; i < nx * n; i += kPT) sm[L.G0 + i] = 0.0;
+    int& nA_s = *reinterpret_cast<int*>(sm + L.red + 12);
+    __syncthreads();
+    // the active list (ascending rows), wave 0 by ballot; nA_s = |A| (rows past amax are not listed)
+    auto active_list = [&]() {
+        if (tid < kWave) {
+            int base = 0;
+            for (int r0 = 0; r0 < m; r0 += kWave) {
+                const int r = r0 + tid;
+                const bool f = r < m && (in[r] & 2);
+                const unsigned long long msk = __ballot(f);
+                const int pos = base + __popcll(msk & ((1ull << tid) - 1ull));
+                if (f && pos < amax) Ar[pos] = r;
+                base += __popcll(msk);
+            }
+            if (tid == 0) nA_s = base;
+        }
+        __syncthreads();
+    };
+    // pass 0's rows of G_A are formed in the H build below (c_r' Gamma_{k+1} at stage k, as
+    // cmpc_oracle.c polish_one); the bound rows +-e_i here
+    active_list();
+    const int nA0 = nA_s;
+    if (nA0 <= amax) {
+        for (int e = tid; e < nA0 * ldY; e += kPT) {
+            const int qa = e / ldY, i = e - qa * ldY, r = Ar[qa];
+            double v = 0.0;
+            if (r >= ms && i == ((r - ms) >> 1)) v = ((r - ms) & 1) ? -1.0 : 1.0;
+            Y[e] = v;
+        }
+    }
     __syncthreads();
     // diagnostic section clocks (MpcPtrs::stamps slots 9..15, thread 0): init, H build, H factor,
-    // active rows (Y), S build + factor, Newton steps + evaluation, output
+    // G_A rows, Y, S build + factor + the Newton steps' linear algebra, the residual sweeps (simulation,
+    // adjoints, reductions) of the Newton steps and evaluations; slot 8: Newton steps run
     unsigned long long tsum[7] = {0, 0, 0, 0, 0, 0, 0}, t_a = P.stamps ? clock64_() : 0;
 #define PSTAMP(slot)                         \
     if (P.stamps && tid == 0) {              \
@@ -564,75 +768,121 @@ __global__ __launch_bounds__(kPT) void mpc_polish_kernel(const MpcConst c_arg, c
         t_a = t_b;                           \
     }
     PSTAMP(0);
-    // ---- H = sum_k Gamma_{k+1}' 2Q Gamma_{k+1} + the 2R / 2dR band (lower triangle), H = L L' ----
-    // by the backward recursion S_N = 2Q, S_k = 2Q + A_k' S_{k+1} A_k (S_{i+1} = the cost-to-go
-    // weight of the state after input stage i): for i >= j the block
-    //     H_ij = B_i' S_{i+1} A_i A_{i-1} ... A_{j+1} B_j,
-    // one thread per row of H carrying r = B_i[:, a]' S_{i+1} Phi back over the stages
+    // ---- H = sum_k Gamma_{k+1}' (2Q Gamma_{k+1}) + the 2R / 2dR band (lower triangle), H = L L' ----
+    // (cmpc_oracle.c polish_one's build.)  Gamma_{k+1} = A_k Gamma_k + B_k E_k (nx x n, zero beyond column
+    // (k + 1) nu) and W = 2Q Gamma_{k+1} are formed stage by stage in LDS ping-pong buffers (thread: column
+    // l, rows wave + 4 i); the 16 x 16 lower tiles of H accumulate Gamma' W on V_MFMA_F64_16X16X4_F64 over
+    // the nx rows (padded to 4), a wave holding up to three tiles in its accumulators through the horizon;
+    // tiles whose Gamma columns are still zero are skipped.  (Was wave 0 alone: the backward recursion
+    // S_k = 2Q + A_k' S_{k+1} A_k, then one lane per row of H carrying B_i' S_{i+1} A_i ... back over the
+    // stages: 0.165 M clocks.)
     {
-        double* Sk = Y;                  // S_1 .. S_N (N nx^2)
-        double* T = sm + L.G0;           // S_{k+1} A_k
-        if (tid < kWave) {               // wave 0 alone: compiler fences instead of barriers
-            const int l = tid;
-            for (int e = l; e < nx * nx; e += kWave) Sk[(N - 1) * nx * nx + e] = 2.0 * c.Q[e];
-            wsync();
-            for (int k = N - 1; k >= 1; --k) {
+        const int KR = (nx + 3) & ~3;
+        double* Gb = Sm;                      // Gamma_k, Gamma_{k+1}: 2 x KR x kLdG
+        double* Wb = Sm + 2 * KR * kLdG;      // 2Q Gamma: 2 x KR x kLdG
+        for (int i = tid; i < 4 * KR * kLdG; i += kPT) Sm[i] = 0.0;
+        int qptr = 0;  // the first active row of pass 0 not yet formed (Ar ascending: stage by stage)
+        const int T = (n + 15) >> 4, NT = T * (T + 1) / 2;
+        const int wv = tid >> 6, l = tid & 63;
+        int tI[3], tJ[3];
+#pragma unroll
+        for (int sl = 0; sl < 3; ++sl) tile_ij(wv + 4 * sl < NT ? wv + 4 * sl : 0, tI[sl], tJ[sl]);
+        v4d acc[3];
+#pragma unroll
+        for (int sl = 0; sl < 3; ++sl) acc[sl] = v4d{0.0, 0.0, 0.0, 0.0};
+        // a diagonal Q (the reference's agent, the double integrators): the MFMA's B fragment is 2 Q_ss Gamma,
+        // formed as it is loaded (the same rounding as the W sum, whose other terms are zeros) — no W phase
+        bool qd_l = true;
+        for (int i = l; i < nx * nx; i += kWave)
+            if (i / nx != i % nx && c.Q[i] != 0.0) qd_l = false;
+        const bool qd = __ballot(!qd_l) == 0ull;  // (wave-uniform; every wave reads the same Q)
+        double qv[3];
+#pragma unroll
+        for (int ks = 0; ks < 3; ++ks) {
+            const int s2 = 4 * ks + (l >> 4);
+            qv[ks] = s2 < nx ? 2.0 * c.Q[s2 * nx + s2] : 0.0;
+        }
+        __syncthreads();
+        for (int k = 0; k < N; ++k) {
+            const double* Gc = Gb + (k & 1) * KR * kLdG;
+            double* Gn = Gb + ((k + 1) & 1) * KR * kLdG;
+            double* Wn = Wb + ((k + 1) & 1) * KR * kLdG;
+            const int ncol = (k + 1) * nu, j = l;
+            if (j < ncol) {
                 const double* Ak = q.A + k * nx * nx;
-                const double* Sn = Sk + k * nx * nx;
-                for (int e = l; e < nx * nx; e += kWave) {
-                    const int r = e / nx, cc = e - r * nx;
-                    double v = 0.0;
-                    for (int u = 0; u < nx; ++u) v += Sn[r * nx + u] * Ak[u * nx + cc];
-                    T[e] = v;
-                }
-                wsync();
-                for (int e = l; e < nx * nx; e += kWave) {
-                    const int r = e / nx, cc = e - r * nx;
-                    double v = 2.0 * c.Q[e];
-                    for (int u = 0; u < nx; ++u) v += Ak[u * nx + r] * T[u * nx + cc];
-                    Sk[(k - 1) * nx * nx + e] = v;
-                }
-                wsync();
-            }
-            // lane `row` (n <= 64) carries r = B_i[:, a]' S_{i+1} A_i ... back over the stages, every lane
-            // at the same stage (broadcast reads of A_j, B_j)
-            const int row = l, i2 = row / nu, a = row - i2 * nu;
-            double v[CMPC_MAX_NX], w2[CMPC_MAX_NX];
-            double* Hrow = Lh + row * (row + 1) / 2;
-            for (int j2 = N - 1; j2 >= 0; --j2) {
-                const double* Bj = q.B + j2 * nx * nu;
-                if (row < n && i2 == j2) {  // r = B_i[:, a]' S_{i+1}
-                    const double* S1 = Sk + i2 * nx * nx;
+                const double* Bk = q.B + k * nx * nu;
+                double gc[CMPC_MAX_NX];
 #pragma unroll
-                    for (int cc = 0; cc < CMPC_MAX_NX; ++cc) {
-                        double h = 0.0;
-                        if (cc < nx)
-                            for (int u = 0; u < nx; ++u) h += Bj[u * nu + a] * S1[u * nx + cc];
-                        v[cc] = h;
-                    }
-                }
-                if (row < n && i2 >= j2) {
-                    for (int b2 = 0; b2 < nu; ++b2) {
-                        const int col = j2 * nu + b2;
-                        double h = 0.0;
+                for (int t2 = 0; t2 < CMPC_MAX_NX; ++t2) gc[t2] = t2 < nx ? Gc[t2 * kLdG + j] : 0.0;
 #pragma unroll
-                        for (int u = 0; u < CMPC_MAX_NX; ++u)
-                            if (u < nx) h += v[u] * Bj[u * nu + b2];
-                        if (col <= row) Hrow[col] = h;
-                    }
-                    if (j2 > 0) {  // r <- r A_j
-                        const double* Aj = q.A + j2 * nx * nx;
+                for (int i = 0; i < 3; ++i) {  // rows wv, wv + 4, wv + 8: three independent chains
+                    const int s2 = wv + 4 * i;
+                    if (s2 < nx) {
+                        double v = 0.0;
+                        if (j >= k * nu) {
+                            v = Bk[s2 * nu + (j - k * nu)];
+                        } else {
 #pragma unroll
-                        for (int t2 = 0; t2 < CMPC_MAX_NX; ++t2) {
-                            double h = 0.0;
-#pragma unroll
-                            for (int u = 0; u < CMPC_MAX_NX; ++u)
-                                if (u < nx && t2 < nx) h += v[u] * Aj[u * nx + t2];
-                            w2[t2] = h;
+                            for (int t2 = 0; t2 < CMPC_MAX_NX; ++t2)
+                                if (t2 < nx) v += Ak[s2 * nx + t2] * gc[t2];
                         }
-#pragma unroll
-                        for (int u = 0; u < CMPC_MAX_NX; ++u) v[u] = w2[u];
+                        Gn[s2 * kLdG + j] = v;
                     }
+                }
+            }
+            __syncthreads();
+            if (nA0 <= amax) {  // pass 0's active rows of stage k: g = c_r' Gamma_{k+1}
+                int q1 = qptr;
+                while (q1 < nA0 && Ar[q1] < ms && Ar[q1] / mc == k) ++q1;
+                for (int qa = qptr + wv; qa < q1; qa += kPT / kWave) {
+                    if (j < ncol) {
+                        const double* cr = q.C + (size_t)Ar[qa] * nx;
+                        double v = 0.0;
+#pragma unroll
+                        for (int t2 = 0; t2 < CMPC_MAX_NX; ++t2)
+                            if (t2 < nx) v += cr[t2] * Gn[t2 * kLdG + j];
+                        Y[(size_t)qa * ldY + j] = v;
+                    }
+                }
+                qptr = q1;
+            }
+            if (!qd) {
+                if (j < ncol) {
+                    double gn[CMPC_MAX_NX];
+#pragma unroll
+                    for (int t2 = 0; t2 < CMPC_MAX_NX; ++t2) gn[t2] = t2 < nx ? Gn[t2 * kLdG + j] : 0.0;
+                    for (int s2 = wv; s2 < nx; s2 += 4) {
+                        double v = 0.0;
+#pragma unroll
+                        for (int t2 = 0; t2 < CMPC_MAX_NX; ++t2)
+                            if (t2 < nx) v += 2.0 * c.Q[s2 * nx + t2] * gn[t2];
+                        Wn[s2 * kLdG + j] = v;
+                    }
+                }
+                __syncthreads();
+            }
+#pragma unroll
+            for (int sl = 0; sl < 3; ++sl) {
+                if (wv + 4 * sl < NT && 16 * tI[sl] < ncol) {
+#pragma unroll
+                    for (int ks = 0; ks < 3; ++ks) {
+                        if (4 * ks < KR) {
+                            const int row = (4 * ks + (l >> 4)) * kLdG;
+                            const double gi = Gn[row + 16 * tI[sl] + (l & 15)], gj = Gn[row + 16 * tJ[sl] + (l & 15)];
+                            const double wj = qd ? qv[ks] * gj : Wn[row + 16 * tJ[sl] + (l & 15)];
+                            acc[sl] = __builtin_amdgcn_mfma_f64_16x16x4f64(gi, wj, acc[sl], 0, 0, 0);
+                        }
+                    }
+                }
+            }
+        }
+#pragma unroll
+        for (int sl = 0; sl < 3; ++sl) {
+            if (wv + 4 * sl < NT) {
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int row = 16 * tI[sl] + (l >> 4) + 4 * r, col = 16 * tJ[sl] + (l & 15);
+                    if (row < n && col <= row) Lh[row * (row + 1) / 2 + col] = acc[sl][r];
                 }
             }
         }
@@ -653,7 +903,7 @@ __global__ __launch_bounds__(kPT) void mpc_polish_kernel(const MpcConst c_arg, c
     auto is = [](int i, int j) { return i * (i + 1) / 2 + j; };
     int& flag_s = *reinterpret_cast<int*>(sm + L.red + 14);
     if (tid < kWave) {  // one wave, in the accumulators (n <= 64: every polished condensed shape)
-        const bool ok = wave_chol64(Lh, sm + L.rdH, n, Y);
+        const bool ok = wave_chol64(Lh, sm + L.rdH, n, Sm);
         if (tid == 0) flag_s = ok ? 1 : 0;
     }
     __syncthreads();
@@ -661,30 +911,17 @@ __global__ __launch_bounds__(kPT) void mpc_polish_kernel(const MpcConst c_arg, c
     PSTAMP(2);
     __syncthreads();
     double best = INFINITY, best_kkt = INFINITY;
-    int& nA_s = *reinterpret_cast<int*>(sm + L.red + 12);
-    int passes = 0;
-    if (tid == 0) nA_s = -1;
-    __syncthreads();
+    int passes = 0, nsteps = 0;
+#ifdef CMPC_POL_LAB
+    unsigned long long lab_fwd = 0;
+#endif
     for (int pass = 0; pass < kPolishPasses && h_ok; ++pass) {
         passes = pass + 1;
-        // the active list (ascending rows), wave 0 by ballot
-        if (tid < kWave) {
-            int base = 0;
-            for (int r0 = 0; r0 < m; r0 += kWave) {
-                const int r = r0 + tid;
-                const bool f = r < m && (in[r] & 2);
-                const unsigned long long msk = __ballot(f);
-                const int pos = base + __popcll(msk & ((1ull << tid) - 1ull));
-                if (f && pos < amax) Ar[pos] = r;
-                base += __popcll(msk);
-            }
-            if (tid == 0) nA_s = base;
-        }
-        __syncthreads();
+        if (pass) active_list();
         const int nA = nA_s;
         if (nA > amax) break;
-        // G_A rows by adjoint recursions (one thread a row), then Y rows = L^-1 g (in place)
-        for (int qa = tid; qa < nA; qa += kPT) {
+        // later passes: G_A rows by adjoint recursions (one thread a row)
+        for (int qa = pass ? tid : nA; qa < nA; qa += kPT) {
             const int r = Ar[qa];
             double* g = Y + (size_t)qa * ldY;
             for (int i = 0; i < n; ++i) g[i] = 0.0;
@@ -713,22 +950,14 @@ __global__ __launch_bounds__(kPT) void mpc_polish_kernel(const MpcConst c_arg, c
                 const int qq = r - ms;
                 g[qq >> 1] = (qq & 1) ? -1.0 : 1.0;
             }
-            for (int i = 0; i < n; ++i) {  // four partial sums: the loads of a group go out together
-                const double* Li = Lh + i * (i + 1) / 2;
-                double v0 = g[i], v1 = 0.0, v2 = 0.0, v3 = 0.0;
-                int p2 = 0;
-                for (; p2 + 4 <= i; p2 += 4) {
-                    v0 -= Li[p2] * g[p2];
-                    v1 -= Li[p2 + 1] * g[p2 + 1];
-                    v2 -= Li[p2 + 2] * g[p2 + 2];
-                    v3 -= Li[p2 + 3] * g[p2 + 3];
-                }
-                for (; p2 < i; ++p2) v0 -= Li[p2] * g[p2];
-                g[i] = ((v0 + v1) + (v2 + v3)) / Li[i];
-            }
         }
         __syncthreads();
         PSTAMP(3);
+        // Y rows = L^-1 g: wave w substitutes rows w, w + 4, ... (lane i: entry i; the solved entry broadcast
+        // by readlane).  (Was one thread per row, an n-step dot-product loop: 0.17 M clocks at |A| ~ 20.)
+        for (int qa = tid >> 6; qa < nA; qa += kPT / kWave) wave_fsub64(Lh, sm + L.rdH, n, ih, Y + (size_t)qa * ldY);
+        __syncthreads();
+        PSTAMP(4);
         // S = Y Y' + E (packed lower): the active rows' Gram matrix on V_MFMA_F64_16X16X4_F64.  16 x 16
         // tiles (I, J), I >= J, over nA padded to 16, dealt round-robin to the four waves, two tiles in
         // flight per wave (independent accumulator chains); k-steps of 4 over the n columns.  Both
@@ -738,11 +967,6 @@ __global__ __launch_bounds__(kPT) void mpc_polish_kernel(const MpcConst c_arg, c
         {
             const int TA = (nA + 15) >> 4, NTt = TA * (TA + 1) / 2, KS = (n + 3) >> 2;
             const int wv = tid >> 6, l = tid & 63, i16 = l & 15, kq = l >> 4;
-            auto tile_ij = [](int t, int& I, int& J) {
-                I = 0;
-                while ((I + 1) * (I + 2) / 2 <= t) ++I;
-                J = t - I * (I + 1) / 2;
-            };
             auto frag = [&](int blk, int s) {
                 const int row = 16 * blk + i16, col = 4 * s + kq;
                 const double v = Y[(size_t)(row < nA ? row : 0) * ldY + (col < n ? col : 0)];
@@ -792,7 +1016,7 @@ __global__ __launch_bounds__(kPT) void mpc_polish_kernel(const MpcConst c_arg, c
                 for (int i = tid; i < nA; i += kPT) sm[L.rdS + i] = 1.0 / Sm[is(i, i)];
         }
         __syncthreads();
-        PSTAMP(4);
+        PSTAMP(5);
         if (!flag_s) break;
         // Newton steps from (U, sigma, lambda_A)
         for (int i = tid; i < n; i += kPT) Uc[i] = U[i];
@@ -809,7 +1033,10 @@ __global__ __launch_bounds__(kPT) void mpc_polish_kernel(const MpcConst c_arg, c
             for (int qa = tid; qa < nA; qa += kPT) lamp[Ar[qa]] = lA[qa];
             __syncthreads();
             double kk0;
-            pol_residuals(q, Uc, sc, tp, lamp, in, false, &kk0);  // t = 0: rp = row - w on A
+            // t = 0: rp = row - w on A (X: Uc's states after the first step, left by the evaluation below)
+            PSTAMP(5);
+            pol_residuals(q, Uc, sc, tp, lamp, in, false, step == 0, &kk0);
+            PSTAMP(6);
             for (int qa = tid; qa < nA; qa += kPT) {
                 const int r = Ar[qa];
                 double ra = rp[r];
@@ -821,7 +1048,7 @@ __global__ __launch_bounds__(kPT) void mpc_polish_kernel(const MpcConst c_arg, c
             }
             for (int i = tid; i < n; i += kPT) zv[i] = rd[i];
             __syncthreads();
-            if (tid < kWave) wave_fsub(Lh, sm + L.rdH, n, ih, zv);  // z = L^-1 rU
+            if (tid < kWave) wave_fsub64(Lh, sm + L.rdH, n, ih, zv);  // z = L^-1 rU
             __syncthreads();
             for (int qa = tid; qa < nA; qa += kPT) {
                 double v = rA[qa];
@@ -830,8 +1057,13 @@ __global__ __launch_bounds__(kPT) void mpc_polish_kernel(const MpcConst c_arg, c
             }
             __syncthreads();
             if (tid < kWave) {
-                wave_fsub(Sm, sm + L.rdS, nA, is, dl);
-                wave_bsub(Sm, sm + L.rdS, nA, is, dl);
+                if (nA <= 64) {
+                    wave_fsub64(Sm, sm + L.rdS, nA, is, dl);
+                    wave_bsub64(Sm, sm + L.rdS, nA, is, dl);
+                } else {
+                    wave_fsub(Sm, sm + L.rdS, nA, is, dl);
+                    wave_bsub(Sm, sm + L.rdS, nA, is, dl);
+                }
             }
             __syncthreads();
             for (int i = tid; i < n; i += kPT) {  // z + Y dlam
@@ -840,7 +1072,7 @@ __global__ __launch_bounds__(kPT) void mpc_polish_kernel(const MpcConst c_arg, c
                 gz[i] = v;
             }
             __syncthreads();
-            if (tid < kWave) wave_bsub(Lh, sm + L.rdH, n, ih, gz);  // H^-1 (rU + G_A' dlam)
+            if (tid < kWave) wave_bsub64(Lh, sm + L.rdH, n, ih, gz);  // H^-1 (rU + G_A' dlam)
             __syncthreads();
             for (int i = tid; i < n; i += kPT) Uc[i] -= gz[i];
             for (int e = tid; e < N * ns; e += kPT) {
@@ -857,8 +1089,16 @@ __global__ __launch_bounds__(kPT) void mpc_polish_kernel(const MpcConst c_arg, c
             // the polished point as an interior-point iterate: t = 0 and lambda = max(lambda_A, 0) on A,
             // t = max(w - row, 0) and lambda = 0 elsewhere; one Newton step normally reaches tol, a
             // refinement step follows only when it does not
+            PSTAMP(5);
+#ifdef CMPC_POL_LAB  // lab: the clocks of one simulation sweep in slot 8
+            const unsigned long long t_f0 = clock64_();
+#endif
             pol_fwd(q, Uc, sm + L.X);
             __syncthreads();
+#ifdef CMPC_POL_LAB
+            lab_fwd = clock64_() - t_f0;
+#endif
+            PSTAMP(6);
             for (int r = tid; r < m; r += kPT) {
                 lamp[r] = 0.0;
                 tp[r] = ((in[r] & 1) && !(in[r] & 2)) ? fmax(w[r] - pol_row(q, sm + L.X, Uc, sc, r), 0.0) : 1.0;
@@ -869,7 +1109,10 @@ __global__ __launch_bounds__(kPT) void mpc_polish_kernel(const MpcConst c_arg, c
                 tp[Ar[qa]] = 0.0;
             }
             __syncthreads();
-            mp = pol_residuals(q, Uc, sc, tp, lamp, in, true, &kk);
+            PSTAMP(5);
+            mp = pol_residuals(q, Uc, sc, tp, lamp, in, true, false, &kk);  // (X: pol_fwd above)
+            PSTAMP(6);
+            ++nsteps;
             if (mp < c.tol) break;
         }
         PSTAMP(5);
@@ -905,7 +1148,12 @@ __global__ __launch_bounds__(kPT) void mpc_polish_kernel(const MpcConst c_arg, c
         st[3] = (unsigned long long)__double_as_longlong(best_m);
         st[4] = h_ok ? 1ull : 0ull;
         for (int i = 0; i < 3; ++i) st[5 + i] = (unsigned long long)__double_as_longlong(sm[L.red + 8 + i]);
-        for (int i = 0; i < 6; ++i) st[9 + i] = tsum[i];
+#ifdef CMPC_POL_LAB
+        st[8] = lab_fwd;
+#else
+        st[8] = (unsigned long long)nsteps;
+#endif
+        for (int i = 0; i < 7; ++i) st[9 + i] = tsum[i];
     }
     // kept only when it beats the method's best AND lands at the rounding floor at least (stop_status's
     // 1e3 tol): below tol it is solved (1), below the floor solved-inaccurate (2).  A polish of a solve
@@ -947,12 +1195,12 @@ __global__ __launch_bounds__(kPT) void mpc_polish_kernel(const MpcConst c_arg, c
 size_t mpc_polish_lds_bytes(const MpcConst& c) { return sizeof(double) * (size_t)pol_layout(c).total; }
 int mpc_polish_max_active(const MpcConst& c) { return pol_layout(c).amax; }
 
-template <int NXT>
+template <int NXT, int NUT>
 static hipError_t polish_launch_t(const MpcConst& c, const MpcPtrs& p, int batch, hipStream_t s, size_t lds) {
-    hipError_t e = hipFuncSetAttribute((const void*)mpc_polish_kernel<NXT>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                       (int)lds);
+    hipError_t e = hipFuncSetAttribute((const void*)mpc_polish_kernel<NXT, NUT>,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(mpc_polish_kernel<NXT>, dim3(batch), dim3(kPT), lds, s, c, p);
+    hipLaunchKernelGGL((mpc_polish_kernel<NXT, NUT>), dim3(batch), dim3(kPT), lds, s, c, p);
     return hipGetLastError();
 }
 
@@ -961,10 +1209,10 @@ hipError_t mpc_polish_launch(const MpcConst& c, const MpcPtrs& p, int batch, hip
     const size_t lds = mpc_polish_lds_bytes(c);
     if (lds > kMaxLdsBytes) return hipErrorInvalidValue;
     switch (c.nx) {  // the reference's agent (9), the BASELINE double-integrator families (4, 6)
-        case 9: return polish_launch_t<9>(c, p, batch, s, lds);
-        case 4: return polish_launch_t<4>(c, p, batch, s, lds);
-        case 6: return polish_launch_t<6>(c, p, batch, s, lds);
-        default: return polish_launch_t<0>(c, p, batch, s, lds);
+        case 9: return c.nu == 2 ? polish_launch_t<9, 2>(c, p, batch, s, lds) : polish_launch_t<9, 0>(c, p, batch, s, lds);
+        case 4: return c.nu == 2 ? polish_launch_t<4, 2>(c, p, batch, s, lds) : polish_launch_t<4, 0>(c, p, batch, s, lds);
+        case 6: return c.nu == 3 ? polish_launch_t<6, 3>(c, p, batch, s, lds) : polish_launch_t<6, 0>(c, p, batch, s, lds);
+        default: return polish_launch_t<0, 0>(c, p, batch, s, lds);
     }
 }
 
