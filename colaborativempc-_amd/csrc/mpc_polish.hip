@@ -58,7 +58,7 @@ __host__ __device__ inline PolLayout pol_layout_for(const MpcConst& c, int amax)
     // S; also Gamma and 2Q Gamma while H is built (4 x KR x kLdG), and the one-wave Cholesky's scratch while
     // H is factored (wave_chol64: 4 x 272 + 3 x 272)
     const int sG = 4 * ((nx + 3) & ~3) * kLdG, sS = amax * (amax + 1) / 2;
-    const int sS2 = sG > 7 * 272 ? sG : 7 * 272;
+    const int sS2 = sG > 8 * 272 ? sG : 8 * 272;  // (8 x 272: also the blocked Y solve's D_J and tiles)
     L.S = take(sS > sS2 ? sS : sS2);
     L.sA = take(N * nx * nx);                           // the agent's stage data, staged once
     L.sB = take(N * nx * nu);
@@ -135,8 +135,8 @@ __device__ double block_sum(double v, double* red) {
 // (Out of line, so its registers stay out of the kernel's other sections; the operands are cast to the LDS
 // address space, or the call's generic pointers would make every access a flat one.)
 typedef __attribute__((address_space(3))) double lds_f64;
+template <int T>  // 16 x 16 tiles per side: n <= 16 T
 __device__ __attribute__((noinline)) bool wave_chol64(double* M_, double* rd_, int n, double* scratch) {
-    constexpr int T = 4;
     const int l = threadIdx.x & 63;
     lds_f64* M = (lds_f64*)M_;
     lds_f64* rd = (lds_f64*)rd_;
@@ -768,6 +768,9 @@ __global__ __launch_bounds__(kPT) void mpc_polish_kernel(const MpcConst c_arg, c
         t_a = t_b;                           \
     }
     PSTAMP(0);
+#ifdef CMPC_POL_LAB  // lab: the clocks of a chosen region in slot 8 (CMPC_POL_LAB_REGION)
+    unsigned long long lab_fwd = 0, lab_t0 = 0;
+#endif
     // ---- H = sum_k Gamma_{k+1}' (2Q Gamma_{k+1}) + the 2R / 2dR band (lower triangle), H = L L' ----
     // (cmpc_oracle.c polish_one's build.)  Gamma_{k+1} = A_k Gamma_k + B_k E_k (nx x n, zero beyond column
     // (k + 1) nu) and W = 2Q Gamma_{k+1} are formed stage by stage in LDS ping-pong buffers (thread: column
@@ -783,7 +786,7 @@ __global__ __launch_bounds__(kPT) void mpc_polish_kernel(const MpcConst c_arg, c
         for (int i = tid; i < 4 * KR * kLdG; i += kPT) Sm[i] = 0.0;
         int qptr = 0;  // the first active row of pass 0 not yet formed (Ar ascending: stage by stage)
         const int T = (n + 15) >> 4, NT = T * (T + 1) / 2;
-        const int wv = tid >> 6, l = tid & 63;
+        const int wv = __builtin_amdgcn_readfirstlane(tid >> 6), l = tid & 63;  // (wave-uniform)
         int tI[3], tJ[3];
 #pragma unroll
         for (int sl = 0; sl < 3; ++sl) tile_ij(wv + 4 * sl < NT ? wv + 4 * sl : 0, tI[sl], tJ[sl]);
@@ -804,6 +807,9 @@ __global__ __launch_bounds__(kPT) void mpc_polish_kernel(const MpcConst c_arg, c
         }
         __syncthreads();
         for (int k = 0; k < N; ++k) {
+#if defined(CMPC_POL_LAB) && CMPC_POL_LAB == 1
+            lab_t0 = clock64_();
+#endif
             const double* Gc = Gb + (k & 1) * KR * kLdG;
             double* Gn = Gb + ((k + 1) & 1) * KR * kLdG;
             double* Wn = Wb + ((k + 1) & 1) * KR * kLdG;
@@ -831,9 +837,15 @@ __global__ __launch_bounds__(kPT) void mpc_polish_kernel(const MpcConst c_arg, c
                 }
             }
             __syncthreads();
+#if defined(CMPC_POL_LAB) && CMPC_POL_LAB == 1
+            lab_fwd += clock64_() - lab_t0;
+#endif
             if (nA0 <= amax) {  // pass 0's active rows of stage k: g = c_r' Gamma_{k+1}
-                int q1 = qptr;
-                while (q1 < nA0 && Ar[q1] < ms && Ar[q1] / mc == k) ++q1;
+                // (this stage's rows follow qptr in Ar: counted by ballot over the next 64, every wave alike;
+                // a stage holds at most mc <= 64 rows)
+                const int qn = qptr + l;
+                const bool at_k = qn < nA0 && Ar[qn] < ms && Ar[qn] / mc == k;
+                const int q1 = qptr + __popcll(__ballot(at_k));
                 for (int qa = qptr + wv; qa < q1; qa += kPT / kWave) {
                     if (j < ncol) {
                         const double* cr = q.C + (size_t)Ar[qa] * nx;
@@ -861,20 +873,31 @@ __global__ __launch_bounds__(kPT) void mpc_polish_kernel(const MpcConst c_arg, c
                 }
                 __syncthreads();
             }
+            // every fragment loaded first, then the three tiles' MFMA chains interleaved
+            double fa[3][3], fb[3][3];
+            const double* Bsrc = qd ? Gn : Wn;
 #pragma unroll
-            for (int sl = 0; sl < 3; ++sl) {
-                if (wv + 4 * sl < NT && 16 * tI[sl] < ncol) {
+            for (int sl = 0; sl < 3; ++sl)
 #pragma unroll
-                    for (int ks = 0; ks < 3; ++ks) {
-                        if (4 * ks < KR) {
-                            const int row = (4 * ks + (l >> 4)) * kLdG;
-                            const double gi = Gn[row + 16 * tI[sl] + (l & 15)], gj = Gn[row + 16 * tJ[sl] + (l & 15)];
-                            const double wj = qd ? qv[ks] * gj : Wn[row + 16 * tJ[sl] + (l & 15)];
-                            acc[sl] = __builtin_amdgcn_mfma_f64_16x16x4f64(gi, wj, acc[sl], 0, 0, 0);
-                        }
-                    }
+                for (int ks = 0; ks < 3; ++ks) {
+                    const int row = (4 * ks + (l >> 4)) * kLdG;
+                    const bool ld = wv + 4 * sl < NT && 16 * tI[sl] < ncol && 4 * ks < KR;
+                    fa[sl][ks] = ld ? Gn[row + 16 * tI[sl] + (l & 15)] : 0.0;
+                    fb[sl][ks] = ld ? Bsrc[row + 16 * tJ[sl] + (l & 15)] : 0.0;
                 }
+            if (qd) {
+#pragma unroll
+                for (int sl = 0; sl < 3; ++sl)
+#pragma unroll
+                    for (int ks = 0; ks < 3; ++ks) fb[sl][ks] *= qv[ks];
             }
+            // (unconditional: a tile or k-step without data has zero operands and adds zeros — no exec-mask
+            // branches around the MFMAs, whose accumulators then stay in place)
+#pragma unroll
+            for (int ks = 0; ks < 3; ++ks)
+#pragma unroll
+                for (int sl = 0; sl < 3; ++sl)
+                    acc[sl] = __builtin_amdgcn_mfma_f64_16x16x4f64(fa[sl][ks], fb[sl][ks], acc[sl], 0, 0, 0);
         }
 #pragma unroll
         for (int sl = 0; sl < 3; ++sl) {
@@ -903,7 +926,7 @@ __global__ __launch_bounds__(kPT) void mpc_polish_kernel(const MpcConst c_arg, c
     auto is = [](int i, int j) { return i * (i + 1) / 2 + j; };
     int& flag_s = *reinterpret_cast<int*>(sm + L.red + 14);
     if (tid < kWave) {  // one wave, in the accumulators (n <= 64: every polished condensed shape)
-        const bool ok = wave_chol64(Lh, sm + L.rdH, n, Sm);
+        const bool ok = n <= 32 ? wave_chol64<2>(Lh, sm + L.rdH, n, Sm) : wave_chol64<4>(Lh, sm + L.rdH, n, Sm);
         if (tid == 0) flag_s = ok ? 1 : 0;
     }
     __syncthreads();
@@ -912,9 +935,6 @@ __global__ __launch_bounds__(kPT) void mpc_polish_kernel(const MpcConst c_arg, c
     __syncthreads();
     double best = INFINITY, best_kkt = INFINITY;
     int passes = 0, nsteps = 0;
-#ifdef CMPC_POL_LAB
-    unsigned long long lab_fwd = 0;
-#endif
     for (int pass = 0; pass < kPolishPasses && h_ok; ++pass) {
         passes = pass + 1;
         if (pass) active_list();
@@ -953,9 +973,81 @@ __global__ __launch_bounds__(kPT) void mpc_polish_kernel(const MpcConst c_arg, c
         }
         __syncthreads();
         PSTAMP(3);
-        // Y rows = L^-1 g: wave w substitutes rows w, w + 4, ... (lane i: entry i; the solved entry broadcast
-        // by readlane).  (Was one thread per row, an n-step dot-product loop: 0.17 M clocks at |A| ~ 20.)
-        for (int qa = tid >> 6; qa < nA; qa += kPT / kWave) wave_fsub64(Lh, sm + L.rdH, n, ih, Y + (size_t)qa * ldY);
+        // Y = G_A L^-T in place, blocked by 16 on V_MFMA_F64_16X16X4_F64: with D_J = L_JJ^-1 (the diagonal
+        // 16 x 16 blocks' inverses, lane (J, c) substituting column c of block J; rows past n the identity),
+        //     Y_J = (G_J - sum_{K<J} Y_K L_JK') D_J'
+        // for each 16-row tile of the active rows (wave w: tiles w, w + 4, ...), J = 0 .. T-1.  S's region
+        // is free until S is built: D_J at Sm (T x 16 x 17), each wave's staging tile after it.
+        // (Was wave-level forward substitution of each row, 60 readlane-chained steps: 60 k clocks at |A| ~ 20;
+        // before that one thread per row: 0.17 M.)
+        {
+            const int T = (n + 15) >> 4, RT = (nA + 15) >> 4;
+            const int wv = __builtin_amdgcn_readfirstlane(tid >> 6), l = tid & 63;
+            double* Dj = Sm;
+            double* Ts = Sm + 4 * 272 + wv * 272;
+            const double* rdH = sm + L.rdH;
+            if (tid < kWave) {
+                const int J = l >> 4, cc = l & 15;
+                if (J < T) {
+                    double x[16];
+#pragma unroll
+                    for (int i = 0; i < 16; ++i) {
+                        const int gi = 16 * J + i;
+                        double v = (i == cc) ? 1.0 : 0.0;
+#pragma unroll
+                        for (int p2 = 0; p2 < i; ++p2) {
+                            const double lv = gi < n ? Lh[gi * (gi + 1) / 2 + 16 * J + p2] : 0.0;
+                            v -= lv * x[p2];
+                        }
+                        x[i] = v * (gi < n ? rdH[gi] : 1.0);
+                    }
+#pragma unroll
+                    for (int i = 0; i < 16; ++i) Dj[J * 272 + i * 17 + cc] = x[i];
+                }
+            }
+            __syncthreads();
+            for (int I = wv; I < RT; I += kPT / kWave) {
+                for (int J = 0; J < T; ++J) {
+                    v4d acc;
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        const int row = 16 * I + (l >> 4) + 4 * r, col = 16 * J + (l & 15);
+                        acc[r] = (row < nA && col < n) ? Y[(size_t)row * ldY + col] : 0.0;
+                    }
+                    for (int K = 0; K < J; ++K) {
+                        double fa[4], fb[4];
+#pragma unroll
+                        for (int s2 = 0; s2 < 4; ++s2) {
+                            const int ra = 16 * I + (l & 15), rb = 16 * J + (l & 15), kc = 16 * K + 4 * s2 + (l >> 4);
+                            fa[s2] = ra < nA ? -Y[(size_t)ra * ldY + kc] : 0.0;
+                            fb[s2] = rb < n ? Lh[rb * (rb + 1) / 2 + kc] : 0.0;
+                        }
+#pragma unroll
+                        for (int s2 = 0; s2 < 4; ++s2) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(fa[s2], fb[s2], acc, 0, 0, 0);
+                    }
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) Ts[((l >> 4) + 4 * r) * 17 + (l & 15)] = acc[r];
+                    wsync();
+                    v4d yj = {0.0, 0.0, 0.0, 0.0};
+                    {
+                        double fa[4], fb[4];
+#pragma unroll
+                        for (int s2 = 0; s2 < 4; ++s2) {
+                            fa[s2] = Ts[(l & 15) * 17 + 4 * s2 + (l >> 4)];
+                            fb[s2] = Dj[J * 272 + (l & 15) * 17 + 4 * s2 + (l >> 4)];
+                        }
+#pragma unroll
+                        for (int s2 = 0; s2 < 4; ++s2) yj = __builtin_amdgcn_mfma_f64_16x16x4f64(fa[s2], fb[s2], yj, 0, 0, 0);
+                    }
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        const int row = 16 * I + (l >> 4) + 4 * r, col = 16 * J + (l & 15);
+                        if (row < nA && col < n) Y[(size_t)row * ldY + col] = yj[r];
+                    }
+                    wsync();
+                }
+            }
+        }
         __syncthreads();
         PSTAMP(4);
         // S = Y Y' + E (packed lower): the active rows' Gram matrix on V_MFMA_F64_16X16X4_F64.  16 x 16
@@ -966,7 +1058,7 @@ __global__ __launch_bounds__(kPT) void mpc_polish_kernel(const MpcConst c_arg, c
         // (Was one thread per packed entry with an n-term LDS dot product: 0.15 M clocks at nA ~ 80.)
         {
             const int TA = (nA + 15) >> 4, NTt = TA * (TA + 1) / 2, KS = (n + 3) >> 2;
-            const int wv = tid >> 6, l = tid & 63, i16 = l & 15, kq = l >> 4;
+            const int wv = __builtin_amdgcn_readfirstlane(tid >> 6), l = tid & 63, i16 = l & 15, kq = l >> 4;
             auto frag = [&](int blk, int s) {
                 const int row = 16 * blk + i16, col = 4 * s + kq;
                 const double v = Y[(size_t)(row < nA ? row : 0) * ldY + (col < n ? col : 0)];
@@ -1006,7 +1098,8 @@ __global__ __launch_bounds__(kPT) void mpc_polish_kernel(const MpcConst c_arg, c
         __syncthreads();
         if (nA <= 64 && (amax - nA) * ldY >= 7 * 272) {  // (Y is live: the scratch is its rows past nA)
             if (tid < kWave) {
-                const bool ok = wave_chol64(Sm, sm + L.rdS, nA, Y + (size_t)nA * ldY);
+                double* chs = Y + (size_t)nA * ldY;
+                const bool ok = nA <= 32 ? wave_chol64<2>(Sm, sm + L.rdS, nA, chs) : wave_chol64<4>(Sm, sm + L.rdS, nA, chs);
                 if (tid == 0) flag_s = ok ? 1 : 0;
             }
         } else {
@@ -1090,12 +1183,12 @@ __global__ __launch_bounds__(kPT) void mpc_polish_kernel(const MpcConst c_arg, c
             // t = max(w - row, 0) and lambda = 0 elsewhere; one Newton step normally reaches tol, a
             // refinement step follows only when it does not
             PSTAMP(5);
-#ifdef CMPC_POL_LAB  // lab: the clocks of one simulation sweep in slot 8
+#if defined(CMPC_POL_LAB) && CMPC_POL_LAB == 2
             const unsigned long long t_f0 = clock64_();
 #endif
             pol_fwd(q, Uc, sm + L.X);
             __syncthreads();
-#ifdef CMPC_POL_LAB
+#if defined(CMPC_POL_LAB) && CMPC_POL_LAB == 2
             lab_fwd = clock64_() - t_f0;
 #endif
             PSTAMP(6);
