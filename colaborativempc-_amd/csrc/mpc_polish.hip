@@ -435,9 +435,24 @@ __device__ void wave_bsub64(const double* M, const double* rd, int n, Idx idx, d
 }
 
 // The stage recursions below run on wave 0 with the state (or costate) in lanes 0..nx-1 of a register and
-// its entries broadcast by readlane: no LDS round trip or fence in the chain, and a stage's A / B entries
-// are loaded before it (one FMA chain per stage).  Same sums in the same order as the LDS forms they
-// replace (0.5-1.1 k clocks per stage: a load latency inside every chain).
+// its entries broadcast by readlane: no LDS round trip or fence in the chain.  The next stage's A / B
+// entries are loaded while a stage computes (two register sets, the loop unrolled by two), and each
+// nx-term product runs as three partial sums (terms t = 0, 3, 6, ...; 1, 4, 7, ...; 2, 5, 8, ...) so
+// the dependent chain is a third as long.  (Was an LDS form, one load latency inside every 9-term chain:
+// 0.7 k clocks per stage.)
+
+// the three partial sums of sum_t a[t] * v[t], t < nx, added in a fixed order
+template <int M>
+__device__ __forceinline__ double dot3(const double (&a)[M], const double (&v)[M], int nx) {
+    double s0 = 0.0, s1 = 0.0, s2 = 0.0;
+#pragma unroll
+    for (int t = 0; t < M; t += 3) {
+        if (t < nx) s0 = fma(a[t], v[t], s0);
+        if (t + 1 < M && t + 1 < nx) s1 = fma(a[t + 1], v[t + 1], s1);
+        if (t + 2 < M && t + 2 < nx) s2 = fma(a[t + 2], v[t + 2], s2);
+    }
+    return (s0 + s1) + s2;
+}
 
 // X = simulation of (x0, U) (wave 0; the other waves wait at the caller's barrier)
 __device__ __forceinline__ void pol_fwd(const PolCtx& q, const double* U, double* X) {
@@ -445,28 +460,42 @@ __device__ __forceinline__ void pol_fwd(const PolCtx& q, const double* U, double
     const int nx = q.nx, nu = q.nu, N = c.N, l = threadIdx.x;
     if (l >= kWave) return;
     const int lr = l < nx ? l : 0;
-    double x = q.x0[lr];
-    if (l < nx) X[l] = x;
-    for (int k = 0; k < N; ++k) {
-        const double* Ak = q.A + ((size_t)k * nx + lr) * nx;
-        const double* Bk = q.B + ((size_t)k * nx + lr) * nu;
+    struct Set {
         double a[CMPC_MAX_NX], bu[CMPC_MAX_NU], u[CMPC_MAX_NU];
+    };
+    auto load = [&](Set& S, int k) {
+        const int kk = k < N ? k : N - 1;  // (a clamped dummy past the horizon)
+        const double* Ak = q.A + ((size_t)kk * nx + lr) * nx;
+        const double* Bk = q.B + ((size_t)kk * nx + lr) * nu;
 #pragma unroll
-        for (int t = 0; t < CMPC_MAX_NX; ++t) a[t] = t < nx ? Ak[t] : 0.0;
+        for (int t = 0; t < CMPC_MAX_NX; ++t) S.a[t] = t < nx ? Ak[t] : 0.0;
 #pragma unroll
         for (int i = 0; i < CMPC_MAX_NU; ++i) {
-            bu[i] = i < nu ? Bk[i] : 0.0;
-            u[i] = i < nu ? U[k * nu + i] : 0.0;
+            S.bu[i] = i < nu ? Bk[i] : 0.0;
+            S.u[i] = i < nu ? U[kk * nu + i] : 0.0;
         }
-        double v = 0.0;
+    };
+    double x = q.x0[lr];
+    if (l < nx) X[l] = x;
+    auto stage = [&](const Set& S, int k) {
+        double xs[CMPC_MAX_NX];
 #pragma unroll
-        for (int t = 0; t < CMPC_MAX_NX; ++t)
-            if (t < nx) v += a[t] * readlane_d(x, t);
+        for (int t = 0; t < CMPC_MAX_NX; ++t) xs[t] = t < nx ? readlane_d(x, t) : 0.0;
+        double v = dot3(S.a, xs, nx);
 #pragma unroll
         for (int i = 0; i < CMPC_MAX_NU; ++i)
-            if (i < nu) v += bu[i] * u[i];
+            if (i < nu) v = fma(S.bu[i], S.u[i], v);
         x = v;
         if (l < nx) X[(k + 1) * nx + l] = v;
+    };
+    Set S0, S1;
+    load(S0, 0);
+    for (int k = 0; k < N; k += 2) {
+        load(S1, k + 1);
+        stage(S0, k);
+        if (k + 1 >= N) break;
+        load(S0, k + 2);
+        stage(S1, k + 1);
     }
     wsync();
 }
@@ -478,39 +507,46 @@ __device__ __forceinline__ void pol_adjoint(const PolCtx& q, double* y, double* 
     const int nx = q.nx, nu = q.nu, N = c.N, l = threadIdx.x;
     if (l >= kWave) return;
     const int lr = l < nx ? l : 0, lb = l < nu ? l : 0;
-    double psi = y[N * nx + lr];
-    for (int k = N - 1; k >= 0; --k) {
-        const double* Ak = q.A + (size_t)k * nx * nx;
-        const double* Bk = q.B + (size_t)k * nx * nu;
-        double a[CMPC_MAX_NX], bc[CMPC_MAX_NX], ps[CMPC_MAX_NX];
+    struct Set {
+        double a[CMPC_MAX_NX], bc[CMPC_MAX_NX], yk;
+    };
+    auto load = [&](Set& S, int k) {
+        const int kk = k >= 0 ? k : 0;
+        const double* Ak = q.A + (size_t)kk * nx * nx;
+        const double* Bk = q.B + (size_t)kk * nx * nu;
 #pragma unroll
         for (int s2 = 0; s2 < CMPC_MAX_NX; ++s2) {
-            a[s2] = s2 < nx ? Ak[s2 * nx + lr] : 0.0;
-            bc[s2] = s2 < nx ? Bk[s2 * nu + lb] : 0.0;
+            S.a[s2] = s2 < nx ? Ak[s2 * nx + lr] : 0.0;
+            S.bc[s2] = s2 < nx ? Bk[s2 * nu + lb] : 0.0;
         }
-        const double yk = y[k * nx + lr];
+        S.yk = y[kk * nx + lr];
+    };
+    double psi = y[N * nx + lr];
+    auto stage = [&](const Set& S, int k) {
+        double ps[CMPC_MAX_NX];
 #pragma unroll
         for (int s2 = 0; s2 < CMPC_MAX_NX; ++s2) ps[s2] = s2 < nx ? readlane_d(psi, s2) : 0.0;
-        double vo = 0.0;
-#pragma unroll
-        for (int s2 = 0; s2 < CMPC_MAX_NX; ++s2)
-            if (s2 < nx) vo += bc[s2] * ps[s2];
+        const double vo = dot3(S.bc, ps, nx);
         if (l < nu) out[k * nu + l] = vo;
         if (k > 0) {
-            double v = yk;
-#pragma unroll
-            for (int s2 = 0; s2 < CMPC_MAX_NX; ++s2)
-                if (s2 < nx) v += a[s2] * ps[s2];
-            psi = v;
-            if (l < nx) y[k * nx + l] = v;
+            psi = S.yk + dot3(S.a, ps, nx);
+            if (l < nx) y[k * nx + l] = psi;
         }
+    };
+    Set S0, S1;
+    load(S0, N - 1);
+    for (int k = N - 1; k >= 0; k -= 2) {
+        load(S1, k - 1);
+        stage(S0, k);
+        if (k - 1 < 0) break;
+        load(S0, k - 2);
+        stage(S1, k - 1);
     }
     wsync();
 }
 
 // both residual adjoints of pol_residuals in one sweep: chain 0 (lanes 0..31) as pol_adjoint on y (out0 = gU),
-// chain 1 (lanes 32..63) on y2 = y + C' lam on stages 1..N, formed as it goes (out1 = rd).  Same sums in the
-// same order as two pol_adjoint sweeps, y2 built as in pol_residuals.
+// chain 1 (lanes 32..63) on y2 = y + C' lam on stages 1..N, formed as it goes (out1 = rd).
 __device__ __forceinline__ void pol_adjoint2(const PolCtx& q, double* y, double* out0, double* out1, const double* lam) {
     const MpcConst& c = q.c;
     const int nx = q.nx, nu = q.nu, N = c.N, mc = c.mc, l = threadIdx.x;
@@ -523,34 +559,40 @@ __device__ __forceinline__ void pol_adjoint2(const PolCtx& q, double* y, double*
             for (int r = 0; r < mc; ++r) v += lam[(k - 1) * mc + r] * q.C[((size_t)(k - 1) * mc + r) * nx + lr];
         return v;
     };
-    double psi = y2(N);
-    for (int k = N - 1; k >= 0; --k) {
-        const double* Ak = q.A + (size_t)k * nx * nx;
-        const double* Bk = q.B + (size_t)k * nx * nu;
-        double a[CMPC_MAX_NX], bc[CMPC_MAX_NX], ps[CMPC_MAX_NX];
+    struct Set {
+        double a[CMPC_MAX_NX], bc[CMPC_MAX_NX], yk;
+    };
+    auto load = [&](Set& S, int k) {
+        const int kk = k >= 0 ? k : 0;
+        const double* Ak = q.A + (size_t)kk * nx * nx;
+        const double* Bk = q.B + (size_t)kk * nx * nu;
 #pragma unroll
         for (int s2 = 0; s2 < CMPC_MAX_NX; ++s2) {
-            a[s2] = s2 < nx ? Ak[s2 * nx + lr] : 0.0;
-            bc[s2] = s2 < nx ? Bk[s2 * nu + lb] : 0.0;
+            S.a[s2] = s2 < nx ? Ak[s2 * nx + lr] : 0.0;
+            S.bc[s2] = s2 < nx ? Bk[s2 * nu + lb] : 0.0;
         }
-        const double yk = k > 0 ? y2(k) : 0.0;
+        S.yk = kk > 0 ? y2(kk) : 0.0;
+    };
+    double psi = y2(N);
+    auto stage = [&](const Set& S, int k) {
+        double ps[CMPC_MAX_NX];
 #pragma unroll
         for (int s2 = 0; s2 < CMPC_MAX_NX; ++s2) {
             const double p0 = s2 < nx ? readlane_d(psi, s2) : 0.0, p1 = s2 < nx ? readlane_d(psi, 32 + s2) : 0.0;
             ps[s2] = ch ? p1 : p0;
         }
-        double vo = 0.0;
-#pragma unroll
-        for (int s2 = 0; s2 < CMPC_MAX_NX; ++s2)
-            if (s2 < nx) vo += bc[s2] * ps[s2];
+        const double vo = dot3(S.bc, ps, nx);
         if (j < nu) (ch ? out1 : out0)[k * nu + j] = vo;
-        if (k > 0) {
-            double v = yk;
-#pragma unroll
-            for (int s2 = 0; s2 < CMPC_MAX_NX; ++s2)
-                if (s2 < nx) v += a[s2] * ps[s2];
-            psi = v;
-        }
+        if (k > 0) psi = S.yk + dot3(S.a, ps, nx);
+    };
+    Set S0, S1;
+    load(S0, N - 1);
+    for (int k = N - 1; k >= 0; k -= 2) {
+        load(S1, k - 1);
+        stage(S0, k);
+        if (k - 1 < 0) break;
+        load(S0, k - 2);
+        stage(S1, k - 1);
     }
     wsync();
 }
