@@ -811,7 +811,7 @@ __global__ __launch_bounds__(kPT) void mpc_polish_kernel(const MpcConst c_arg, c
     }
     PSTAMP(0);
 #ifdef CMPC_POL_LAB  // lab: the clocks of a chosen region in slot 8 (CMPC_POL_LAB_REGION)
-    unsigned long long lab_fwd = 0, lab_t0 = 0;
+    unsigned long long lab_fwd = 0;
 #endif
     // ---- H = sum_k Gamma_{k+1}' (2Q Gamma_{k+1}) + the 2R / 2dR band (lower triangle), H = L L' ----
     // (cmpc_oracle.c polish_one's build.)  Gamma_{k+1} = A_k Gamma_k + B_k E_k (nx x n, zero beyond column
@@ -824,7 +824,7 @@ __global__ __launch_bounds__(kPT) void mpc_polish_kernel(const MpcConst c_arg, c
     {
         const int KR = (nx + 3) & ~3;
         double* Gb = Sm;                      // Gamma_k, Gamma_{k+1}: 2 x KR x kLdG
-        double* Wb = Sm + 2 * KR * kLdG;      // 2Q Gamma: 2 x KR x kLdG
+        double* Wb = Sm + 2 * KR * kLdG;      // 2Q Gamma_{k+1}: KR x kLdG
         for (int i = tid; i < 4 * KR * kLdG; i += kPT) Sm[i] = 0.0;
         int qptr = 0;  // the first active row of pass 0 not yet formed (Ar ascending: stage by stage)
         const int T = (n + 15) >> 4, NT = T * (T + 1) / 2;
@@ -847,14 +847,10 @@ __global__ __launch_bounds__(kPT) void mpc_polish_kernel(const MpcConst c_arg, c
             const int s2 = 4 * ks + (l >> 4);
             qv[ks] = s2 < nx ? 2.0 * c.Q[s2 * nx + s2] : 0.0;
         }
-        __syncthreads();
-        for (int k = 0; k < N; ++k) {
-#if defined(CMPC_POL_LAB) && CMPC_POL_LAB == 1
-            lab_t0 = clock64_();
-#endif
+        // Gamma_{k+1} from Gamma_k (ping-pong buffer k & 1 -> (k + 1) & 1; thread: column l, rows wv + 4 i)
+        auto gamma_step = [&](int k) {
             const double* Gc = Gb + (k & 1) * KR * kLdG;
             double* Gn = Gb + ((k + 1) & 1) * KR * kLdG;
-            double* Wn = Wb + ((k + 1) & 1) * KR * kLdG;
             const int ncol = (k + 1) * nu, j = l;
             if (j < ncol) {
                 const double* Ak = q.A + k * nx * nx;
@@ -878,10 +874,43 @@ __global__ __launch_bounds__(kPT) void mpc_polish_kernel(const MpcConst c_arg, c
                     }
                 }
             }
-            __syncthreads();
-#if defined(CMPC_POL_LAB) && CMPC_POL_LAB == 1
-            lab_fwd += clock64_() - lab_t0;
-#endif
+        };
+        __syncthreads();
+        gamma_step(0);
+        __syncthreads();
+        // one barrier per stage: stage k's MFMAs and G_A rows read Gamma_{k+1} while the same phase forms
+        // Gamma_{k+2} into the other buffer (Gamma_k's, read by nobody after the previous barrier)
+        for (int k = 0; k < N; ++k) {
+            const double* Gn = Gb + ((k + 1) & 1) * KR * kLdG;
+            const int ncol = (k + 1) * nu, j = l;
+            if (!qd) {  // W = 2Q Gamma_{k+1} (one buffer: the previous stage's MFMAs finished before the barrier)
+                if (j < ncol) {
+                    double gn[CMPC_MAX_NX];
+#pragma unroll
+                    for (int t2 = 0; t2 < CMPC_MAX_NX; ++t2) gn[t2] = t2 < nx ? Gn[t2 * kLdG + j] : 0.0;
+                    for (int s2 = wv; s2 < nx; s2 += 4) {
+                        double v = 0.0;
+#pragma unroll
+                        for (int t2 = 0; t2 < CMPC_MAX_NX; ++t2)
+                            if (t2 < nx) v += 2.0 * c.Q[s2 * nx + t2] * gn[t2];
+                        Wb[s2 * kLdG + j] = v;
+                    }
+                }
+                __syncthreads();
+            }
+            // every fragment loaded first, then the next stage's Gamma, then the three tiles' MFMA chains
+            double fa[3][3], fb[3][3];
+            const double* Bsrc = qd ? Gn : Wb;
+#pragma unroll
+            for (int sl = 0; sl < 3; ++sl)
+#pragma unroll
+                for (int ks = 0; ks < 3; ++ks) {
+                    const int row = (4 * ks + (l >> 4)) * kLdG;
+                    const bool ld = wv + 4 * sl < NT && 16 * tI[sl] < ncol && 4 * ks < KR;
+                    fa[sl][ks] = ld ? Gn[row + 16 * tI[sl] + (l & 15)] : 0.0;
+                    fb[sl][ks] = ld ? Bsrc[row + 16 * tJ[sl] + (l & 15)] : 0.0;
+                }
+            if (k + 1 < N) gamma_step(k + 1);
             if (nA0 <= amax) {  // pass 0's active rows of stage k: g = c_r' Gamma_{k+1}
                 // (this stage's rows follow qptr in Ar: counted by ballot over the next 64, every wave alike;
                 // a stage holds at most mc <= 64 rows)
@@ -900,33 +929,6 @@ __global__ __launch_bounds__(kPT) void mpc_polish_kernel(const MpcConst c_arg, c
                 }
                 qptr = q1;
             }
-            if (!qd) {
-                if (j < ncol) {
-                    double gn[CMPC_MAX_NX];
-#pragma unroll
-                    for (int t2 = 0; t2 < CMPC_MAX_NX; ++t2) gn[t2] = t2 < nx ? Gn[t2 * kLdG + j] : 0.0;
-                    for (int s2 = wv; s2 < nx; s2 += 4) {
-                        double v = 0.0;
-#pragma unroll
-                        for (int t2 = 0; t2 < CMPC_MAX_NX; ++t2)
-                            if (t2 < nx) v += 2.0 * c.Q[s2 * nx + t2] * gn[t2];
-                        Wn[s2 * kLdG + j] = v;
-                    }
-                }
-                __syncthreads();
-            }
-            // every fragment loaded first, then the three tiles' MFMA chains interleaved
-            double fa[3][3], fb[3][3];
-            const double* Bsrc = qd ? Gn : Wn;
-#pragma unroll
-            for (int sl = 0; sl < 3; ++sl)
-#pragma unroll
-                for (int ks = 0; ks < 3; ++ks) {
-                    const int row = (4 * ks + (l >> 4)) * kLdG;
-                    const bool ld = wv + 4 * sl < NT && 16 * tI[sl] < ncol && 4 * ks < KR;
-                    fa[sl][ks] = ld ? Gn[row + 16 * tI[sl] + (l & 15)] : 0.0;
-                    fb[sl][ks] = ld ? Bsrc[row + 16 * tJ[sl] + (l & 15)] : 0.0;
-                }
             if (qd) {
 #pragma unroll
                 for (int sl = 0; sl < 3; ++sl)
@@ -940,6 +942,7 @@ __global__ __launch_bounds__(kPT) void mpc_polish_kernel(const MpcConst c_arg, c
 #pragma unroll
                 for (int sl = 0; sl < 3; ++sl)
                     acc[sl] = __builtin_amdgcn_mfma_f64_16x16x4f64(fa[sl][ks], fb[sl][ks], acc[sl], 0, 0, 0);
+            __syncthreads();
         }
 #pragma unroll
         for (int sl = 0; sl < 3; ++sl) {
