@@ -44,6 +44,11 @@ constexpr int kStageMax = CMPC_MAX_NX * CMPC_MAX_NX + CMPC_MAX_NX * CMPC_MAX_NU 
 constexpr int kPerMax = (kStageMax + kWave - 1) / kWave;  // stage-image values per lane (largest dims)
 constexpr int kPerSmall = 2;                               // ... when the stage image fits 128 values
 constexpr int kDepth = 3;  // stage images in flight: a sweep step waits for a load issued 2 steps earlier
+// Row loops over r = l, l + 64, ... < m run in chunks of kRowChunk rows per lane, every load of a chunk
+// issued before any of its arithmetic (rows past m read row l, a valid index, and are not used): the GR
+// instantiations keep the row vectors in global scratch, and a per-row loop with the loads behind its
+// branches waited one memory latency per row.  The same operations in the same order per row.
+constexpr int kRowChunk = 4;
 constexpr double kDdTh = 1e10;   // max th above which an iteration runs in double-double ...
 // ... once the solve has made no new best iterate for kDdStall iterations (or the fp64 factorisation
 // broke down): on 2048 BASELINE cfg5 agents the double-double iterations drop 3136 -> 181 (25 % ->
@@ -1868,19 +1873,38 @@ __global__ __launch_bounds__(kWave) void mpc_riccati_kernel(const MpcConst c_arg
         for (int i = l; i < N * ns; i += kWave) {
             const int k = i / ns, j = i - k * ns;
             double v = 2.0 * c.Qs[j] * sig[i];
-            for (int r = 0; r < mc; ++r)
-                if (c.row_slack[r] == j) v += c.row_sign[r] * lam[k * mc + r];
+            constexpr int MCB = G::MC ? G::MC : CMPC_MAX_MC;
+            double lk[MCB];
+#pragma unroll
+            for (int r = 0; r < MCB; ++r) lk[r] = r < mc ? lam[k * mc + r] : 0.0;
+#pragma unroll
+            for (int r = 0; r < MCB; ++r)
+                if (r < mc && c.row_slack[r] == j) v += c.row_sign[r] * lk[r];
             rsig[i] = v;
             nrs_l = nmax(nrs_l, fabs(v));
         }
-        for (int r = l; r < m; r += kWave) {
-            if (isfinite(w[r])) {
-                const double v = row_value<G>(c, C, r, X, U, sig) + t[r] - w[r];
-                rp[r] = v;
-                nrp_l = nmax(nrp_l, fabs(v));
-                mu_l += t[r] * lam[r];
-            } else {
-                rp[r] = 0.0;
+        for (int r0 = l; r0 < m; r0 += kRowChunk * kWave) {
+            double wv[kRowChunk], tv[kRowChunk], lv[kRowChunk], gv[kRowChunk];
+#pragma unroll
+            for (int i = 0; i < kRowChunk; ++i) {
+                const int r = r0 + i * kWave, rc = r < m ? r : l;
+                wv[i] = w[rc];
+                tv[i] = t[rc];
+                lv[i] = lam[rc];
+                gv[i] = row_value<G>(c, C, rc, X, U, sig);
+            }
+#pragma unroll
+            for (int i = 0; i < kRowChunk; ++i) {
+                const int r = r0 + i * kWave;
+                if (r >= m) break;
+                if (isfinite(wv[i])) {
+                    const double v = gv[i] + tv[i] - wv[i];
+                    rp[r] = v;
+                    nrp_l = nmax(nrp_l, fabs(v));
+                    mu_l += tv[i] * lv[i];
+                } else {
+                    rp[r] = 0.0;
+                }
             }
         }
         const double mu = wave_sum(mu_l) / mact;
@@ -1914,7 +1938,21 @@ __global__ __launch_bounds__(kWave) void mpc_riccati_kernel(const MpcConst c_arg
 
         RSTAMP(0);
         // ================= Newton system: Riccati factorisation =================
-        for (int r = l; r < m; r += kWave) th[r] = isfinite(w[r]) ? lam[r] / t[r] : 0.0;
+        for (int r0 = l; r0 < m; r0 += kRowChunk * kWave) {
+            double wv[kRowChunk], tv[kRowChunk], lv[kRowChunk];
+#pragma unroll
+            for (int i = 0; i < kRowChunk; ++i) {
+                const int r = r0 + i * kWave, rc = r < m ? r : l;
+                wv[i] = w[rc];
+                tv[i] = t[rc];
+                lv[i] = lam[rc];
+            }
+#pragma unroll
+            for (int i = 0; i < kRowChunk; ++i) {
+                const int r = r0 + i * kWave;
+                if (r < m) th[r] = isfinite(wv[i]) ? lv[i] / tv[i] : 0.0;
+            }
+        }
         wsync();
         for (int i = l; i < N * ns; i += kWave) {
             const int k = i / ns, j = i - k * ns;
@@ -1964,14 +2002,30 @@ __global__ __launch_bounds__(kWave) void mpc_riccati_kernel(const MpcConst c_arg
         // ================= predictor / corrector =================
         double sig_c = 0.0, alpha = 0.0;
         for (int pass = 0; pass < 2; ++pass) {
-            for (int r = l; r < m; r += kWave) {
-                if (!isfinite(w[r])) {
-                    rho[r] = 0.0;
-                    continue;
+            for (int r0 = l; r0 < m; r0 += kRowChunk * kWave) {
+                double wv[kRowChunk], tv[kRowChunk], lv[kRowChunk], pv[kRowChunk], av[kRowChunk], bv[kRowChunk];
+#pragma unroll
+                for (int i = 0; i < kRowChunk; ++i) {
+                    const int r = r0 + i * kWave, rc = r < m ? r : l;
+                    wv[i] = w[rc];
+                    tv[i] = t[rc];
+                    lv[i] = lam[rc];
+                    pv[i] = rp[rc];
+                    av[i] = pass ? dta[rc] : 0.0;
+                    bv[i] = pass ? dla[rc] : 0.0;
                 }
-                double rc = -t[r] * lam[r];
-                if (pass) rc += sig_c * mu - dta[r] * dla[r];
-                rho[r] = (rc + lam[r] * rp[r]) / t[r];
+#pragma unroll
+                for (int i = 0; i < kRowChunk; ++i) {
+                    const int r = r0 + i * kWave;
+                    if (r >= m) break;
+                    if (!isfinite(wv[i])) {
+                        rho[r] = 0.0;
+                        continue;
+                    }
+                    double rc = -tv[i] * lv[i];
+                    if (pass) rc += sig_c * mu - av[i] * bv[i];
+                    rho[r] = (rc + lv[i] * pv[i]) / tv[i];
+                }
             }
             rsync();  // rho: read across lanes (same-stage rows, slack directions)
             for (int r = l; r < m; r += kWave) {
@@ -1979,12 +2033,17 @@ __global__ __launch_bounds__(kWave) void mpc_riccati_kernel(const MpcConst c_arg
                 if (r < ms) {
                     const int k = r / mc, rr = r - k * mc, j = c.row_slack[rr];
                     if (j >= 0) {
+                        constexpr int MCB = G::MC ? G::MC : CMPC_MAX_MC;
+                        double rk[MCB];  // the stage's rho, loaded together
+#pragma unroll
+                        for (int r2 = 0; r2 < MCB; ++r2) rk[r2] = r2 < mc ? rho[k * mc + r2] : 0.0;
                         const double q = 2.0 * c.Qs[j];
                         v = q * rho[r] - th[r] * c.row_sign[rr] * rsig[k * ns + j];
-                        for (int r2 = 0; r2 < mc; ++r2) {
-                            if (r2 == rr || c.row_slack[r2] != j) continue;
+#pragma unroll
+                        for (int r2 = 0; r2 < MCB; ++r2) {
+                            if (r2 >= mc || r2 == rr || c.row_slack[r2] != j) continue;
                             const int R2 = k * mc + r2;
-                            v += th[R2] * rho[r] - th[r] * c.row_sign[rr] * c.row_sign[r2] * rho[R2];
+                            v += th[R2] * rho[r] - th[r] * c.row_sign[rr] * c.row_sign[r2] * rk[r2];
                         }
                         v /= Dsig[k * ns + j];
                     }
@@ -2039,15 +2098,33 @@ __global__ __launch_bounds__(kWave) void mpc_riccati_kernel(const MpcConst c_arg
                 fwd_sim<G>(c, d, sAB, sb, nullptr, dU, dX);
                 RSTAMP(6);
             }
-            for (int r = l; r < m; r += kWave) GdU[r] = row_value<G>(c, C, r, dX, dU, nullptr);
+            for (int r0 = l; r0 < m; r0 += kRowChunk * kWave) {
+                double gv[kRowChunk];
+#pragma unroll
+                for (int i = 0; i < kRowChunk; ++i) {
+                    const int r = r0 + i * kWave;
+                    gv[i] = row_value<G>(c, C, r < m ? r : l, dX, dU, nullptr);
+                }
+#pragma unroll
+                for (int i = 0; i < kRowChunk; ++i)
+                    if (r0 + i * kWave < m) GdU[r0 + i * kWave] = gv[i];
+            }
             rsync();  // GdU: read across lanes by the slack directions
             for (int i = l; i < N * ns; i += kWave) {
                 const int k = i / ns, j = i - k * ns;
                 double v = rsig[i];
-                for (int r = 0; r < mc; ++r)
-                    if (c.row_slack[r] == j) {
+                constexpr int MCB = G::MC ? G::MC : CMPC_MAX_MC;
+                double rk[MCB], gk[MCB];  // the stage's rho and GdU, loaded together
+#pragma unroll
+                for (int r = 0; r < MCB; ++r) {
+                    rk[r] = r < mc ? rho[k * mc + r] : 0.0;
+                    gk[r] = r < mc ? GdU[k * mc + r] : 0.0;
+                }
+#pragma unroll
+                for (int r = 0; r < MCB; ++r)
+                    if (r < mc && c.row_slack[r] == j) {
                         const int R1 = k * mc + r;
-                        v += c.row_sign[r] * (rho[R1] + th[R1] * GdU[R1]);
+                        v += c.row_sign[r] * (rk[r] + th[R1] * gk[r]);
                     }
                 dsig[i] = -v / Dsig[i];
             }
@@ -2055,32 +2132,61 @@ __global__ __launch_bounds__(kWave) void mpc_riccati_kernel(const MpcConst c_arg
             double amax_l = 1.0e300;
             double* dtp = pass ? rho : dta;  // corrector reuses rho/rt storage for (dt, dl)
             double* dlp = pass ? rt : dla;
-            for (int r = l; r < m; r += kWave) {
-                if (!isfinite(w[r])) {
-                    dtp[r] = 0.0;
-                    dlp[r] = 0.0;
-                    continue;
+            for (int r0 = l; r0 < m; r0 += kRowChunk * kWave) {
+                double wv[kRowChunk], rv[kRowChunk], pv[kRowChunk], gv[kRowChunk], tv[kRowChunk], lv[kRowChunk];
+#pragma unroll
+                for (int i = 0; i < kRowChunk; ++i) {
+                    const int r = r0 + i * kWave, rc = r < m ? r : l;
+                    wv[i] = w[rc];
+                    rv[i] = rho[rc];
+                    pv[i] = rp[rc];
+                    gv[i] = GdU[rc];
+                    tv[i] = t[rc];
+                    lv[i] = lam[rc];
                 }
-                double sd = 0.0;
-                if (r < ms) {
-                    const int k = r / mc, rr = r - k * mc, j = c.row_slack[rr];
-                    if (j >= 0) sd = c.row_sign[rr] * dsig[k * ns + j];
+#pragma unroll
+                for (int i = 0; i < kRowChunk; ++i) {
+                    const int r = r0 + i * kWave;
+                    if (r >= m) break;
+                    if (!isfinite(wv[i])) {
+                        dtp[r] = 0.0;
+                        dlp[r] = 0.0;
+                        continue;
+                    }
+                    double sd = 0.0;
+                    if (r < ms) {
+                        const int k = r / mc, rr = r - k * mc, j = c.row_slack[rr];
+                        if (j >= 0) sd = c.row_sign[rr] * dsig[k * ns + j];
+                    }
+                    const double rho_r = rv[i];
+                    const double dtv = -pv[i] - gv[i] - sd;
+                    const double dlv = rho_r + th[r] * (gv[i] + sd);
+                    dtp[r] = dtv;
+                    dlp[r] = dlv;
+                    if (dtv < 0.0) amax_l = fmin(amax_l, -tv[i] / dtv);
+                    if (dlv < 0.0) amax_l = fmin(amax_l, -lv[i] / dlv);
                 }
-                const double rho_r = rho[r];
-                const double dtv = -rp[r] - GdU[r] - sd;
-                const double dlv = rho_r + th[r] * (GdU[r] + sd);
-                dtp[r] = dtv;
-                dlp[r] = dlv;
-                if (dtv < 0.0) amax_l = fmin(amax_l, -t[r] / dtv);
-                if (dlv < 0.0) amax_l = fmin(amax_l, -lam[r] / dlv);
             }
             const double amax = fmin(wave_min(amax_l), 1.0e300);
             wsync();
             if (!pass) {
                 const double a = fmin(amax, 1.0);
                 double mua_l = 0.0;
-                for (int r = l; r < m; r += kWave)
-                    if (isfinite(w[r])) mua_l += (t[r] + a * dta[r]) * (lam[r] + a * dla[r]);
+                for (int r0 = l; r0 < m; r0 += kRowChunk * kWave) {
+                    double wv[kRowChunk], tv[kRowChunk], lv[kRowChunk], av[kRowChunk], bv[kRowChunk];
+#pragma unroll
+                    for (int i = 0; i < kRowChunk; ++i) {
+                        const int r = r0 + i * kWave, rc = r < m ? r : l;
+                        wv[i] = w[rc];
+                        tv[i] = t[rc];
+                        lv[i] = lam[rc];
+                        av[i] = dta[rc];
+                        bv[i] = dla[rc];
+                    }
+#pragma unroll
+                    for (int i = 0; i < kRowChunk; ++i)
+                        if (r0 + i * kWave < m && isfinite(wv[i])) mua_l += (tv[i] + a * av[i]) * (lv[i] + a * bv[i]);
+                }
                 const double mu_aff = wave_sum(mua_l) / mact;
                 const double ratio = mu > 0.0 ? mu_aff / mu : 0.0;
                 // e = 3; a warm continuation of a condensed solve keeps that method's e = 2 (internal.h)
@@ -2091,12 +2197,25 @@ __global__ __launch_bounds__(kWave) void mpc_riccati_kernel(const MpcConst c_arg
                 // stay in the wide neighbourhood t_r lam_r >= gamma mu(alpha) (see kNbhdGamma)
                 for (int bt = 0; bt < kMaxBacktrack; ++bt) {
                     double mn_l = 0.0, pm_l = INFINITY;
-                    for (int r = l; r < m; r += kWave)
-                        if (isfinite(w[r])) {
-                            const double pr = (t[r] + alpha * rho[r]) * (lam[r] + alpha * rt[r]);
-                            mn_l += pr;
-                            pm_l = fmin(pm_l, pr);
+                    for (int r0 = l; r0 < m; r0 += kRowChunk * kWave) {
+                        double wv[kRowChunk], tv[kRowChunk], rv[kRowChunk], lv[kRowChunk], qv[kRowChunk];
+#pragma unroll
+                        for (int i = 0; i < kRowChunk; ++i) {
+                            const int r = r0 + i * kWave, rc = r < m ? r : l;
+                            wv[i] = w[rc];
+                            tv[i] = t[rc];
+                            rv[i] = rho[rc];
+                            lv[i] = lam[rc];
+                            qv[i] = rt[rc];
                         }
+#pragma unroll
+                        for (int i = 0; i < kRowChunk; ++i)
+                            if (r0 + i * kWave < m && isfinite(wv[i])) {
+                                const double pr = (tv[i] + alpha * rv[i]) * (lv[i] + alpha * qv[i]);
+                                mn_l += pr;
+                                pm_l = fmin(pm_l, pr);
+                            }
+                    }
                     if (wave_min(pm_l) >= kNbhdGamma * (wave_sum(mn_l) / mact)) break;
                     alpha *= 0.8;
                 }
@@ -2108,11 +2227,26 @@ __global__ __launch_bounds__(kWave) void mpc_riccati_kernel(const MpcConst c_arg
         for (int i = l; i < n; i += kWave) U[i] = fma(alpha, dU[i], U[i]);
         for (int i = l; i < N * ns; i += kWave) sig[i] = fma(alpha, dsig[i], sig[i]);
         for (int i = l; i < (N + 1) * nx; i += kWave) X[i] = fma(alpha, dX[i], X[i]);
-        for (int r = l; r < m; r += kWave)
-            if (isfinite(w[r])) {
-                t[r] = fma(alpha, rho[r], t[r]);
-                lam[r] = fma(alpha, rt[r], lam[r]);
+        for (int r0 = l; r0 < m; r0 += kRowChunk * kWave) {
+            double wv[kRowChunk], tv[kRowChunk], rv[kRowChunk], lv[kRowChunk], qv[kRowChunk];
+#pragma unroll
+            for (int i = 0; i < kRowChunk; ++i) {
+                const int r = r0 + i * kWave, rc = r < m ? r : l;
+                wv[i] = w[rc];
+                tv[i] = t[rc];
+                rv[i] = rho[rc];
+                lv[i] = lam[rc];
+                qv[i] = rt[rc];
             }
+#pragma unroll
+            for (int i = 0; i < kRowChunk; ++i) {
+                const int r = r0 + i * kWave;
+                if (r < m && isfinite(wv[i])) {
+                    t[r] = fma(alpha, rv[i], tv[i]);
+                    lam[r] = fma(alpha, qv[i], lv[i]);
+                }
+            }
+        }
         rsync();  // lam: read across lanes by the next residuals
         RSTAMP(8);
     }
