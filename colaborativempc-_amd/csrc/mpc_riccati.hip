@@ -43,7 +43,7 @@ constexpr int kStageMax = CMPC_MAX_NX * CMPC_MAX_NX + CMPC_MAX_NX * CMPC_MAX_NU 
                           CMPC_MAX_NU * CMPC_MAX_NU;
 constexpr int kPerMax = (kStageMax + kWave - 1) / kWave;  // stage-image values per lane (largest dims)
 constexpr int kPerSmall = 2;                               // ... when the stage image fits 128 values
-constexpr int kDepth = 3;  // stage images in flight: a sweep step waits for a load issued 2 steps earlier
+constexpr int kDepth = 6;  // stage images in flight: a sweep step waits for a load issued 5 steps earlier
 // Row loops over r = l, l + 64, ... < m run in chunks of kRowChunk rows per lane, every load of a chunk
 // issued before any of its arithmetic (rows past m read row l, a valid index, and are not used): the GR
 // instantiations keep the row vectors in global scratch, and a per-row loop with the loads behind its
