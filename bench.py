@@ -231,11 +231,13 @@ def main():
         dist.destroy_process_group()
 
 
-def cfg5_line(ctx, steps=5, warmup=2):
+def cfg5_line(ctx, steps=10, warmup=2):
     """BASELINE configs[4] inside the default line, so the driver observes it: 8192 agents, N = 50,
     3-D double integrator (nx 6, nu 3), nb 2 — the fp64 stage-wise Riccati path and the fp32 path
     (the Riccati kernel's fp32 mode: fp32 factorisation and Newton recursions, fp64 iterates,
-    tol 1e-6), each timed over `steps` device-resident rounds after `warmup` (the same step as the
+    tol 1e-6), each timed over `steps` device-resident rounds after `warmup` (10 / 2: the standalone
+    `--config cfg5` line's counts, so the two agree; 5 timed rounds read ~7 % lower: 237.7k against
+    255.8k agent-QP/s in profiles/r05ad_*) (the same step as the
     main line: build + solve + advance + exchange), with the fp32 path's tolerance check against the
     fp64 solve of the same problems (fp32_vs_fp64: every agent's max |z32 - z64| / max(1, |z64|),
     bar 1e-3) and its roofline (stage-wise Riccati flops at the measured iterations)."""
