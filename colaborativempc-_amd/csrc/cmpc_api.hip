@@ -220,13 +220,17 @@ int cmpc_solve_mpc_batch_dev(cmpc_ctx* ctx, const cmpc_mpc_dims* dims, const cmp
     if (rc != CMPC_OK) return fail(ctx, rc, msg);
     if ((rc = set_device(ctx)) != CMPC_OK) return rc;
     double* ws = nullptr;
+    int* plist = nullptr;
     if (const size_t wsd = cmpc::mpc_ws_doubles(c) * (size_t)dims->batch) {
-        ws = reinterpret_cast<double*>(arena(ctx, 8 * wsd));
+        // (+ the polish launch's compacted agent list: batch + 1 ints after the scratch)
+        ws = reinterpret_cast<double*>(arena(ctx, 8 * wsd + 4 * ((size_t)dims->batch + 1)));
         if (!ws) return fail(ctx, CMPC_ERR_NOMEM, "device scratch allocation failed");
+        plist = reinterpret_cast<int*>(ws + wsd);
     }
     cmpc::MpcPtrs p{in->A, in->B, in->x0, in->u_prev, in->qlin, in->C, in->h, out->z, out->kkt, out->iters, out->status,
                     opts ? (unsigned long long*)opts->stamps : nullptr, ws};
     p.order = opts ? opts->order : nullptr;
+    p.plist = plist;
     HIP_TRY(cmpc::mpc_launch(c, p, dims->batch, (hipStream_t)stream, opts ? opts->flags : 0));
     return CMPC_OK;
 }
@@ -275,7 +279,7 @@ int cmpc_solve_mpc_batch(cmpc_ctx* ctx, const cmpc_mpc_dims* d, const cmpc_mpc_w
     const size_t sA = B * N * nx * nx, sB = B * N * nx * nu, sx = B * nx, su = B * nu, sp = B * (N + 1) * nx,
                  sC = B * N * mc * nx, sh = B * N * mc, sz = B * mpc_nz(*d);
     const size_t sw = cmpc::mpc_ws_doubles(c) * B;
-    const size_t bytes = 8 * (sA + sB + sx + su + sp + sC + sh + sz + B + sw) + 8 * B + 16 * 256;
+    const size_t bytes = 8 * (sA + sB + sx + su + sp + sC + sh + sz + B + sw) + 8 * B + 4 * (B + 1) + 16 * 256;
     char* base = arena(ctx, bytes);
     if (!base) return fail(ctx, CMPC_ERR_NOMEM, "device arena allocation failed");
     Carve cv{base};
@@ -284,6 +288,7 @@ int cmpc_solve_mpc_batch(cmpc_ctx* ctx, const cmpc_mpc_dims* d, const cmpc_mpc_w
            *dh = cv.take<double>(sh), *dz = cv.take<double>(sz), *dk = cv.take<double>(B);
     int *di = cv.take<int>(B), *ds = cv.take<int>(B);
     double* dw = sw ? cv.take<double>(sw) : nullptr;
+    int* dpl = sw ? cv.take<int>(B + 1) : nullptr;  // the polish launch's compacted agent list
     hipStream_t s = ctx->stream;
     HIP_TRY(hipMemcpyAsync(dA, in->A, 8 * sA, hipMemcpyHostToDevice, s));
     HIP_TRY(hipMemcpyAsync(dB, in->B, 8 * sB, hipMemcpyHostToDevice, s));
@@ -294,6 +299,7 @@ int cmpc_solve_mpc_batch(cmpc_ctx* ctx, const cmpc_mpc_dims* d, const cmpc_mpc_w
     HIP_TRY(hipMemcpyAsync(dh, in->h, 8 * sh, hipMemcpyHostToDevice, s));
     cmpc::MpcPtrs p{dA, dB, dx0, du, dp, dC, dh, dz, dk, di, ds,
                     opts ? (unsigned long long*)opts->stamps : nullptr, dw};  // stamps: device memory
+    p.plist = dpl;
     HIP_TRY(cmpc::mpc_launch(c, p, d->batch, s, opts ? opts->flags : 0));
     HIP_TRY(hipMemcpyAsync(out->z, dz, 8 * sz, hipMemcpyDeviceToHost, s));
     if (out->kkt) HIP_TRY(hipMemcpyAsync(out->kkt, dk, 8 * B, hipMemcpyDeviceToHost, s));
@@ -307,7 +313,7 @@ int cmpc_solve_mpc_batch(cmpc_ctx* ctx, const cmpc_mpc_dims* d, const cmpc_mpc_w
 static size_t lpv_ws_bytes(const cmpc_lpv_dims* d, size_t solver_ws_doubles) {
     const size_t B = d->batch, N = d->N, mc = 4 + d->nb;
     return 8 * (B * N * 81 + B * N * 18 + B * (N + 1) * 9 + B * N * mc * 9 + B * N * mc + B * solver_ws_doubles) +
-           4 * B + 10 * 256;
+           4 * B + 4 * (B + 1) + 11 * 256;  // (B + 1 ints: the polish launch's compacted agent list)
 }
 
 static int lpv_run(cmpc_ctx* ctx, const cmpc_lpv_params* prm, const cmpc_track* tr, const cmpc_lpv_dims* d,
@@ -324,11 +330,13 @@ static int lpv_run(cmpc_ctx* ctx, const cmpc_lpv_params* prm, const cmpc_track* 
     int* err = cv.take<int>(B);
     const size_t sw = cmpc::mpc_ws_doubles(mc) * B;
     double* ws = sw ? cv.take<double>(sw) : nullptr;
+    int* plist = sw ? cv.take<int>(B + 1) : nullptr;  // the polish launch's compacted agent list
     HIP_TRY(hipMemsetAsync(err, 0, 4 * B, s));
     cmpc::LpvPtrs lp{in->x_last, in->u_last, in->x_agents, in->pose, A, Bm, p, C, h, out->planes, err};
     HIP_TRY(cmpc::lpv_build_launch(lc, lp, d->batch, s));
     cmpc::MpcPtrs mp{A, Bm, in->x0, in->u_old, p, C, h, out->z, out->kkt, out->iters, out->status,
                     opts ? (unsigned long long*)opts->stamps : nullptr, ws};  // stamps: device memory
+    mp.plist = plist;
     HIP_TRY(cmpc::mpc_launch(mc, mp, d->batch, s, opts ? opts->flags : 0));
     HIP_TRY(cmpc::lpv_mark_launch(err, out->status, out->z, (int)(12 * (N + 1) + 4 * N), d->batch, s));
     return CMPC_OK;

@@ -84,6 +84,9 @@ struct MpcPtrs {
     double* ws;                  // device scratch, batch x mpc_ws_doubles(c) (Riccati kernel; else unused)
     DiFuse fuse;                 // fused row build (v3 kernel only; on = 0 elsewhere)
     const int* order;            // optional launch order (Riccati kernel: workgroup i solves agent order[i])
+    // optional device scratch of batch + 1 ints for the polish launch's compacted agent list (mpc_polish.hip):
+    // without it every workgroup maps to its own agent and the flagged ones queue behind each other on a CU
+    int* plist = nullptr;
 };
 
 // Interior-point safeguards shared by both solver kernels and the C oracle (oracle/cmpc_oracle.c).

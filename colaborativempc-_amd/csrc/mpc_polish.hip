@@ -713,7 +713,13 @@ __device__ __forceinline__ double pol_residuals(const PolCtx& q, const double* U
 template <int NXT, int NUT>
 __global__ __launch_bounds__(kPT) void mpc_polish_kernel(const MpcConst c_arg, const MpcPtrs P) {
     extern __shared__ __attribute__((aligned(16))) double sm[];
-    const int b = blockIdx.x;
+    // with the compacted list (polish_list_kernel): workgroup i polishes the i-th flagged agent, so the
+    // flagged agents start on distinct CUs at once instead of queueing behind each other
+    int b = blockIdx.x;
+    if (P.plist) {
+        if (b >= P.plist[gridDim.x]) return;
+        b = P.plist[b];
+    }
     double* hd = P.ws + (size_t)b * c_arg.ws_stride;
     // flag 2: a final exit short of tol; flag 1: a condensed breakdown handed over to the Riccati
     // rescue — polished first, and handed over only when that does not reach tol
@@ -1330,6 +1336,31 @@ __global__ __launch_bounds__(kPT) void mpc_polish_kernel(const MpcConst c_arg, c
 
 }  // namespace
 
+// The polish launch's compacted agent list: list[0 .. count) = the agents whose rescue image carries flag 1 or 2
+// (ascending), list[batch] = count.  One 1024-thread workgroup: a ballot per wave, the waves' counts summed
+// through LDS, 1024 agents per step.
+__global__ __launch_bounds__(1024) void polish_list_kernel(const double* __restrict__ ws, unsigned long long stride,
+                                                         int batch, int* __restrict__ list) {
+    __shared__ int cnt[16];
+    const int tid = threadIdx.x, wv = tid >> 6, l = tid & 63;
+    int base = 0;
+    for (int b0 = 0; b0 < batch; b0 += 1024) {
+        const int b = b0 + tid;
+        double f = 0.0;
+        if (b < batch) f = ws[(size_t)b * stride];
+        const bool on = f == 1.0 || f == 2.0;
+        const unsigned long long msk = __ballot(on);
+        if (l == 0) cnt[wv] = __popcll(msk);
+        __syncthreads();
+        int off = base;
+        for (int w = 0; w < wv; ++w) off += cnt[w];
+        if (on) list[off + __popcll(msk & ((1ull << l) - 1ull))] = b;
+        for (int w = 0; w < 16; ++w) base += cnt[w];
+        __syncthreads();
+    }
+    if (tid == 0) list[batch] = base;
+}
+
 size_t mpc_polish_lds_bytes(const MpcConst& c) { return sizeof(double) * (size_t)pol_layout(c).total; }
 int mpc_polish_max_active(const MpcConst& c) { return pol_layout(c).amax; }
 
@@ -1346,6 +1377,11 @@ hipError_t mpc_polish_launch(const MpcConst& c, const MpcPtrs& p, int batch, hip
     if (batch == 0) return hipSuccess;
     const size_t lds = mpc_polish_lds_bytes(c);
     if (lds > kMaxLdsBytes) return hipErrorInvalidValue;
+    if (p.plist) {
+        hipLaunchKernelGGL(polish_list_kernel, dim3(1), dim3(1024), 0, s, p.ws, c.ws_stride, batch, p.plist);
+        const hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+    }
     switch (c.nx) {  // the reference's agent (9), the BASELINE double-integrator families (4, 6)
         case 9: return c.nu == 2 ? polish_launch_t<9, 2>(c, p, batch, s, lds) : polish_launch_t<9, 0>(c, p, batch, s, lds);
         case 4: return c.nu == 2 ? polish_launch_t<4, 2>(c, p, batch, s, lds) : polish_launch_t<4, 0>(c, p, batch, s, lds);
