@@ -306,20 +306,33 @@ def sq_profile(kind):
     sys.path.insert(0, os.path.join(ROOT, "tools"))
     from prof_summary import solver_sources_sha
 
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"sq_{kind}_r*.json")))
-    if not files:
-        return None
-    try:
-        with open(files[-1]) as f:
-            rec = json.load(f)
-    except (OSError, ValueError):
+    path, rec = select_profile(glob.glob(os.path.join(ROOT, "profiles", f"sq_{kind}_r*.json")), solver_sources_sha())
+    if rec is None:
         return None
     sha = rec.get("sources_sha")
     out = dict(rec.get("fractions_of_wave_time", {}))
     out.update({"valu_insts_per_wave": rec.get("per_wave", {}).get("valu_insts"),
-                "source": os.path.relpath(files[-1], ROOT), "commit": rec.get("commit"),
+                "source": os.path.relpath(path, ROOT), "commit": rec.get("commit"),
                 "stale": None if sha is None else sha != solver_sources_sha()})
     return out
+
+
+def select_profile(files, sha_now):
+    """The committed counter summary that describes the current kernels: a record whose
+    `sources_sha` equals the current sources' wins; among equals the one taken last (`taken_unix`,
+    written by tools/prof_summary.py since round 6), then the file name.  (The file name alone
+    misorders: a round-5 `sq_cfg5_r05sq.json` sorts after the newer `sq_cfg5_r05am.json`.)"""
+    best, best_key = (None, None), None
+    for path in files:
+        try:
+            with open(path) as f:
+                rec = json.load(f)
+        except (OSError, ValueError):
+            continue
+        key = (rec.get("sources_sha") == sha_now, float(rec.get("taken_unix") or 0.0), os.path.basename(path))
+        if best_key is None or key > best_key:
+            best, best_key = (path, rec), key
+    return best
 
 
 def reference_config(ctx, reps=10, cpu=True):
@@ -468,7 +481,7 @@ def lpv_check_round(bp, R, sample):
              u_prev=R.u_old.cpu().numpy()[sample], qlin=b["qlin"], C=b["C"], h=b["h"])
     finish = bool(bp.opts.flags & 64)   # CMPC_FLAG_FINISH
     polish = bool(bp.opts.flags & 256)  # CMPC_FLAG_POLISH
-    amax = 0
+    amax = None
     if polish:  # the polish kernel's active-set capacity for this shape (both sides polish the same agents)
         from cmpc.solver import plan
 
@@ -574,7 +587,7 @@ def lpv_rounds(ctx, replicas=341, rounds=20, warmup=2, rescue=True, check=True, 
     return out
 
 
-def osqp_dropin(ctx, reps=20):
+def osqp_dropin(ctx, reps=20, cpu=True):
     """The literal reference boundary, osqp_solve_qp(P, q, G, h, A, b) (LPV_Planner.py:192-249),
     timed on the reference-captured N=30 QPs of tests/golden/lpv_n30_a3.npz (3 agents, several
     closed-loop steps): csr matrices in, (res, feasible) out, as PlannerLPV.solve calls it
@@ -608,14 +621,47 @@ def osqp_dropin(ctx, reps=20):
     bat_ms = (time.perf_counter() - t0) / reps * 1e3
     err = max(float(np.abs(r.x - d["z"][j]).max()) for j, (r, _) in enumerate(out))
     berr = max(float(np.abs(r.x - d["z"][j]).max()) for j, (r, _) in enumerate(bat))
-    return {"workload": f"osqp_solve_qp drop-in on the {len(qps)} reference-captured N=30 agent QPs of "
-                        f"lpv_n30_a3 (nx=9 nu=2, n={qps[0][0].shape[0]} vars, "
-                        f"{qps[0][2].shape[0] + qps[0][4].shape[0]} rows, csr in)",
-            "ms_per_call": one_ms, "batch_call_ms": bat_ms, "qps": len(qps),
-            "status_val": sorted({int(r.info.status_val) for r, _ in out}),
-            "max_kkt": max(float(r.info.kkt) for r, _ in out),
-            "max_abs_err_vs_certified_optimum": err, "batch_max_abs_err_vs_certified_optimum": berr,
-            "reps": reps}
+    res = {"workload": f"osqp_solve_qp drop-in on the {len(qps)} reference-captured N=30 agent QPs of "
+                       f"lpv_n30_a3 (nx=9 nu=2, n={qps[0][0].shape[0]} vars, "
+                       f"{qps[0][2].shape[0] + qps[0][4].shape[0]} rows, csr in)",
+           "ms_per_call": one_ms, "batch_call_ms": bat_ms, "qps": len(qps),
+           "status_val": sorted({int(r.info.status_val) for r, _ in out}),
+           "max_kkt": max(float(r.info.kkt) for r, _ in out),
+           "max_abs_err_vs_certified_optimum": err, "batch_max_abs_err_vs_certified_optimum": berr,
+           "reps": reps}
+    if cpu:
+        res["cpu"] = osqp_dropin_cpu(qps, d["z"])
+    return res
+
+
+def osqp_dropin_cpu(qps, z_cert, reps=3):
+    """The CPU figure beside the literal boundary: each of the same QPs, recognised into the structured
+    form the GPU path solves (cmpc.structure.recognize), solved by the C restatement of the same
+    policy (oracle/cmpc_oracle.c: the condensed IPM, rescue hand-over and polish; solve_batch_rescue) on
+    ONE thread, one QP after another as PlannerLPV.solve calls osqp_solve_qp; per-QP wall time, best of
+    `reps` (the recognition is the GPU call's too and is not timed here)."""
+    from cmpc import structure as St
+    from cmpc.solver import plan
+    from oracle import cmpc_oracle as CO
+
+    ms, errs, st = [], [], []
+    for j, qp in enumerate(qps):
+        P = St.recognize(*qp[:6])
+        amax = plan(P, 1, rescue=True, polish=True)["polish_max_active"]
+        best = np.inf
+        for _ in range(reps):
+            t0 = time.perf_counter()
+            zc, _, _, sc = CO.solve_batch_rescue(P, nthreads=1, polish=True, polish_amax=amax)
+            best = min(best, time.perf_counter() - t0)
+        ms.append(best * 1e3)
+        st.append(int(sc[0]))
+        errs.append(float(np.abs(zc[0] - z_cert[j]).max()))
+    model_name, nproc, _ = host_cpu()
+    return {"kind": "port", "cores": 1, "cpu_model": model_name, "nproc": nproc,
+            "ms_per_call_mean": float(np.mean(ms)), "ms_per_call_max": float(np.max(ms)), "status": sorted(set(st)),
+            "max_abs_err_vs_certified_optimum": max(errs),
+            "sample": "the same QPs in structured form, the C restatement (rescue + polish policy) on one thread, "
+                      "best of 3 per QP"}
 
 
 def fp32_vs_fp64(R):
@@ -654,17 +700,13 @@ def pmc_traffic(kind=None):
     sys.path.insert(0, os.path.join(ROOT, "tools"))
     from prof_summary import solver_sources_sha
 
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"pmc_{kind}_r*.json" if kind else "pmc_r*.json")))
-    if not files:
+    path, rec = select_profile(glob.glob(os.path.join(ROOT, "profiles", f"pmc_{kind}_r*.json" if kind else "pmc_r*.json")),
+                               solver_sources_sha())
+    if rec is None:
         return None, None
-    try:
-        with open(files[-1]) as f:
-            rec = json.load(f)
-        traffic = rec.get("solve_kernel", {}).get("hbm_bytes_per_launch")
-    except (OSError, ValueError):
-        return None, None
+    traffic = rec.get("solve_kernel", {}).get("hbm_bytes_per_launch")
     sha = rec.get("sources_sha")
-    return traffic, {"file": os.path.relpath(files[-1], ROOT), "commit": rec.get("commit"),
+    return traffic, {"file": os.path.relpath(path, ROOT), "commit": rec.get("commit"),
                      "stale": None if sha is None else sha != solver_sources_sha()}
 
 

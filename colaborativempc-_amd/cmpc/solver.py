@@ -57,14 +57,14 @@ def _flags(fp32=False, riccati=False, generic=False, rescue=False, lane=False, p
         (L.CMPC_FLAG_LANE if lane else 0) | (L.CMPC_FLAG_POLISH if polish else 0)
 
 
-def plan(shared, batch=1, fp32=False, riccati=False, generic=False, lane=False, rescue=False, polish=False):
+def plan(shared, batch=1, fp32=False, riccati=False, generic=False, lane=False, rescue=False, polish=False, flags=0):
     """Which solver cmpc_solve_mpc_batch would run for this problem shape, and its occupancy
     (cmpc_plan_mpc, host only): dict(solver=name, lds_bytes, wg_per_cu, agents_per_wg, waves_per_agent,
     polish_lds_bytes, polish_max_active) — the last two describe the rescue policy's polish launch (0 without
-    ``rescue`` and ``polish``)."""
+    ``rescue`` and ``polish``).  ``flags``: further CMPC_FLAG_* bits."""
     w, keep = _weights(shared)
     d = _dims(shared, batch)
-    o = L.opts(None, None, _flags(fp32, riccati, generic, rescue, lane, polish))
+    o = L.opts(None, None, _flags(fp32, riccati, generic, rescue, lane, polish) | int(flags))
     info = L.cmpc_plan_info()
     rc = L.load().cmpc_plan_mpc(ct.byref(d), ct.byref(w), ct.byref(o), ct.byref(info))
     if rc != L.CMPC_OK:

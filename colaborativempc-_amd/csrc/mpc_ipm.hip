@@ -777,6 +777,10 @@ int mpc_prepare(const cmpc_mpc_dims* d, const cmpc_mpc_weights* wt, const cmpc_o
                  mpc_riccati_lds_bytes(*c) <= kMaxLdsBytes)
                     ? 1 : 0;
     c->finish = (c->rescue && (o->flags & CMPC_FLAG_FINISH)) ? 1 : 0;
+    if (o && (o->flags & CMPC_FLAG_TWO_WAVES) && (o->flags & CMPC_FLAG_ONE_WAVE)) {
+        *msg = "CMPC_FLAG_ONE_WAVE and CMPC_FLAG_TWO_WAVES are exclusive";
+        return CMPC_ERR_ARG;
+    }
     c->waves = (o && (o->flags & CMPC_FLAG_TWO_WAVES)) ? 2 : ((o && (o->flags & CMPC_FLAG_ONE_WAVE)) ? 1 : 0);
     c->polish = 0;
     // (mpc_polish.hip: one lane per condensed variable in its H build, so n <= 64 — every condensed

@@ -805,9 +805,10 @@ __global__ __launch_bounds__(kPT) void mpc_polish_kernel(const MpcConst c_arg, c
         }
     }
     __syncthreads();
-    // diagnostic section clocks (MpcPtrs::stamps slots 9..15, thread 0): init, H build, H factor,
+    // diagnostic section clocks (MpcPtrs::stamps slots 8..14, thread 0): init, H build, H factor,
     // G_A rows, Y, S build + factor + the Newton steps' linear algebra, the residual sweeps (simulation,
-    // adjoints, reductions) of the Newton steps and evaluations; slot 8: Newton steps run
+    // adjoints, reductions) of the Newton steps and evaluations; slot 4 bits 1..: Newton steps run
+    // (slot 15 stays the solver's iteration count, kStampSlots - 1)
     unsigned long long tsum[7] = {0, 0, 0, 0, 0, 0, 0}, t_a = P.stamps ? clock64_() : 0;
 #define PSTAMP(slot)                         \
     if (P.stamps && tid == 0) {              \
@@ -1282,22 +1283,21 @@ __global__ __launch_bounds__(kPT) void mpc_polish_kernel(const MpcConst c_arg, c
         __syncthreads();
     }
     __syncthreads();
-    // diagnostics (MpcPtrs::stamps, tools/polish_diag.py): [passes run, |A| of the last, polished merit,
-    // the method's best merit, H factored]
+    // diagnostics (MpcPtrs::stamps, tools/polish_diag.py, tools/polish_stamps.py): [passes run, |A| of the
+    // last, polished merit, the method's best merit, H factored | Newton steps << 1, three reductions, the
+    // section clocks]; slot 15 (the solver's iteration count) is left alone
     if (P.stamps && tid == 0) {
         unsigned long long* st = P.stamps + (size_t)b * kStampSlots;
         st[0] = (unsigned long long)passes;
         st[1] = (unsigned long long)nA_s;
         st[2] = (unsigned long long)__double_as_longlong(best);
         st[3] = (unsigned long long)__double_as_longlong(best_m);
-        st[4] = h_ok ? 1ull : 0ull;
+        st[4] = (h_ok ? 1ull : 0ull) | ((unsigned long long)nsteps << 1);
         for (int i = 0; i < 3; ++i) st[5 + i] = (unsigned long long)__double_as_longlong(sm[L.red + 8 + i]);
 #ifdef CMPC_POL_LAB
-        st[8] = lab_fwd;
-#else
-        st[8] = (unsigned long long)nsteps;
+        st[7] = lab_fwd;
 #endif
-        for (int i = 0; i < 7; ++i) st[9 + i] = tsum[i];
+        for (int i = 0; i < 7; ++i) st[8 + i] = tsum[i];
     }
     // kept only when it beats the method's best AND lands at the rounding floor at least (stop_status's
     // 1e3 tol): below tol it is solved (1), below the floor solved-inaccurate (2).  A polish of a solve

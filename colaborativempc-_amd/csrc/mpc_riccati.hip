@@ -1781,6 +1781,16 @@ __global__ __launch_bounds__(kWave) void mpc_riccati_kernel(const MpcConst c_arg
 #define RCOUNT(slot) \
     if (stamp && l == 0) tsum[slot] += 1;
 
+    // Cfg::F32: an fp32-mode solve that ends short of tol restarts cold in fp64 (no fp32 stage) at
+    // tol * 1e-3, so that its rounding floor is the requested tol: on 4 rounds of 8192 BASELINE cfg5
+    // agents 2 solves ended at status 2 with KKT 4e-6 / 7e-6 (a dual residual the fp32 phase left,
+    // then a breakdown at th ~ 1e25); restarted, all 32768 solve with KKT <= 1e-6 (tools/f32_lab.py,
+    // oracle RIC_F32).  `tol` is the attempt's tolerance, it_done the iterations of the first attempt.
+    double tol = c.tol;
+    int it_done = 0;
+    double best_m, best_kkt, kkt;
+    int best_it, stop, it;
+    for (int attempt = 0;; ++attempt) {
     // ---- row right-hand sides; inactive rows carry w = +inf ----
     for (int r = l; r < m; r += kWave) {
         double v;
@@ -1819,9 +1829,11 @@ __global__ __launch_bounds__(kWave) void mpc_riccati_kernel(const MpcConst c_arg
     rsync();  // lam: read across lanes by the residuals
     if (warm && l == 0) hand[0] = 0.0;  // (every lane has read the flag: `warm` steered the loop above)
 
-    double best_m = INFINITY, best_kkt = INFINITY;
-    int best_it = 0, stop = kStopMaxIter, it;
-    double kkt = INFINITY;
+    best_m = INFINITY;
+    best_kkt = INFINITY;
+    best_it = 0;
+    stop = kStopMaxIter;
+    kkt = INFINITY;
     RSTAMP(14);
     double alpha_prev = 1;  // step of the previous iteration (kShortStep guard)
     for (it = it0 + 1; it <= c.max_iter; ++it) {
@@ -1922,11 +1934,11 @@ __global__ __launch_bounds__(kWave) void mpc_riccati_kernel(const MpcConst c_arg
             for (int i = l; i < n; i += kWave) bU[i] = U[i];
             for (int i = l; i < N * ns; i += kWave) bsig[i] = sig[i];
         }
-        if (merit < c.tol) {
+        if (merit < tol) {
             stop = kStopConverged;
             break;
         }
-        if (best_m < 1e3 * c.tol && it - best_it >= kStallIters) {
+        if (best_m < 1e3 * tol && it - best_it >= kStallIters) {
             stop = kStopStalled;
             break;
         }
@@ -2252,12 +2264,25 @@ __global__ __launch_bounds__(kWave) void mpc_riccati_kernel(const MpcConst c_arg
     }
     if (it > c.max_iter) it = c.max_iter;
     wsync();
+    if constexpr (G::F32) {
+        if (attempt == 0 && !warm && stop != kStopConverged) {  // the fp64 restart (above)
+            it_done = it;
+            f32_on = dd_on = false;
+            tol = c.tol * 1e-3;
+            for (int i = l; i < n; i += kWave) U[i] = 0.0;
+            for (int i = l; i < N * ns; i += kWave) sig[i] = 0.0;
+            wsync();
+            continue;
+        }
+    }
+    break;
+    }
     int status = CMPC_SOLVED;
     // polish (CMPC_FLAG_POLISH): a rescue-pass solve that stops short of tol for the last time — status 2 or
     // -2, or anything on the second (cold) pass, rescue == 2 — leaves its last iterate in the rescue image
     // with flag 2 and its best merit (mpc_polish.hip)
     const bool pol = c_arg.rescue && c.polish && stop != kStopConverged && stop != kStopNonFinite &&
-                     (best_m < 1e3 * c.tol || stop == kStopMaxIter || c_arg.rescue == 2);
+                     (best_m < 1e3 * tol || stop == kStopMaxIter || c_arg.rescue == 2);
     if (pol) {
         const int ht = (int)hand_t(c);
         for (int i = l; i < n; i += kWave) hand[2 + i] = U[i];
@@ -2277,7 +2302,8 @@ __global__ __launch_bounds__(kWave) void mpc_riccati_kernel(const MpcConst c_arg
             for (int i = l; i < N * ns; i += kWave) sig[i] = bsig[i];
             kkt = best_kkt;
         }
-        status = stop_status(stop, best_m, c.tol);
+        // (an fp64 restart that ends with its best merit below the requested tol has met it)
+        status = (it_done && best_m < c.tol) ? CMPC_SOLVED : stop_status(stop, best_m, c.tol);
     }
     wsync();
 
@@ -2297,13 +2323,14 @@ __global__ __launch_bounds__(kWave) void mpc_riccati_kernel(const MpcConst c_arg
     }
     if (l == 0) {
         if (P.kkt) P.kkt[b] = kkt;
-        if (P.iters) P.iters[b] = it;
+        if (P.iters) P.iters[b] = it_done + it;
         if (P.status) P.status[b] = status;
     }
     RSTAMP(14);
     if (stamp) {
         wsync();
-        if (l < kStampSlots) P.stamps[(size_t)b * kStampSlots + l] = (l == kStampSlots - 1) ? (unsigned long long)it : tsum[l];
+        if (l < kStampSlots)
+            P.stamps[(size_t)b * kStampSlots + l] = (l == kStampSlots - 1) ? (unsigned long long)(it_done + it) : tsum[l];
     }
 #undef RSTAMP
 #undef RCOUNT

@@ -97,7 +97,10 @@ typedef struct cmpc_ctx cmpc_ctx;
                                    agent (the default) */
 #define CMPC_FLAG_TWO_WAVES 1024 /* ... two wavefronts per agent (a 128-lane workgroup: split K build, the
                                    predictor's right-hand side on the second wave); bit-identical results, no
-                                   faster at 512 agents on one MI355X, so opt-in */
+                                   faster at 512 agents on one MI355X, so opt-in.  Applies to the
+                                   fused double-integrator round only (cmpc_di_solve_dev, the DS instantiation);
+                                   other solves run one wavefront per agent.  Setting both wave flags is
+                                   CMPC_ERR_ARG */
 #define CMPC_FLAG_ALL (CMPC_FLAG_GENERIC | CMPC_FLAG_FP32 | CMPC_FLAG_RICCATI | CMPC_FLAG_RESCUE | CMPC_FLAG_FINISH | \
                        CMPC_FLAG_LANE | CMPC_FLAG_POLISH | CMPC_FLAG_ONE_WAVE | CMPC_FLAG_TWO_WAVES)
                        /* other bits: CMPC_ERR_ARG */

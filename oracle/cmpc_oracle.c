@@ -1444,9 +1444,39 @@ done:
     return best;
 }
 
+#ifdef RIC_F32
+/* lab: the fp64 restart of an fp32-mode solve that ends short of tol (Cfg::F32 of mpc_riccati.hip):
+   f32_no = 1 while it runs (no fp32 stage), at tol * 1e-3 so that its rounding floor is the requested
+   tol; an end with the best merit below the requested tol (f32_req) counts as solved */
+static _Thread_local int f32_no = 0;
+static _Thread_local double f32_req = 0.0;
+long cmpc_f32_restarts = 0;
+#endif
+static int solve_one_base(const shared_t* S, const agent_t* a, double tol, int max_iter, work_t* wk,
+                          double* z, double* kkt_out, int* iters_out);
+
 /* Solve one agent.  Returns OSQP-style status: 1 solved, 2 solved inaccurate, -2 max_iter, -10 unsolved. */
 static int solve_one(const shared_t* S, const agent_t* a, double tol, int max_iter, work_t* wk,
                      double* z, double* kkt_out, int* iters_out) {
+    int st = solve_one_base(S, a, tol, max_iter, wk, z, kkt_out, iters_out);
+#ifdef RIC_F32
+    if (S->newton == 3 && st != 1) {
+        const int it1 = *iters_out;
+#pragma omp atomic
+        cmpc_f32_restarts += 1;
+        f32_no = 1;
+        f32_req = tol;
+        st = solve_one_base(S, a, tol * 1e-3, max_iter, wk, z, kkt_out, iters_out);
+        f32_no = 0;
+        f32_req = 0.0;
+        *iters_out += it1;
+    }
+#endif
+    return st;
+}
+
+static int solve_one_base(const shared_t* S, const agent_t* a, double tol, int max_iter, work_t* wk,
+                          double* z, double* kkt_out, int* iters_out) {
     /* newton 4: the product's CMPC_FLAG_RESCUE policy — the condensed method; at a factorisation
        breakdown the solve continues from that iterate with the Riccati double-double Newton solve
        (newton 3), its best-iterate bookkeeping restarted (the kernels hand the iterate from
@@ -1576,7 +1606,7 @@ static int solve_one(const shared_t* S, const agent_t* a, double tol, int max_it
     double kkt = INFINITY;
     double alpha_prev = 1.0; /* step of the previous iteration (kShortStep rule) */
 #ifdef RIC_F32
-    int f32_on = 1;          /* lab: this agent still factors in fp32 */
+    int f32_on = !f32_no;    /* lab: this agent still factors in fp32 */
 #endif
 #ifndef DD_STALL
 #define DD_STALL 2           /* kDdStall of mpc_riccati.hip */
@@ -2320,6 +2350,9 @@ static int solve_one(const shared_t* S, const agent_t* a, double tol, int max_it
             kkt = best_kkt;
         }
         status = best_m < 1e3 * tol ? 2 : (stop == 0 ? -2 : -10);
+#ifdef RIC_F32
+        if (f32_no) status = best_m < f32_req ? 1 : (best_m < 1e3 * f32_req ? 2 : status);
+#endif
 #ifdef LAB_STOPDUMP
         fprintf(stderr, "STOP status %d stop %d newton %d it %d best_it %d best_m %.2e\n", status, stop, S->newton, it,
                 best_it, best_m);

@@ -51,15 +51,20 @@ def nz_of(p):
     return (p["nx"] + p["ns"]) * (p["N"] + 1) + 2 * p["nu"] * p["N"]
 
 
-def solve_batch_rescue(p, tol=1e-9, max_iter=60, nthreads=0, finish=False, polish=False, polish_amax=0):
+def solve_batch_rescue(p, tol=1e-9, max_iter=60, nthreads=0, finish=False, polish=False, polish_amax=None):
     """The product's CMPC_FLAG_RESCUE policy restated: the condensed method; an agent whose
     factorisation breaks down short of the rounding floor (best merit >= 1e3 tol; with ``finish``,
     CMPC_FLAG_FINISH, every breakdown) continues from that iterate with the Riccati method in the
     kernel's double-double mode, its best-iterate bookkeeping restarted (newton 5 / 4, the kernels'
     hand-over); an agent that still ends CMPC_UNSOLVED is re-solved by that Riccati method from a
     cold start (newton 3, the second rescue pass).  ``polish_amax``: the polish kernel's active-set
-    capacity for this shape (cmpc.solver.plan(..., rescue=True, polish=True)["polish_max_active"]; 0:
-    kPolishMaxActive = 96), so both sides polish the same agents."""
+    capacity for this shape (cmpc.solver.plan(..., rescue=True, polish=True)["polish_max_active"]), so
+    both sides polish the same agents.  Required with ``polish``: the kernel lowers its capacity to fit
+    LDS (88 for the reference agent at N = 30), and a default would polish different agents than the
+    GPU without notice."""
+    if polish and not polish_amax:
+        raise ValueError("solve_batch_rescue(polish=True) needs polish_amax: the GPU layout's capacity "
+                         "(cmpc.solver.plan(P, 1, rescue=True, polish=True)['polish_max_active'])")
     pol = (0x100 | (int(polish_amax) & 0xff) << 16) if polish else 0
     z, kkt, it, st = solve_batch(p, tol, max_iter, nthreads, newton=(4 if finish else 5) | pol)
     bad = np.flatnonzero(st == -10)

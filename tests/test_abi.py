@@ -57,6 +57,10 @@ def test_plan_occupancy_of_the_bench_configs():
     # CMPC_FLAG_POLISH (with CMPC_FLAG_RESCUE) is a known option bit: the condensed plan is unchanged
     pp = plan(S.di_shared(2, 30, 2), 1024, rescue=True, polish=True)
     assert pp["solver"] == "condensed_v3" and pp["wg_per_cu"] == 4, pp
+    # the two wave-count flags are exclusive; a structured batch runs one wave per agent
+    with pytest.raises(cmpc.CmpcError):
+        plan(S.di_shared(2, 30, 2), 512, flags=L.CMPC_FLAG_ONE_WAVE | L.CMPC_FLAG_TWO_WAVES)
+    assert plan(S.di_shared(2, 30, 2), 512, flags=L.CMPC_FLAG_TWO_WAVES)["waves_per_agent"] == 1
 
 
 def test_no_cpu_fallback_without_device():

@@ -95,7 +95,17 @@ def main():
     ap.add_argument("--rounds", type=int, default=1)
     ap.add_argument("variants", nargs="+")
     a = ap.parse_args()
-    pops = population(a.agents, a.rounds)
+    import pickle  # (a cache of this script's own populations, under /tmp)
+
+    cache = os.path.join(OUT, f"pop_{a.agents}_{a.rounds}.pkl")
+    if os.path.exists(cache):
+        with open(cache, "rb") as f:
+            pops = pickle.load(f)
+    else:
+        pops = population(a.agents, a.rounds)
+        os.makedirs(OUT, exist_ok=True)
+        with open(cache, "wb") as f:
+            pickle.dump(pops, f)
     for v in a.variants:
         name, newton, tol, *flags = v.split(":")
         refine = 0
@@ -107,14 +117,15 @@ def main():
                 fl.append(f)
         f32 = name == "f32"
         lib = build(fl, f32)
-        sts, its, errs = [], [], []
+        sts, its, errs, kks = [], [], [], []
         for P, zr, str_ in pops:
             z, kkt, it, st = solve(lib, P, f32, float(tol), int(newton), refine)
+            kks.append(kkt)
             err = np.abs(z - zr) / np.maximum(1.0, np.abs(zr))
             sts.append(st)
             its.append(it)
             errs.append(err.max(axis=1))
-        st, it, err = np.concatenate(sts), np.concatenate(its), np.concatenate(errs)
+        st, it, err, kk = np.concatenate(sts), np.concatenate(its), np.concatenate(errs), np.concatenate(kks)
         u, c = np.unique(st, return_counts=True)
         ok = st == 1
         e1 = err[ok].max() if ok.any() else np.nan
@@ -124,6 +135,7 @@ def main():
             f64i = ct.c_long.in_dll(lib, "cmpc_f64_iters").value
             f64a = ct.c_long.in_dll(lib, "cmpc_f64_agents").value
             cnt = f" | fp32 iters {f32i} fp64 iters {f64i} switched agents {f64a}"
+            cnt += f" restarts {ct.c_long.in_dll(lib, 'cmpc_f32_restarts').value}"
         except ValueError:
             pass
         try:
@@ -132,7 +144,9 @@ def main():
             pass
         print(f"{v}: status {dict(zip(u.tolist(), c.tolist()))} solved {np.mean(st == 1):.4f} iters mean {it.mean():.1f} "
               f"max {it.max()} | rel err max {err.max():.2e} p99 {np.quantile(err, 0.99):.2e} "
-              f"median {np.median(err):.2e} | solved-only max {e1:.2e}{cnt}", flush=True)
+              f"median {np.median(err):.2e} | solved-only max {e1:.2e}{cnt} | max kkt {kk.max():.2e} "
+              f"status-2 kkt {np.sort(kk[st == 2])[::-1][:8].tolist()} (agents {np.nonzero(st == 2)[0].tolist()[:8]})",
+              flush=True)
 
 
 if __name__ == "__main__":

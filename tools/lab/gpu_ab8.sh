@@ -1,5 +1,5 @@
 # A/B of the in-tree library against tools/v3lab/libcmpc_prev.so: cfg3 kernel time and bit equality
-# (v3_ab), the reference-model rounds (lpv_ab); usage: bash tools/gpu_ab8.sh TAG
+# (v3_ab), the reference-model rounds (lpv_ab); usage: bash tools/lab/gpu_ab8.sh TAG
 set -o pipefail
 O=gpurun_out/${1:-ab8}
 mkdir -p $O

@@ -1,4 +1,4 @@
-# usage: bash tools/gpu_prof4.sh TAG — round-4 evidence: SQ counter passes (tools/pmc_sq.sh), PMC traffic passes
+# usage: bash tools/lab/gpu_prof4.sh TAG — round-4 evidence: SQ counter passes (tools/pmc_sq.sh), PMC traffic passes
 # (FETCH_SIZE / WRITE_SIZE) and rocprofv3 kernel-trace stats of the bench commands (cfg3 default, cfg5, cfg5 fp32).
 set -o pipefail
 TAG=${1:-r4}

@@ -1,4 +1,4 @@
-# usage: bash tools/gpu_prof_lane.sh TAG — PMC passes (instruction mix, waits, instruction cache) of the lane kernel
+# usage: bash tools/lab/gpu_prof_lane.sh TAG — PMC passes (instruction mix, waits, instruction cache) of the lane kernel
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 O=gpurun_out/${1:-lanepmc}

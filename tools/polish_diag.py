@@ -21,6 +21,7 @@ def main():
     import bench
     from cmpc import _lib as L
     from cmpc.rounds import LPVRounds
+    from cmpc.solver import plan
     from oracle import cmpc_oracle as CO
 
     out, rounds = sys.argv[1], int(sys.argv[2]) if len(sys.argv) > 2 else 22
@@ -47,7 +48,8 @@ def main():
                      row_slack=np.array([-1, 0, 1, 1] + [2] * R.nb), row_sign=np.array([1, 1, 1, 1] + [-1] * R.nb),
                      A=b["A"], B=b["B"], x0=R.x0.cpu().numpy()[sel], u_prev=R.u_old.cpu().numpy()[sel],
                      qlin=b["qlin"], C=b["C"], h=b["h"])
-            zc, kc, ic, sc = CO.solve_batch_rescue(P, nthreads=16, polish=True)
+            amax = plan(P, 1, rescue=True, polish=True)["polish_max_active"]  # the GPU layout's capacity
+            zc, kc, ic, sc = CO.solve_batch_rescue(P, nthreads=16, polish=True, polish_amax=amax)
             zg, sg, kg = R.z.cpu().numpy()[sel], st[sel], R.kkt.cpu().numpy()[sel]
             err = np.abs(zg - zc).max(1)
             pick = (sg == 2) | (sg == -10) | ((sg == 1) & (sc == 1) & (err > 1e-7))

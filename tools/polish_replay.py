@@ -34,8 +34,8 @@ def main():
     f = lambda i, j: float(s[i, j:j + 1].view(np.float64)[0])  # noqa: E731
     for i in range(len(sel)):
         print(i, "iters", int(it[i]), "passes", int(s[i, 0]), "nA", int(s[i, 1]), "pol merit %.3e" % f(i, 2),
-              "best_m %.3e" % f(i, 3), "h_ok", int(s[i, 4]), "res d/s/p %.2e %.2e %.2e" % (f(i, 5), f(i, 6), f(i, 7)),
-              "clk init/H/chol H/Y/S/newton %s" % s[i, 9:15].tolist())
+              "best_m %.3e" % f(i, 3), "h_ok", int(s[i, 4]) & 1, "newton steps", int(s[i, 4]) >> 1, "res d/s/p %.2e %.2e %.2e" % (f(i, 5), f(i, 6), f(i, 7)),
+              "clk init/H/chol H/G_A/Y/S/sweeps %s" % s[i, 8:15].tolist())
 
 
 if __name__ == "__main__":

@@ -1,8 +1,8 @@
 """Diagnostic (GPU): per-section clocks of the polish kernel (mpc_polish.hip) on one round of bench.py's
 lpv_rounds population.  The round's structured problems (the GPU builder's arrays read back) are re-solved
 through the host-array path with rescue + polish and a stamps buffer; the polish kernel writes its section
-clocks (slots 9..15: init, H build, H factor, G_A rows, Y, S build + factor + Newton linear algebra,
-residual sweeps) for the agents it polished (slots 0 / 1 / 8: passes / |A| / Newton steps; the v3 kernel's own clocks
+clocks (slots 8..14: init, H build, H factor, G_A rows, Y, S build + factor + Newton linear algebra,
+residual sweeps) for the agents it polished (slots 0 / 1 / 4 >> 1: passes / |A| / Newton steps; the v3 kernel's own clocks
 stay in the others' slots).
 
   python tools/polish_stamps.py [round] [reps]
@@ -42,13 +42,13 @@ def main():
         pol = (s[:, 0] >= 1) & (s[:, 0] <= 2) & (s[:, 1] < 1000)
         print(f"rep {rep}: {int(pol.sum())} polished agents of {R.B}; status {dict(zip(*np.unique(status, return_counts=True)))}")
         if pol.any():
-            sec = s[pol][:, 9:16].astype(np.float64)
+            sec = s[pol][:, 8:15].astype(np.float64)
             print("   |A| mean %.1f max %d, passes mean %.2f, Newton steps mean %.2f max %d" % (
-                s[pol, 1].mean(), s[pol, 1].max(), s[pol, 0].mean(), s[pol, 8].mean(), s[pol, 8].max()))
+                s[pol, 1].mean(), s[pol, 1].max(), s[pol, 0].mean(), (s[pol, 4] >> 1).mean(), (s[pol, 4] >> 1).max()))
             for j, nm in enumerate(names):
                 print(f"   {nm:16s} mean {sec[:, j].mean() / 1e3:8.1f} k clk   max {sec[:, j].max() / 1e3:8.1f} k")
-            if os.environ.get("CMPC_LIB_PATH"):  # lab builds (-DCMPC_POL_LAB): a lab figure in slot 8
-                print(f"   slot 8 (lab)     mean {s[pol, 8].mean() / 1e3:8.1f} k clk   max {s[pol, 8].max() / 1e3:8.1f} k")
+            if os.environ.get("CMPC_LIB_PATH"):  # lab builds (-DCMPC_POL_LAB): a lab figure in slot 7
+                print(f"   slot 7 (lab)     mean {s[pol, 7].mean() / 1e3:8.1f} k clk   max {s[pol, 7].max() / 1e3:8.1f} k")
             tot = sec.sum(1)
             print(f"   total            mean {tot.mean() / 1e3:8.1f} k clk   max {tot.max() / 1e3:8.1f} k")
 

@@ -18,6 +18,7 @@ import hashlib
 import json
 import os
 import sys
+import time
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
@@ -79,7 +80,7 @@ def pmc(fetch_csv, write_csv, out, commit=None):
                             "fetch_kB_raw": fk, "write_kB_raw": wk,
                             "note": "FETCH_SIZE x2 (gfx950 half-count of wide reads); first dispatch skipped",
                             "kernel_filter": SOLVER},
-           "commit": commit, "sources_sha": solver_sources_sha()}
+           "commit": commit, "sources_sha": solver_sources_sha(), "taken_unix": time.time()}
     json.dump(res, open(out, "w"), indent=1)
     print(json.dumps(res))
 
@@ -110,7 +111,8 @@ def sq(out, commit, *csvs):
     mean = {k: (sum(v[1:]) / len(v[1:]) if len(v) > 1 else v[0]) for k, v in per.items() if v}
     g = mean.get
     wc = g("SQ_WAVE_CYCLES")
-    res = {"counters_per_launch": mean, "kernel_filter": SOLVER, "commit": commit, "sources_sha": solver_sources_sha()}
+    res = {"counters_per_launch": mean, "kernel_filter": SOLVER, "commit": commit, "sources_sha": solver_sources_sha(),
+           "taken_unix": time.time()}
     if wc:
         res["fractions_of_wave_time"] = {
             "active_inst_any": g("SQ_ACTIVE_INST_ANY", 0.0) / wc,
