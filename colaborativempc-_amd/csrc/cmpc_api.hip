@@ -260,7 +260,7 @@ int cmpc_plan_mpc(const cmpc_mpc_dims* dims, const cmpc_mpc_weights* w, const cm
     out->lds_bytes = (int)lds;
     const size_t wg = lds ? cmpc::kMaxLdsBytes / lds : 4;
     out->wg_per_cu = (int)(wg < 4 ? wg : 4);
-    out->waves_per_agent = 1;
+    out->waves_per_agent = (c.riccati && !c.lane && cmpc::mpc_riccati_mw(c)) ? 4 : 1;  // (the Riccati latency mode)
     out->polish_lds_bytes = c.polish ? (int)cmpc::mpc_polish_lds_bytes(c) : 0;
     out->polish_max_active = c.polish ? cmpc::mpc_polish_max_active(c) : 0;
     return CMPC_OK;

@@ -181,6 +181,7 @@ hipError_t mpc_polish_launch(const MpcConst& c, const MpcPtrs& p, int batch, hip
 // Stage-wise Riccati kernel (mpc_riccati.hip): any horizon whose per-agent rows fit LDS.
 size_t mpc_riccati_lds_bytes(const MpcConst& c);
 bool mpc_riccati_f32_supported(const MpcConst& c);  // Cfg::F32 instantiations (BASELINE cfg5 dimensions)
+bool mpc_riccati_mw(const MpcConst& c);             // the Riccati latency mode (four wavefronts per agent) applies
 size_t mpc_riccati_ws_doubles(const MpcConst& c);
 hipError_t mpc_riccati_launch(const MpcConst& c, const MpcPtrs& p, int batch, hipStream_t s);
 // Lane-per-agent stage-wise kernel (mpc_lane.hip): the dimension sets it is instantiated for.

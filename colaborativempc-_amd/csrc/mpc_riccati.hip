@@ -74,6 +74,10 @@ constexpr double kRefineTol = 1e-13;  // ... until |correction| <= kRefineTol |d
                                       // the steps on the captured LPV QPs by 39% (752 -> 456) with the
                                       // same iterates to 1e-13 (tools/ipm_lab.py, oracle REF_TOL)
 
+// The lane of this thread in its wavefront: the sweep helpers below are wave-level code, run by the one
+// wave of mpc_riccati_kernel or by one of the waves of the latency mode (mpc_riccati_mw_kernel)
+__device__ __forceinline__ int lane_id() { return (int)(threadIdx.x & (kWave - 1)); }
+
 struct RLds {
     int t, lam, th, rp, rho, rt, w, GdU;  // per row
     int X, dX, yb, yb2, psi;              // per stage state (yb | yb2: the dd states of kres_dd)
@@ -83,6 +87,7 @@ struct RLds {
     int Pd, PAd, PBd, Hd, Hyd, Kd, psid;  // double-double working set
     int stamps;                           // diagnostic clock sums (kStampSlots u64)
     int cst;                              // copy of MpcConst (weights read from LDS)
+    int sb2, red, ring;                   // latency mode only: wave 1's stage slots, block reductions, gains ring
     int total;
 };
 
@@ -202,6 +207,7 @@ __host__ __device__ inline RLds r_layout_ex(const MpcConst& c, bool gr) {
     // image 41.3 KB, over the 40 KB that lets four waves share a CU (three did: a quarter of the
     // SIMDs idle); without Q's unused tail it is 40.4 KB
     L.cst = take(mpc_const_used_doubles(c));
+    L.sb2 = L.red = L.ring = 0;
     L.total = o;
     return L;
 }
@@ -270,7 +276,7 @@ struct StageSrc {
 // the counter before every use)
 template <int KP>
 __device__ __forceinline__ void stage_fetch(const StageSrc& s, int k, int cnt, double (&r)[KP]) {
-    const int l = threadIdx.x;
+    const int l = lane_id();
     const int kf = k - s.lag > 0 ? k - s.lag : 0;
 #pragma unroll
     for (int q = 0; q < KP; ++q) {
@@ -285,7 +291,7 @@ __device__ __forceinline__ void stage_fetch(const StageSrc& s, int k, int cnt, d
 
 template <int KP>
 __device__ __forceinline__ void stage_put(double* buf, int cnt, const double (&r)[KP]) {
-    const int l = threadIdx.x;
+    const int l = lane_id();
 #pragma unroll
     for (int q = 0; q < KP; ++q) {
         const int e = l + q * kWave;
@@ -314,7 +320,7 @@ struct Pipe {
         : src(s_), cnt(cnt_), N(N_), S(S_), back(back_), sb(sb_) {
 #pragma unroll
         for (int q = 0; q < KP; ++q) {
-            int e = (int)threadIdx.x + q * kWave;
+            int e = lane_id() + q * kWave;
             e = e < cnt ? e : cnt - 1;
             const bool ia = e < src.sA, ib = !ia && e < src.sA + src.sB;
             pb[q] = ia ? src.A + e : (ib ? src.B + (e - src.sA) : src.F + (e - src.sA - src.sB));
@@ -430,7 +436,7 @@ __device__ __forceinline__ double m_entry(const MpcConst& c, const double* __res
 template <class G>
 __device__ __forceinline__ void fwd_sim(const MpcConst& c, const Dims& d, const StageSrc& src, double* sb,
                         const double* __restrict__ x0, const double* U, double* X) {
-    const int l = threadIdx.x, nx = d.nx, nu = d.nu, N = c.N;
+    const int l = lane_id(), nx = d.nx, nu = d.nu, N = c.N;
     Pipe<G::KP> pp(src, d.sAB, N, d.Sl, false, sb);
     pp.prime();
     if (l < nx) X[l] = x0 ? x0[l] : 0.0;
@@ -471,7 +477,7 @@ __device__ __forceinline__ void fwd_sim(const MpcConst& c, const Dims& d, const 
 template <class G>
 __device__ __forceinline__ void adjoint(const MpcConst& c, const Dims& d, const StageSrc& src, double* sb, const double* yb,
                         double* out, double* psi2) {
-    const int l = threadIdx.x, nx = d.nx, nu = d.nu, N = c.N;
+    const int l = lane_id(), nx = d.nx, nu = d.nu, N = c.N;
     Pipe<G::KP> pp(src, d.sAB, N, d.Sl, true, sb);
     pp.prime();
     if (l < nx) psi2[l] = yb[N * nx + l];
@@ -521,10 +527,11 @@ __device__ __forceinline__ void adjoint(const MpcConst& c, const Dims& d, const 
 template <class G>
 __device__ __forceinline__ void adjoint2(const MpcConst& c, const Dims& d, const StageSrc& src, double* sb,
                                          const double* yb1, double* out1, const double* yb2, double* out2,
-                                         double* psi4) {
+                                         double* psi4, volatile double* prog = nullptr) {
+    // prog (latency mode): stages done, after the stage's outputs
     constexpr int NX = G::NX, NU = G::NU;
     static_assert(NX != 0 && NX <= 16 && NU <= 16, "fixed dimensions");
-    const int l = threadIdx.x, N = c.N;
+    const int l = lane_id(), N = c.N;
     Pipe<G::KP> pp(src, d.sAB, N, d.Sl, true, sb);
     pp.prime();
     const bool second = (l & 16) != 0;  // lanes 16..31, 48..63
@@ -554,13 +561,19 @@ __device__ __forceinline__ void adjoint2(const MpcConst& c, const Dims& d, const
         for (int s2 = 0; s2 < NX; ++s2) v = fma(cv[s2], pv[s2], v);
         if (bl && (l & 15) < NU) out[k * NU + (l & 15)] = v;
         else if (!bl && k > 0 && (l & 15) < NX) pb[l & 15] = v;
+        if (prog) {
+            wsync();
+            if (l == 0) *prog = (double)(N - k);
+        }
     });
 }
 
 // W_k = 2Q + M_k of the state X_{k+1} for every block k (global scratch, one pass of all lanes)
 template <class G>
 __device__ __forceinline__ void stage_weights(const MpcConst& c, const RLds& L, const double* sm,
-                                              const double* __restrict__ C, double* __restrict__ Wg) {
+                                              const double* __restrict__ C, double* __restrict__ Wg,
+                                              int e0 = -1, int stride = kWave) {
+    if (e0 < 0) e0 = lane_id();  // (the latency mode spreads the items over its four waves)
     const int nx = G::NX ? G::NX : c.nx, nx2 = nx * nx, mc = mc_t<G>(c), ns = c.ns;
     const double* th = sm + L.th;
     const double* Dsig = sm + L.Dsig;
@@ -568,7 +581,7 @@ __device__ __forceinline__ void stage_weights(const MpcConst& c, const RLds& L, 
         // one lane per row (k, i) of W_k: the stage's constraint rows are read once per row
         // and every load of an item issues together (same grouping as m_entry)
         constexpr int NX = G::NX, MC = G::MC;
-        for (int e = threadIdx.x; e < c.N * NX; e += kWave) {
+        for (int e = e0; e < c.N * NX; e += stride) {
             const int k = e / NX, i = e - k * NX;
             const double* Ck = C + (size_t)k * MC * NX;
             const double* thk = th + k * MC;
@@ -609,7 +622,7 @@ __device__ __forceinline__ void stage_weights(const MpcConst& c, const RLds& L, 
             for (int u = 0; u < NX; ++u) Wg[(size_t)k * NX * NX + i * NX + u] = 2.0 * c.Q[i * NX + u] + w[u];
         }
     } else {
-        for (int e = threadIdx.x; e < c.N * nx2; e += kWave) {
+        for (int e = e0; e < c.N * nx2; e += stride) {
             const int k = e / nx2, q = e - k * nx2, i = q / nx, j = q - i * nx;
             Wg[e] = 2.0 * c.Q[q] + m_entry<G>(c, C + (size_t)k * mc * nx, th + k * mc, Dsig + k * ns, i, j);
         }
@@ -651,12 +664,12 @@ __device__ __forceinline__ float rcp_r(float x) {
 template <class G, class R = double>
 __device__ __forceinline__ bool factor_stage_fixed(const MpcConst& c, int k, const double* Ak, double* P, double* T,
                                                    double* Gm, const double* th, double* __restrict__ Fk, int ms,
-                                                   unsigned long long* sub) {
+                                                   unsigned long long* sub, double* Fr = nullptr) {
     constexpr int NX = G::NX, NU = G::NU, NA = NX + NU, NC = NA;
     constexpr int NE = NA * NC, RT = (NE + kWave - 1) / kWave;           // T entries, rounds
     constexpr int NT = NC * (NC + 1) / 2, RG = (NT + kWave - 1) / kWave; // G lower entries
     constexpr int NP = NA * (NA + 1) / 2, RP = (NP + kWave - 1) / kWave; // P lower entries
-    const int l = threadIdx.x;
+    const int l = lane_id();
     const double* Bk = Ak + NX * NX;
     const double* Wk = Ak + NX * NX + NX * NU;
 #ifdef CMPC_RIC_SUBSTAMP
@@ -856,7 +869,10 @@ __device__ __forceinline__ bool factor_stage_fixed(const MpcConst& c, int k, con
                     if (a2 == ka) hab = Hi[a2][b];
                 kv = fma(-hab, hv(kj, kg[b], kt[b], kd[b]), kv);
             }
-            if (l < NK) Fk[l] = kv;
+            if (l < NK) {
+                Fk[l] = kv;
+                if (Fr) Fr[l] = kv;  // (latency mode: the gains to wave 2 through an LDS ring)
+            }
             if (l < NU * NU) {
                 const int a = l / NU, b = l - a * NU;
                 R v = R(0);
@@ -866,6 +882,7 @@ __device__ __forceinline__ bool factor_stage_fixed(const MpcConst& c, int k, con
                     for (int b2 = 0; b2 < NU; ++b2)
                         if (a2 == a && b2 == b) v = Hi[a2][b2];
                 Fk[NK + l] = v;
+                if (Fr) Fr[NK + l] = v;
             }
         }
         // P_k entries (k > 0)
@@ -897,12 +914,31 @@ __device__ __forceinline__ bool factor_stage_fixed(const MpcConst& c, int k, con
 // Wg of stage_weights: writes the gains K_k = -Hvv^-1 Hvy and Hinv_k = Hvv^-1 of every stage
 // into F.  Returns false on a non-positive pivot (wave-uniform).  R = float: the fp32 stages of
 // Cfg::F32 (fixed dimensions only).
+// Latency mode: wait (bounded) until *v >= want; false on a timeout (the caller marks the agent unsolved
+// rather than hang the workgroup)
+// (LDS: a wave's LDS operations execute in order and the waiting wave's later reads issue after the flag's,
+// so the compiler fence of wsync() on both sides is the whole protocol)
+__device__ __forceinline__ bool spin_until(const volatile double* v, double want) {
+    bool ok = false;
+    for (int i = 0; i < (1 << 18) && !ok; ++i) {
+        ok = *v >= want;
+        if (!ok) __builtin_amdgcn_s_sleep(1);
+    }
+    wsync();
+    return ok;
+}
+constexpr int kRing = 4;  // latency mode: stages of gains in flight between waves 1 and 2
+
 template <class G, class R = double>
 __device__ __forceinline__ bool riccati_factor(const MpcConst& c, const Dims& d, const RLds& L, double* sm,
                                const double* __restrict__ A, const double* __restrict__ B,
                                const double* __restrict__ Wg, double* __restrict__ F,
-                               unsigned long long* sub = nullptr) {
-    const int l = threadIdx.x, nx = d.nx, nu = d.nu, na = d.na, nc = d.nc, N = c.N;
+                               unsigned long long* sub = nullptr, double* ring = nullptr,
+                               volatile double* prog = nullptr, const volatile double* cons = nullptr,
+                               volatile double* err = nullptr) {
+    // ring / prog / cons (latency mode, fixed dimensions): stage k's gains also go to LDS ring slot k % kRing,
+    // the slot written only once the consumer (wave 2) has passed stage k + kRing; prog = stages done
+    const int l = lane_id(), nx = d.nx, nu = d.nu, na = d.na, nc = d.nc, N = c.N;
     const int ms = c.ms;  // (a register: see riccati_solve)
 #ifdef CMPC_RIC_SUBSTAMP  // lab build (tools/ric_stamps.py --sub): per-phase clocks of the fp64 factor sweep
     unsigned long long s_a = sub ? clock64_() : 0;
@@ -934,7 +970,16 @@ __device__ __forceinline__ bool riccati_factor(const MpcConst& c, const Dims& d,
     bool ok = true;
     sweep(pp, [&](int k, const double* Ak) {
       if constexpr (G::NX != 0) {
-        ok = factor_stage_fixed<G, R>(c, k, Ak, P, T, Gm, th, F + (size_t)k * d.sF, ms, sub) && ok;
+        double* Fr = nullptr;
+        if (ring) {
+            if (!spin_until(cons, (double)(N - k - kRing)) && l == 0) *err = 1.0;
+            Fr = ring + (k % kRing) * d.sF;
+        }
+        ok = factor_stage_fixed<G, R>(c, k, Ak, P, T, Gm, th, F + (size_t)k * d.sF, ms, sub, Fr) && ok;
+        if (prog) {
+            wsync();
+            if (l == 0) *prog = (double)(N - k);
+        }
       } else {
         const double* Bk = Ak + d.sA;
         SUBSTAMP(-1)  // slots 9-11: T, G, Hvv..K; the rest of the factor (P update, stage advance) is slot 2 minus them
@@ -1085,7 +1130,7 @@ template <class G>
 __device__ __forceinline__ bool riccati_factor_dd(const MpcConst& c, const Dims& d, const RLds& L, double* sm,
                                   const double* __restrict__ A, const double* __restrict__ B,
                                   const double* __restrict__ Wg, double* __restrict__ F) {
-    const int l = threadIdx.x, nx = d.nx, nu = d.nu, na = d.na, N = c.N;
+    const int l = lane_id(), nx = d.nx, nu = d.nu, na = d.na, N = c.N;
     double* P = sm + L.Pd;
     double* PA = sm + L.PAd;
     double* PB = sm + L.PBd;
@@ -1362,8 +1407,9 @@ template <class G, class R = double>
 __device__ __forceinline__ void riccati_solve(const MpcConst& c, const Dims& d, const RLds& L, double* sm,
                               const double* __restrict__ A, const double* __restrict__ B,
                               const double* __restrict__ F, const double* rh, double* dU, double* dX,
-                              const double* yb = nullptr, const double* rd = nullptr, const double* rt = nullptr) {
-    const int l = threadIdx.x, nx = d.nx, nu = d.nu, na = d.na, N = c.N;
+                              const double* yb = nullptr, const double* rd = nullptr, const double* rt = nullptr,
+                              int part = 3) {  // part: 1 the backward pass, 2 the forward pass, 3 both
+    const int l = lane_id(), nx = d.nx, nu = d.nu, na = d.na, N = c.N;
     const int ms = c.ms;  // in a register: a read of c (LDS) inside a step waits on every read before it
     double* sb = sm + L.sb;
     double* pv = sm + L.pv;
@@ -1371,7 +1417,7 @@ __device__ __forceinline__ void riccati_solve(const MpcConst& c, const Dims& d, 
     const StageSrc src{A, B, F, d.sA, d.sB, d.sF, 0};
     // backward: p_N = 0;  g = -rh_k + B'p_x + p_u;  kk_k = -Hinv g (into dU);  p_k = [A'p_x; 0] + K'g.
     // Every lane forms the nu values of g itself (nu <= 4), so a stage needs one barrier.
-    {
+    if (part & 1) {
         Pipe<G::KP> pp(src, d.S, N, d.Sl, true, sb);
         pp.prime();
         if (l < na) pv[l] = (yb && l < nx) ? yb[N * nx + l] : 0.0;
@@ -1456,7 +1502,7 @@ __device__ __forceinline__ void riccati_solve(const MpcConst& c, const Dims& d, 
         });
     }
     // forward: y_0 = 0;  v_k = kk_k + K_k y_k;  dX_{k+1} = A_k dX_k + B_k v_k (every lane < nx forms v_k)
-    {
+    if (part & 2) {
         Pipe<G::KP> pp(src, d.S, N, d.Sl, false, sb);
         pp.prime();
         if (l < nx) {
@@ -1541,6 +1587,84 @@ __device__ __forceinline__ void riccati_solve(const MpcConst& c, const Dims& d, 
     }
 }
 
+// Latency mode, wave 2: the predictor's backward Riccati pass (riccati_solve part 1 with the pass-0
+// right-hand side, the same arithmetic) run stage by stage behind wave 1's factorisation and wave 0's
+// residual adjoint sweep: stage k's gains from the LDS ring once prog_f says the factorisation has passed
+// k, the adjoint's rd of stage k (finished here as the residual phase finishes it: + the 2R / 2dR gradient
+// and the input rows' multipliers) once prog_a says the adjoint sweep has.  cons: stages done (the
+// factorisation's ring back-pressure).  ybC: C'rt of the pass-0 rows.  Returns false on a wait timeout.
+template <class G>
+__device__ __forceinline__ bool riccati_back_piped(const MpcConst& c, const double* __restrict__ A,
+                                                   const double* __restrict__ B, const double* ring, int sF,
+                                                   const volatile double* prog_f, const volatile double* prog_a,
+                                                   volatile double* cons, const double* ybC, const double* rdA,
+                                                   const double* rt, const double* lam, const double* U,
+                                                   const double* up, double* pv, double* dU, int ms) {
+    constexpr int NX = G::NX, NU = G::NU, NA = NX + NU;
+    static_assert(NX != 0, "fixed dimensions");
+    const int l = lane_id(), N = c.N;
+    const int lx = l < NX ? l : NX - 1, la = l < NA ? l : NA - 1, lu = l < NU ? l : NU - 1;
+    if (l < NA) pv[l] = (l < NX) ? ybC[N * NX + l] : 0.0;
+    wsync();
+    bool okw = true;
+    for (int k = N - 1; k >= 0; --k) {
+        // A_k, B_k: kernel inputs, never written — loaded before the waits
+        const double* Ak = A + (size_t)k * NX * NX;
+        const double* Bk = B + (size_t)k * NX * NU;
+        double bm[NX][NU], ac[NX];
+#pragma unroll
+        for (int s2 = 0; s2 < NX; ++s2) {
+#pragma unroll
+            for (int a = 0; a < NU; ++a) bm[s2][a] = Bk[s2 * NU + a];
+            ac[s2] = Ak[s2 * NX + lx];
+        }
+        okw = spin_until(prog_a, (double)(N - k)) && okw;
+        okw = spin_until(prog_f, (double)(N - k)) && okw;
+        const double* Kg = ring + (k % kRing) * sF;
+        const double* Hg = Kg + NU * NA;
+        const double* pc = pv + ((N - 1 - k) & 1) * NA;
+        double* pn = pv + ((N - k) & 1) * NA;
+        double p[NA], kg[NU], hg[NU], r0[NU];
+#pragma unroll
+        for (int a = 0; a < NU; ++a) {
+            const int ci = k * NU + a, r = ms + 2 * ci;
+            const double rdf = rdA[ci] + (rdr_grad<G>(c, U, up, ci) + lam[r] - lam[r + 1]);  // (the residual phase's rd)
+            r0[a] = rdf + (rt[ms + 2 * ci] - rt[ms + 2 * ci + 1]);
+            kg[a] = Kg[a * NA + la];
+            hg[a] = Hg[lu * NU + a];
+        }
+        const double y0 = (l < NX) ? ybC[k * NX + l] : 0.0;
+#pragma unroll
+        for (int s2 = 0; s2 < NA; ++s2) p[s2] = pc[s2];
+        __builtin_amdgcn_sched_barrier(0);
+        double g[NU];
+#pragma unroll
+        for (int a = 0; a < NU; ++a) {
+            double v = p[NX + a] + r0[a];
+#pragma unroll
+            for (int s2 = 0; s2 < NX; ++s2) v = fma(bm[s2][a], p[s2], v);
+            g[a] = v;
+        }
+        double v = y0;
+        if (l < NX) {
+#pragma unroll
+            for (int s2 = 0; s2 < NX; ++s2) v = fma(ac[s2], p[s2], v);
+        }
+#pragma unroll
+        for (int a = 0; a < NU; ++a) v = fma(kg[a], g[a], v);
+        if (l < NA) pn[l] = v;
+        if (l < NU) {
+            double u = 0.0;
+#pragma unroll
+            for (int b = 0; b < NU; ++b) u = fma(-hg[b], g[b], u);
+            dU[k * NU + l] = u;
+        }
+        wsync();
+        if (l == 0) *cons = (double)(N - k);
+    }
+    return okw;
+}
+
 // out = rhs - K v with the product evaluated in double-double (the refinement residual of a
 // double-double iteration):  K v = sum_k Gamma_k' W_k Gamma_k v + (2R + 2D'dR D + diag(th_u)) v,
 // through the stage recursions (dd states in [yb, yb2), dd adjoint in psid).
@@ -1549,7 +1673,7 @@ __device__ __forceinline__ void kres_dd(const MpcConst& c, const Dims& d, const 
                                         const double* __restrict__ A, const double* __restrict__ B,
                                         const double* __restrict__ Wg, const double* v, const double* rhs,
                                         double* out) {
-    const int l = threadIdx.x, nx = d.nx, nu = d.nu, N = c.N, nx2 = nx * nx;
+    const int l = lane_id(), nx = d.nx, nu = d.nu, N = c.N, nx2 = nx * nx;
     double* Xd = sm + L.yb;
     double* sb = sm + L.sb;
     const double* th = sm + L.th;
@@ -2336,11 +2460,599 @@ __global__ __launch_bounds__(kWave) void mpc_riccati_kernel(const MpcConst c_arg
 #undef RCOUNT
 }
 
+
+// ---------------------------------------------------------------------------------------------------
+// Latency mode: four wavefronts per agent (mpc_riccati_mw_kernel).
+//
+// At the reference's shipped horizon (config_LPV.py:13-24: N = 125, 3 agents) the LDS image of one agent
+// is ~154 KB, so a CU holds one agent and three of its four SIMDs idle; a 3-agent step is then one serial
+// wave per agent, no faster than a CPU core running the C restatement (round 5: 11.2 / 43.4 ms against
+// 10.5 / 45.8 ms).  This kernel gives the agent's workgroup all four SIMDs:
+//   * every per-row / per-stage item loop (rows, residual rows, th, Dsig, the stage weights W_k, the
+//     right-hand sides rho / rt / C'rt, the row directions, the step bounds, the update) runs over the
+//     256 threads;
+//   * the residual adjoint sweep (wave 0) runs beside the Riccati factorisation (wave 1, its own stage
+//     slots sb2) and the residual rows (waves 2, 3).  The factorisation's precision (double-double or
+//     not) is decided in the one-wave kernel after this iteration's merit; here it is speculated from
+//     the state before it ("no new best iterate") and the factorisation is redone in the rare iteration
+//     where the merit says otherwise;
+//   * the Newton solves (serial in the stages) run on wave 0.
+// Every value is computed by the same expressions in the same order as in mpc_riccati_kernel; the sums
+// that cross rows (mu, mu_aff, the neighbourhood test) are accumulated by wave 0 in the one-wave
+// kernel's lane order, so the iterates are those of the one-wave kernel (GPU test
+// test_riccati_latency_mode_matches_one_wave).  CMPC_FLAG_ONE_WAVE keeps the one-wave kernel.
+constexpr int kMW = 4;  // wavefronts per agent
+
+__host__ __device__ inline RLds r_layout_mw(const MpcConst& c) {
+    RLds L = r_layout_ex(c, false);
+    const Dims d = dims_of(c);
+    L.sb2 = L.total;
+    L.red = L.sb2 + 2 * d.Sl;
+    L.ring = L.red + 16;
+    L.total = L.ring + ((kRing * d.sF + 1) & ~1);
+    return L;
+}
+
+// rt of the rows (the slack groups' Schur form of rho; mpc_riccati_kernel's loop) over nt threads
+template <class G>
+__device__ __forceinline__ void mw_rt(const MpcConst& c, int tid, int nt, const double* rho, const double* th,
+                                      const double* rsig, const double* Dsig, double* rt) {
+    constexpr int MC = G::MC;
+    const int ms = c.ms, mc = MC, ns = c.ns, m = c.m;
+    for (int r = tid; r < m; r += nt) {
+        double v = rho[r];
+        if (r < ms) {
+            const int k = r / mc, rr = r - k * mc, j = c.row_slack[rr];
+            if (j >= 0) {
+                double rk[MC];
+#pragma unroll
+                for (int r2 = 0; r2 < MC; ++r2) rk[r2] = rho[k * mc + r2];
+                const double q = 2.0 * c.Qs[j];
+                v = q * rho[r] - th[r] * c.row_sign[rr] * rsig[k * ns + j];
+#pragma unroll
+                for (int r2 = 0; r2 < MC; ++r2) {
+                    if (r2 == rr || c.row_slack[r2] != j) continue;
+                    const int R2 = k * mc + r2;
+                    v += th[R2] * rho[r] - th[r] * c.row_sign[rr] * c.row_sign[r2] * rk[r2];
+                }
+                v /= Dsig[k * ns + j];
+            }
+        }
+        rt[r] = v;
+    }
+}
+
+template <class G>
+__global__ __launch_bounds__(kMW * kWave) void mpc_riccati_mw_kernel(const MpcConst c_arg, const MpcPtrs P) {
+    static_assert(G::NX != 0 && !G::GR && !G::F32, "latency mode: fixed dimensions, rows in LDS, fp64");
+    constexpr int NT = kMW * kWave;
+    extern __shared__ __attribute__((aligned(16))) double sm[];
+    const int b = P.order ? min(max(P.order[blockIdx.x], 0), (int)gridDim.x - 1) : (int)blockIdx.x;
+    if (c_arg.rescue) {  // (as mpc_riccati_kernel; the whole workgroup returns)
+        const RGlb g0 = r_glb(c_arg);
+        if (P.ws[(size_t)b * g0.total + g0.hand] != 1.0 && P.status[b] != CMPC_UNSOLVED) return;
+    }
+    const int tid = threadIdx.x, l = lane_id();
+    const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const RLds L = r_layout_mw(c_arg);
+    {
+        const unsigned long long* src = reinterpret_cast<const unsigned long long*>(&c_arg);
+        unsigned long long* dst = reinterpret_cast<unsigned long long*>(sm + L.cst);
+        for (int i = tid; i < mpc_const_used_doubles(c_arg); i += NT) dst[i] = src[i];
+    }
+    __syncthreads();
+    const MpcConst& c = *reinterpret_cast<const MpcConst*>(sm + L.cst);
+    const Dims d = dims_t<G>(c);
+    const RGlb gl = r_glb(c);
+    constexpr int NX = G::NX, MC = G::MC;
+    const int nx = NX, nu = G::NU, N = c.N, ns = c.ns, mc = MC, n = c.n, ms = c.ms, m = c.m;
+
+    const double* __restrict__ A = P.A + (size_t)b * N * nx * nx;
+    const double* __restrict__ B = P.B + (size_t)b * N * nx * nu;
+    const double* __restrict__ x0 = P.x0 + (size_t)b * nx;
+    const double* __restrict__ up = P.up + (size_t)b * nu;
+    const double* __restrict__ pl = P.p + (size_t)b * (N + 1) * nx;
+    const double* __restrict__ C = P.C + (size_t)b * N * mc * nx;
+    const double* __restrict__ h = P.h + (size_t)b * N * mc;
+    double* __restrict__ ws = P.ws + (size_t)b * gl.total;
+    double* dta = ws + gl.dta;
+    double* dla = ws + gl.dla;
+    double* F = ws + gl.F;
+    double* bU = ws + gl.bU;
+    double* bsig = ws + gl.bsig;
+    double* Wg = ws + gl.Wk;
+    double* t = sm + L.t;
+    double* lam = sm + L.lam;
+    double* th = sm + L.th;
+    double* rp = sm + L.rp;
+    double* rho = sm + L.rho;
+    double* rt = sm + L.rt;
+    double* w = sm + L.w;
+    double* GdU = sm + L.GdU;
+    double* X = sm + L.X;
+    double* dX = sm + L.dX;
+    double* yb = sm + L.yb;
+    double* yb2 = sm + L.yb2;
+    double* psi = sm + L.psi;
+    double* U = sm + L.U;
+    double* dU = sm + L.dU;
+    double* rd = sm + L.rd;
+    double* gU = sm + L.gU;
+    double* rh = sm + L.rh;
+    double* cr = sm + L.cr;
+    double* sig = sm + L.sig;
+    double* dsig = sm + L.dsig;
+    double* Dsig = sm + L.Dsig;
+    double* rsig = sm + L.rsig;
+    double* sb = sm + L.sb;
+    double* red = sm + L.red;  // [0, 4): block reductions; 8..: values handed between waves
+    RLds L1 = L;
+    L1.sb = L.sb2;  // wave 1's stage slots: the factorisation runs beside wave 0's adjoint sweep
+    const StageSrc sAB{A, B, B, d.sA, d.sB, d.sF, 0};
+
+    // block reductions (max / min are order-free; the cross-row SUMS are wave 0's, below)
+    auto bred = [&](double v, int op) __attribute__((always_inline)) -> double {
+        v = op == 0 ? wave_max(v) : wave_min(v);
+        if (l == 0) red[wv] = v;
+        __syncthreads();
+        double r = red[0];
+        for (int q = 1; q < kMW; ++q) r = op == 0 ? nmax(r, red[q]) : fmin(r, red[q]);
+        __syncthreads();
+        return r;
+    };
+    // a value of wave 0 to every thread
+    auto from0 = [&](double v, int slot) __attribute__((always_inline)) -> double {
+        if (wv == 0 && l == 0) red[slot] = v;
+        __syncthreads();
+        const double r = red[slot];
+        __syncthreads();
+        return r;
+    };
+
+    for (int i = tid; i < L.cst; i += NT) sm[i] = 0.0;
+    __syncthreads();
+    double* hand = ws + gl.hand;
+    const bool warm = c_arg.rescue && hand[0] == 1.0;
+    bool dd_on = warm;
+    const int it0 = warm ? (int)hand[1] : 0;
+    if (warm) {
+        for (int i = tid; i < n; i += NT) U[i] = hand[2 + i];
+        for (int i = tid; i < N * ns; i += NT) sig[i] = hand[2 + n + i];
+    }
+    __syncthreads();
+    // per-section clocks (wave 0's view; the overlapped residual / factor phase is slot 0, a redone
+    // factorisation slot 2 / 3)
+    const bool stamp = P.stamps != nullptr;
+    unsigned long long* tsum = reinterpret_cast<unsigned long long*>(sm + L.stamps);
+    unsigned long long t_a = stamp ? clock64_() : 0, t_b = 0;
+#define MSTAMP(slot)                                    \
+    if (stamp && wv == 0) {                             \
+        t_b = clock64_();                               \
+        if (l == 0) tsum[slot] += t_b - t_a;            \
+        t_a = t_b;                                      \
+    }
+#define MCOUNT(slot) \
+    if (stamp && tid == 0) tsum[slot] += 1;
+
+    for (int r = tid; r < m; r += NT) {
+        double v;
+        if (r < ms) {
+            v = h[r];
+        } else {
+            const int q = r - ms, i = (q >> 1) % nu;
+            v = (q & 1) ? -c.u_lb[i] : c.u_ub[i];
+        }
+        w[r] = isfinite(v) ? v : INFINITY;
+    }
+    __syncthreads();
+    if (wv == 0) fwd_sim<G>(c, d, sAB, sb, x0, U, X);
+    __syncthreads();
+    double mact_l = 0.0, sp_l = 1.0;
+    const size_t ht = hand_t(c);
+    for (int r = tid; r < m; r += NT) {
+        if (isfinite(w[r])) {
+            if (warm) {
+                t[r] = hand[ht + r];
+                lam[r] = hand[ht + m + r];
+            } else {
+                const double g = row_value<G>(c, C, r, X, U, sig);
+                t[r] = fmax(w[r] - g, kT0Floor);
+                lam[r] = 1.0;
+            }
+            mact_l += 1.0;
+            sp_l = fmax(sp_l, fabs(w[r]));
+        } else {
+            t[r] = 1.0;
+            lam[r] = 0.0;
+        }
+    }
+    // the active-row count: integer-valued, exact in any order
+    const double mact_w = wave_sum(mact_l);  // (every lane: a cross-lane sum)
+    if (l == 0) red[4 + wv] = mact_w;
+    __syncthreads();
+    const double mact = fmax(red[4] + red[5] + red[6] + red[7], 1.0);
+    const double scale_p = bred(sp_l, 0);  // (its barriers: every thread has read `warm` and the rows)
+    if (warm && tid == 0) hand[0] = 0.0;
+    if (tid == 0) red[15] = 0.0;  // a timed-out wait between the waves
+
+    double best_m = INFINITY, best_kkt = INFINITY;
+    int best_it = 0, stop = kStopMaxIter, it;
+    double kkt = INFINITY;
+    MSTAMP(14);
+    double alpha_prev = 1;
+    bool hp = false;
+    for (it = it0 + 1; it <= c.max_iter; ++it) {
+        // ---- item phases (all waves): the residual adjoints' right-hand sides, th, the residual rows, Dsig,
+        // the stage weights W_k, and the predictor's right-hand side (rho, rt, C'rt: they need only the
+        // iterate, so wave 2 can run its backward pass beside the factorisation) ----
+        if (tid == 0) red[12] = red[13] = red[14] = 0.0;  // progress: factorisation, adjoint sweep, piped pass
+        for (int i = tid; i < (N + 1) * nx; i += NT) {
+            const int k = i / nx, s = i - k * nx;
+            double v = 2.0 * pl[i];
+            for (int u = 0; u < nx; ++u) v = fma(2.0 * c.Q[s * nx + u], X[k * nx + u], v);
+            yb[i] = v;
+        }
+        for (int r = tid; r < m; r += NT) {
+            th[r] = isfinite(w[r]) ? lam[r] / t[r] : 0.0;
+            rp[r] = isfinite(w[r]) ? row_value<G>(c, C, r, X, U, sig) + t[r] - w[r] : 0.0;
+        }
+        for (int i = tid; i < N * ns; i += NT) {
+            const int k = i / ns, j = i - k * ns;
+            double v = 2.0 * c.Qs[j] * sig[i];
+            for (int r = 0; r < mc; ++r)
+                if (c.row_slack[r] == j) v += c.row_sign[r] * lam[k * mc + r];
+            rsig[i] = v;
+        }
+        __syncthreads();
+        for (int i = tid; i < (N + 1) * nx; i += NT) {
+            const int k = i / nx, s = i - k * nx;
+            double v = 0.0;
+            if (k > 0)
+                for (int r = 0; r < mc; ++r) v = fma(lam[(k - 1) * mc + r], C[((size_t)(k - 1) * mc + r) * nx + s], v);
+            yb2[i] = k > 0 ? yb[i] + v : yb[i];
+        }
+        for (int i = tid; i < N * ns; i += NT) {
+            const int k = i / ns, j = i - k * ns;
+            double v = 2.0 * c.Qs[j];
+            for (int r = 0; r < mc; ++r)
+                if (c.row_slack[r] == j) v += th[k * mc + r];
+            Dsig[i] = v;
+        }
+        for (int r = tid; r < m; r += NT) {  // pass 0's rho (the one-wave kernel's statements)
+            if (!isfinite(w[r])) {
+                rho[r] = 0.0;
+                continue;
+            }
+            double rc = -t[r] * lam[r];
+            rho[r] = (rc + lam[r] * rp[r]) / t[r];
+        }
+        __syncthreads();
+        stage_weights<G>(c, L, sm, C, Wg, tid, NT);
+        double thm_l = 0.0;
+        for (int r = tid; r < m; r += NT) thm_l = fmax(thm_l, th[r]);
+        mw_rt<G>(c, tid, NT, rho, th, rsig, Dsig, rt);
+        gsync();  // W_k (global): stored here by every wave, read by wave 1's factorisation
+        const bool above = bred(thm_l, 0) > kDdTh;
+        double* ybC = dX;  // pass 0's C'rt (dX is free until pass 0's forward pass writes it)
+        for (int i = tid; i < (N + 1) * nx; i += NT) {
+            const int k = i / nx, s = i - k * nx;
+            double v = 0.0;
+            if (k > 0)
+                for (int r = 0; r < mc; ++r) v = fma(rt[(k - 1) * mc + r], C[((size_t)(k - 1) * mc + r) * nx + s], v);
+            ybC[i] = v;
+        }
+        __syncthreads();
+        // ---- wave 0: both residual adjoints; wave 1: the factorisation (speculative precision); wave 2
+        // (fp64 guess): the predictor's backward pass, stage by stage behind them ----
+        const bool hp_spec = above && (dd_on || it - best_it >= kDdStall);
+#ifdef RIC_MW_NOPIPE  // lab: no backward pass beside the factorisation
+        const bool piped = false;
+#else
+        const bool piped = !hp_spec;
+#endif
+        MSTAMP(1);  // (slot 1: the item phases before the waves' roles)
+        const unsigned long long t_role = stamp ? clock64_() : 0;
+        auto factor = [&](bool hp_want, bool ring_on) __attribute__((always_inline)) {
+            bool ok = hp_want ? riccati_factor_dd<G>(c, d, L1, sm, A, B, Wg, F)
+                              : riccati_factor<G>(c, d, L1, sm, A, B, Wg, F, nullptr, ring_on ? sm + L.ring : nullptr,
+                                                  red + 12, red + 14, red + 15);
+            bool hp_f = hp_want;
+            if (!ok && !hp_want && above) {  // fp64 breakdown above the threshold: double-double (as the one-wave kernel)
+                gsync();
+                hp_f = true;
+                ok = riccati_factor_dd<G>(c, d, L1, sm, A, B, Wg, F);
+            }
+            gsync();  // the gains F (global), read by wave 0's solves
+            if (l == 0) {
+                red[8] = ok ? 1.0 : 0.0;
+                red[9] = hp_f ? 1.0 : 0.0;
+            }
+        };
+        if (wv == 0) {
+            adjoint2<G>(c, d, sAB, sb, yb, gU, yb2, rd, sm + L.psid, red + 13);
+        } else if (wv == 1) {
+            factor(hp_spec, piped);
+        } else if (wv == 2 && piped) {
+            if (!riccati_back_piped<G>(c, A, B, sm + L.ring, d.sF, red + 12, red + 13, red + 14, ybC, rd, rt, lam, U, up,
+                                       sm + L.pv, dU, ms) && l == 0)
+                red[15] = 1.0;
+        }
+        if (stamp && l == 0 && wv < 3) tsum[9 + wv] += clock64_() - t_role;  // slots 9-11: each role's own clocks
+        __syncthreads();
+        double gs_l = 1.0, nrd_l = 0.0, nrs_l = 0.0, nrp_l = 0.0;
+        for (int i = tid; i < n; i += NT) {
+            gU[i] += rdr_grad<G>(c, U, up, i);
+            gs_l = nmax(gs_l, fabs(gU[i]));
+            const int r = ms + 2 * i;
+            rd[i] += rdr_grad<G>(c, U, up, i) + lam[r] - lam[r + 1];
+            nrd_l = nmax(nrd_l, fabs(rd[i]));
+        }
+        for (int i = tid; i < N * ns; i += NT) nrs_l = nmax(nrs_l, fabs(rsig[i]));
+        for (int r = tid; r < m; r += NT)
+            if (isfinite(w[r])) nrp_l = nmax(nrp_l, fabs(rp[r]));
+        double mu_l = 0.0;  // wave 0, in the one-wave kernel's lane order
+        if (wv == 0)
+            for (int r = l; r < m; r += kWave)
+                if (isfinite(w[r])) mu_l += t[r] * lam[r];
+        const double mu = from0(wave_sum(mu_l) / mact, 10);
+        const double gscale = bred(gs_l, 0);
+        const double nrd = bred(nrd_l, 0), nrs = bred(nrs_l, 0), nrp = bred(nrp_l, 0);
+        const double res = nmax(nmax(nrd / gscale, nrs / c.qs_max), nrp / scale_p);
+        kkt = nmax(res, mu);
+        const double merit = nmax(res, 1e4 * mu);
+        if (!isfinite(merit)) {
+            stop = kStopNonFinite;
+            break;
+        }
+        if (red[15] != 0.0) {  // a wait between the waves timed out (never expected): give the agent up
+            stop = kStopBreakdown;
+            break;
+        }
+        if (merit < best_m) {
+            best_m = merit;
+            best_kkt = kkt;
+            best_it = it;
+            for (int i = tid; i < n; i += NT) bU[i] = U[i];
+            for (int i = tid; i < N * ns; i += NT) bsig[i] = sig[i];
+        }
+        if (merit < c.tol) {
+            stop = kStopConverged;
+            break;
+        }
+        if (best_m < 1e3 * c.tol && it - best_it >= kStallIters) {
+            stop = kStopStalled;
+            break;
+        }
+        if (warm && it - best_it >= kWarmStall) {
+            stop = kStopStalled;
+            break;
+        }
+        // the precision the one-wave kernel picks now (this iteration's best_it); redo on a miss
+        if (!dd_on && it - best_it >= kDdStall) dd_on = true;
+        hp = above && dd_on;
+        MSTAMP(0);
+        if (hp != hp_spec) {
+            if (wv == 1) factor(hp, false);
+            __syncthreads();
+        }
+        const bool fact_ok = red[8] != 0.0;
+        if (red[9] != 0.0 && !hp) dd_on = hp = true;
+        __syncthreads();  // (red[8], red[9] read by every thread before the next writes)
+        if (!fact_ok) {
+            stop = kStopBreakdown;
+            break;
+        }
+        MSTAMP(hp ? 3 : 2);
+        if (hp) MCOUNT(12);
+
+        // ================= predictor / corrector =================
+        double sig_c = 0.0, alpha = 0.0;
+        for (int pass = 0; pass < 2; ++pass) {
+            if (pass) {  // (pass 0's rho, rt and C'rt were formed before the factorisation)
+                for (int r = tid; r < m; r += NT) {
+                    if (!isfinite(w[r])) {
+                        rho[r] = 0.0;
+                        continue;
+                    }
+                    double rc = -t[r] * lam[r];
+                    rc += sig_c * mu - dta[r] * dla[r];
+                    rho[r] = (rc + lam[r] * rp[r]) / t[r];
+                }
+                __syncthreads();
+                mw_rt<G>(c, tid, NT, rho, th, rsig, Dsig, rt);
+                __syncthreads();
+                for (int i = tid; i < (N + 1) * nx; i += NT) {
+                    const int k = i / nx, s = i - k * nx;
+                    double v = 0.0;
+                    if (k > 0)
+                        for (int r = 0; r < mc; ++r) v = fma(rt[(k - 1) * mc + r], C[((size_t)(k - 1) * mc + r) * nx + s], v);
+                    yb[i] = v;
+                }
+                __syncthreads();
+            }
+            const double* yrt = pass ? yb : ybC;
+            MSTAMP(4);
+            if (wv == 0) {  // the Newton solve: serial in the stages
+                if (!hp) {  // (pass 0 with wave 2's backward pass: the forward pass only)
+                    riccati_solve<G>(c, d, L, sm, A, B, F, nullptr, dU, dX, yrt, rd, rt, (!pass && piped) ? 2 : 3);
+                } else {
+                    adjoint<G>(c, d, sAB, sb, yrt, rh, psi);
+                    for (int i = l; i < n; i += kWave) rh[i] = -rd[i] - (rh[i] + rt[ms + 2 * i] - rt[ms + 2 * i + 1]);
+                    wsync();
+                    riccati_solve<G>(c, d, L, sm, A, B, F, rh, dU, dX);
+                    const int nref = warm ? kRefineMaxWarm : kRefineMax;
+                    for (int ir = 0; ir < nref; ++ir) {
+                        kres_dd<G>(c, d, L, sm, A, B, Wg, dU, rh, gU);
+                        riccati_solve<G>(c, d, L, sm, A, B, F, gU, cr, nullptr);
+                        double cn_l = 0.0, un_l = 0.0;
+                        for (int i = l; i < n; i += kWave) {
+                            const double u = dU[i] + cr[i];
+                            dU[i] = u;
+                            cn_l = nmax(cn_l, fabs(cr[i]));
+                            un_l = fmax(un_l, fabs(u));
+                        }
+                        const double cn = wave_max(cn_l), un = wave_max(un_l);
+                        wsync();
+                        MCOUNT(13);
+                        if (!(cn > kRefineTol * un)) break;
+                    }
+                    fwd_sim<G>(c, d, sAB, sb, nullptr, dU, dX);
+                }
+            }
+            __syncthreads();
+            MSTAMP(hp ? 6 : 5);
+            for (int r = tid; r < m; r += NT) GdU[r] = row_value<G>(c, C, r, dX, dU, nullptr);
+            __syncthreads();
+            for (int i = tid; i < N * ns; i += NT) {
+                const int k = i / ns, j = i - k * ns;
+                double v = rsig[i];
+#pragma unroll
+                for (int r = 0; r < MC; ++r)
+                    if (c.row_slack[r] == j) {
+                        const int R1 = k * mc + r;
+                        v += c.row_sign[r] * (rho[R1] + th[R1] * GdU[R1]);
+                    }
+                dsig[i] = -v / Dsig[i];
+            }
+            __syncthreads();
+            double amax_l = 1.0e300;
+            double* dtp = pass ? rho : dta;  // corrector reuses rho/rt storage for (dt, dl)
+            double* dlp = pass ? rt : dla;
+            for (int r = tid; r < m; r += NT) {
+                if (!isfinite(w[r])) {
+                    dtp[r] = 0.0;
+                    dlp[r] = 0.0;
+                    continue;
+                }
+                double sd = 0.0;
+                if (r < ms) {
+                    const int k = r / mc, rr = r - k * mc, j = c.row_slack[rr];
+                    if (j >= 0) sd = c.row_sign[rr] * dsig[k * ns + j];
+                }
+                const double rho_r = rho[r];
+                const double dtv = -rp[r] - GdU[r] - sd;
+                const double dlv = rho_r + th[r] * (GdU[r] + sd);
+                dtp[r] = dtv;
+                dlp[r] = dlv;
+                if (dtv < 0.0) amax_l = fmin(amax_l, -t[r] / dtv);
+                if (dlv < 0.0) amax_l = fmin(amax_l, -lam[r] / dlv);
+            }
+            gsync();  // (dta, dla: global)
+            const double amax = fmin(bred(amax_l, 1), 1.0e300);
+            if (!pass) {
+                const double a = fmin(amax, 1.0);
+                double mua_l = 0.0;
+                if (wv == 0)
+                    for (int r = l; r < m; r += kWave)
+                        if (isfinite(w[r])) mua_l += (t[r] + a * dta[r]) * (lam[r] + a * dla[r]);
+                const double mu_aff = from0(wave_sum(mua_l) / mact, 11);
+                const double ratio = mu > 0.0 ? mu_aff / mu : 0.0;
+                sig_c = warm ? ratio * ratio : ratio * ratio * ratio;
+                if (alpha_prev < kShortStep) sig_c = fmax(sig_c, kSigmaMin);
+            } else {
+                alpha = fmin(1.0, 0.995 * amax);
+                if (wv == 0) {  // the neighbourhood backtracking, in the one-wave kernel's order
+                    for (int bt = 0; bt < kMaxBacktrack; ++bt) {
+                        double mn_l = 0.0, pm_l = INFINITY;
+                        for (int r = l; r < m; r += kWave)
+                            if (isfinite(w[r])) {
+                                const double pr = (t[r] + alpha * rho[r]) * (lam[r] + alpha * rt[r]);
+                                mn_l += pr;
+                                pm_l = fmin(pm_l, pr);
+                            }
+                        if (wave_min(pm_l) >= kNbhdGamma * (wave_sum(mn_l) / mact)) break;
+                        alpha *= 0.8;
+                    }
+                }
+                alpha = from0(alpha, 12);
+            }
+            MSTAMP(7);
+        }
+        alpha_prev = alpha;
+        for (int i = tid; i < n; i += NT) U[i] = fma(alpha, dU[i], U[i]);
+        for (int i = tid; i < N * ns; i += NT) sig[i] = fma(alpha, dsig[i], sig[i]);
+        for (int i = tid; i < (N + 1) * nx; i += NT) X[i] = fma(alpha, dX[i], X[i]);
+        for (int r = tid; r < m; r += NT)
+            if (isfinite(w[r])) {
+                t[r] = fma(alpha, rho[r], t[r]);
+                lam[r] = fma(alpha, rt[r], lam[r]);
+            }
+        __syncthreads();
+        MSTAMP(8);
+    }
+    if (it > c.max_iter) it = c.max_iter;
+    gsync();
+    __syncthreads();
+    int status = CMPC_SOLVED;
+    const bool pol = c_arg.rescue && c.polish && stop != kStopConverged && stop != kStopNonFinite &&
+                     (best_m < 1e3 * c.tol || stop == kStopMaxIter || c_arg.rescue == 2);
+    if (pol) {
+        const int ht2 = (int)hand_t(c);
+        for (int i = tid; i < n; i += NT) hand[2 + i] = U[i];
+        for (int i = tid; i < N * ns; i += NT) hand[2 + n + i] = sig[i];
+        for (int r = tid; r < m; r += NT) {
+            hand[ht2 + r] = t[r];
+            hand[ht2 + m + r] = lam[r];
+        }
+        if (tid == 0) {
+            hand[0] = 2.0;
+            hand[1] = best_m;
+        }
+    }
+    __syncthreads();
+    if (stop != kStopConverged) {
+        if (best_it > 0) {  // restore the best iterate
+            for (int i = tid; i < n; i += NT) U[i] = bU[i];
+            for (int i = tid; i < N * ns; i += NT) sig[i] = bsig[i];
+            kkt = best_kkt;
+        }
+        status = stop_status(stop, best_m, c.tol);
+    }
+    __syncthreads();
+    if (wv == 0) fwd_sim<G>(c, d, sAB, sb, x0, U, X);
+    __syncthreads();
+    const int nxe = nx + ns;
+    const size_t nz = (size_t)nxe * (N + 1) + 2 * (size_t)n;
+    double* z = P.z + (size_t)b * nz;
+    for (int i = tid; i < (N + 1) * nxe; i += NT) {
+        const int k = i / nxe, s = i - k * nxe;
+        z[i] = (s < nx) ? X[k * nx + s] : (k ? sig[(k - 1) * ns + (s - nx)] : 0.0);
+    }
+    for (int i = tid; i < n; i += NT) {
+        const int k = i / nu, j = i - k * nu;
+        z[(size_t)(N + 1) * nxe + i] = U[i];
+        z[(size_t)(N + 1) * nxe + n + i] = U[i] - (k ? U[(k - 1) * nu + j] : up[j]);
+    }
+    if (tid == 0) {
+        if (P.kkt) P.kkt[b] = kkt;
+        if (P.iters) P.iters[b] = it;
+        if (P.status) P.status[b] = status;
+    }
+    MSTAMP(14);
+    if (stamp) {
+        __syncthreads();
+        if (tid < kStampSlots) P.stamps[(size_t)b * kStampSlots + tid] = (tid == kStampSlots - 1) ? (unsigned long long)it : tsum[tid];
+    }
+#undef MSTAMP
+#undef MCOUNT
+}
+
 }  // namespace
 
 bool mpc_riccati_f32_supported(const MpcConst& c) { return c.nx == 6 && c.nu == 3 && c.mc == 6; }
 
-size_t mpc_riccati_lds_bytes(const MpcConst& c) { return sizeof(double) * (size_t)r_layout(c).total; }
+size_t mpc_riccati_lds_bytes(const MpcConst& c) {
+    return sizeof(double) * (size_t)(mpc_riccati_mw(c) ? r_layout_mw(c) : r_layout(c)).total;
+}
+
+// The latency mode (mpc_riccati_mw_kernel) where it applies: the PlannerLPV agent with two neighbours
+// (nx 9, nu 2, 6 rows per stage: the reference's shipped N = 125), fp64, an LDS image that leaves a CU
+// to one agent (over half of it: three SIMDs of the CU would idle), unless CMPC_FLAG_ONE_WAVE.
+bool mpc_riccati_mw(const MpcConst& c) {
+    if (c.f32 || c.waves == 1 || !(c.nx == 9 && c.nu == 2 && c.mc == 6) || r_rows_global(c)) return false;
+    const size_t one = sizeof(double) * (size_t)r_layout(c).total, mw = sizeof(double) * (size_t)r_layout_mw(c).total;
+    return 2 * one > kMaxLdsBytes && mw <= kMaxLdsBytes;
+}
 
 size_t mpc_riccati_ws_doubles(const MpcConst& c) { return r_glb(c).total; }
 
@@ -2361,6 +3073,18 @@ hipError_t mpc_riccati_launch(const MpcConst& c, const MpcPtrs& p, int batch, hi
         return hipSuccess;
     };
     hipError_t e;
+    if (mpc_riccati_mw(c)) {  // the latency mode: four wavefronts per agent
+        using G = Cfg<kPerSmall, 9, 2, 6>;
+        e = hipFuncSetAttribute((const void*)mpc_riccati_mw_kernel<G>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)lds);
+        if (e != hipSuccess) return e;
+        hipLaunchKernelGGL(mpc_riccati_mw_kernel<G>, dim3(batch), dim3(kMW * kWave), lds, s, c, p);
+        return hipGetLastError();
+    }
+#ifdef RIC_LAB_ONLY_MW  // lab builds: the latency-mode kernel alone (a fast compile)
+    (void)small;
+    return hipErrorInvalidValue;
+#else
     if (c.f32) {  // BASELINE cfg5's fp32 path (mpc_riccati_f32_supported)
         if (!mpc_riccati_f32_supported(c)) return hipErrorInvalidValue;
         e = r_rows_global(c) ? go(Cfg<kPerSmall, 6, 3, 6, true, true>{}) : go(Cfg<kPerSmall, 6, 3, 6, false, true>{});
@@ -2372,6 +3096,7 @@ hipError_t mpc_riccati_launch(const MpcConst& c, const MpcPtrs& p, int batch, hi
         e = r_rows_global(c) ? go(Cfg<kPerSmall, 6, 3, 6, true>{}) : go(Cfg<kPerSmall, 6, 3, 6>{});
     else if (small) e = go(Cfg<kPerSmall, 0, 0, 0>{});
     else e = go(Cfg<kPerMax, 0, 0, 0>{});
+#endif
     if (e != hipSuccess) return e;
     return hipGetLastError();
 }

@@ -94,7 +94,8 @@ typedef struct cmpc_ctx cmpc_ctx;
                                (range-space KKT, two active-set corrections) and returns it when its merit
                                is lower (status 1 below tol) */
 #define CMPC_FLAG_ONE_WAVE 512  /* the condensed kernel's fused double-integrator instantiation: one wavefront per
-                                   agent (the default) */
+                                   agent (the default there); the stage-wise Riccati kernel: one wavefront per agent
+                                   also where its latency mode (four per agent) would apply */
 #define CMPC_FLAG_TWO_WAVES 1024 /* ... two wavefronts per agent (a 128-lane workgroup: split K build, the
                                    predictor's right-hand side on the second wave); bit-identical results, no
                                    faster at 512 agents on one MI355X, so opt-in.  Applies to the
@@ -204,9 +205,11 @@ typedef struct {
     int lds_bytes;     /* dynamic LDS per workgroup */
     int wg_per_cu;     /* workgroups resident per CU */
     int agents_per_wg; /* 1, or 32 (lane solver) */
-    int waves_per_agent;   /* wavefronts of one agent's workgroup (1; 2: the condensed kernel's small-batch mode,
-                              CMPC_FLAG_ONE_WAVE / CMPC_FLAG_TWO_WAVES); agents of a fused double-integrator round
-                              only (cmpc_di_solve_dev), so the plan of a structured batch reports 1 */
+    int waves_per_agent;   /* wavefronts of one agent's workgroup: 1; 4 for the stage-wise Riccati kernel's latency
+                              mode (an LDS image over half a CU, the PlannerLPV agent at the reference's N = 125:
+                              the agent's workgroup gets all four SIMDs of its CU; CMPC_FLAG_ONE_WAVE keeps one);
+                              (2: the condensed kernel's CMPC_FLAG_TWO_WAVES mode of a fused double-integrator round,
+                              cmpc_di_solve_dev, which the plan of a structured batch does not describe) */
     /* The rescue policy (CMPC_FLAG_RESCUE [| CMPC_FLAG_POLISH]) adds launches the fields above do not
      * describe: the polish kernel (before the Riccati hand-over and after the Riccati passes; one
      * 256-thread workgroup per agent, agents without a flag return at once) and two Riccati passes.

@@ -4,6 +4,7 @@ device (there is no CPU fallback)."""
 import ctypes as ct
 import re
 
+import numpy as np
 import pytest
 
 import cmpc
@@ -61,6 +62,17 @@ def test_plan_occupancy_of_the_bench_configs():
     with pytest.raises(cmpc.CmpcError):
         plan(S.di_shared(2, 30, 2), 512, flags=L.CMPC_FLAG_ONE_WAVE | L.CMPC_FLAG_TWO_WAVES)
     assert plan(S.di_shared(2, 30, 2), 512, flags=L.CMPC_FLAG_TWO_WAVES)["waves_per_agent"] == 1
+    # the Riccati kernel's latency mode: the PlannerLPV agent at the reference's N = 125 (an LDS image over
+    # half a CU) gets four wavefronts; CMPC_FLAG_ONE_WAVE keeps one; the synthetic shapes keep one
+    lpv = dict(nx=9, nu=2, N=125, ns=3, mc=6, Q=np.diag([10.0, 0, 0, 25, 10, 0, 0, 0, 0]), R=np.zeros((2, 2)),
+               dR=50 * np.eye(2), Qs=1e7 * np.ones(3), u_ub=np.array([0.3, 5.0]), u_lb=np.array([-0.3, -10.0]),
+               row_slack=np.array([-1, 0, 1, 1, 2, 2]), row_sign=np.array([1, 1, 1, 1, -1, -1]))
+    p125 = plan(lpv, 3)
+    assert p125["solver"] == "riccati" and p125["waves_per_agent"] == 4 and p125["lds_bytes"] <= 160 * 1024, p125
+    p125one = plan(lpv, 3, flags=L.CMPC_FLAG_ONE_WAVE)
+    assert p125one["waves_per_agent"] == 1 and p125one["lds_bytes"] < p125["lds_bytes"], p125one
+    assert plan(dict(lpv, N=30), 3, riccati=True)["waves_per_agent"] == 1
+    assert all(plan(S.di_shared(3, 50, 2), 8192, fp32=f)["waves_per_agent"] == 1 for f in (False, True))
 
 
 def test_no_cpu_fallback_without_device():

@@ -63,6 +63,39 @@ def test_lpv_batch_matches_reference_optimum(gpu_ctx, name):
             np.testing.assert_allclose(res["planes"], np.stack([c["planes"] for c in cs]), rtol=0, atol=1e-14)
 
 
+def test_riccati_latency_mode_matches_one_wave(gpu_ctx):
+    """The Riccati kernel's latency mode (four wavefronts per agent: item loops over 256 threads, the
+    residual adjoint sweep beside the factorisation, mpc_riccati_mw_kernel) on the reference's shipped
+    configuration (N = 125, the six captured QPs of lpv_n125_a3, steps 0 and 1 — the latter with
+    double-double iterations): the same iterates as the one-wave kernel (CMPC_FLAG_ONE_WAVE) — z, kkt,
+    iterations and status bit for bit — and the certified optima."""
+    import cmpc
+    from cmpc import _lib as L
+    from oracle import lpv_ref as LR
+
+    g, model = _gains()
+    tr = LR.Track.build("Highway")
+    cs = [c for _, c in lpv_qps("lpv_n125_a3")]
+    for rows in sorted({c["x_last"].shape[0] for c in cs}):
+        grp = [c for c in cs if c["x_last"].shape[0] == rows]
+        lim = LR.scaled_car_limits(grp[0]["vx_ref"])
+        bp = cmpc.PlannerLPVBatch(g["Q"], g["Qs"], g["R"], g["dR"], grp[0]["N"], grp[0]["dt"], tr, g["wq"], model,
+                                  lim, ctx=gpu_ctx)
+        args = (np.stack([c["x0"] for c in grp]), np.stack([c["x_last"] for c in grp]),
+                np.stack([c["u_last"] for c in grp]), np.stack([c["u_old"] for c in grp]),
+                np.stack([c["x_agents"] for c in grp]), np.stack([c["pose"] for c in grp]))
+        mw = bp.solve(*args)
+        bp.opts = L.opts(None, None, bp.opts.flags | L.CMPC_FLAG_ONE_WAVE)
+        one = bp.solve(*args)
+        print(f"N=125 rows {rows}: iterations {mw['iters'].tolist()} (one wave {one['iters'].tolist()}), "
+              f"status {mw['status'].tolist()}, |z_mw - z_one| {np.abs(mw['z'] - one['z']).max():.2e}")
+        for k in ("z", "kkt", "iters", "status"):
+            np.testing.assert_array_equal(mw[k], one[k], err_msg=k)
+        assert (mw["status"] == cmpc.CMPC_SOLVED).all()
+        for a, c in enumerate(grp):
+            assert_matches_optimum(mw["z"][a], c, Z_TOL)
+
+
 def test_planner_lpv_dropin_closed_loop(gpu_ctx):
     """The reference-interface PlannerLPV driven by the reference loop semantics
     (LPV_HP_N_main.py:96-117) reproduces the captured trajectory."""

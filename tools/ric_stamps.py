@@ -1,7 +1,10 @@
 """Diagnostic: per-section shader-clock breakdown of the Riccati kernel (mpc_riccati.hip) on the
 reference's N = 125 captured QPs (tests/golden/lpv_n125_a3.npz), or a synthetic long horizon.
-Usage: python tools/ric_stamps.py [lpv_case] | python tools/ric_stamps.py --cfg5 [agents]
-(--cfg5: the first round of the BASELINE cfg5 population, N = 50, nx 6, nu 3; means over agents)"""
+Usage: python tools/ric_stamps.py [--one-wave] [lpv_case] | python tools/ric_stamps.py --cfg5 [agents]
+(--cfg5: the first round of the BASELINE cfg5 population, N = 50, nx 6, nu 3; means over agents.
+The N = 125 agent runs the kernel's latency mode, four wavefronts per agent, unless --one-wave: there
+slot 0 is the overlapped phase — residual adjoints on wave 0 beside the factorisation on wave 1 —, and
+slots 2 / 3 hold only a factorisation redone after a missed precision guess)"""
 import os
 import sys
 import time
@@ -32,12 +35,21 @@ def report(st, iters, label, ms):
     tot = a[:, [k for k in NAMES]].sum(1)
     for k, nm in NAMES.items():
         print(f"  {nm:34s} " + " ".join(f"{v / 1e6:8.3f}M" for v in a[:, k]) + "   clk per agent")
-        if k == 2 and a[:, 9:12].any():
+        if k == 2 and a[:, 9:12].any() and (ONE_WAVE or not label.startswith("lpv")):
             for k2, nm2 in SUB.items():
                 print(f"  {nm2:34s} " + " ".join(f"{v / 1e6:8.3f}M" for v in a[:, k2]) + "   clk per agent")
+    if not ONE_WAVE and label.startswith("lpv") and a[:, 9:12].any():  # latency mode: each role's own clocks
+        for k2, nm2 in ((9, "  role: residual adjoints (wave 0)"), (10, "  role: factorisation (wave 1)"),
+                        (11, "  role: piped backward pass (wave 2)")):
+            print(f"  {nm2:34s} " + " ".join(f"{v / 1e6:8.3f}M" for v in a[:, k2]) + "   clk per agent")
     it = np.maximum(a[:, SLOTS - 1], 1)
     print(f"  {'total':34s} " + " ".join(f"{v / 1e6:8.3f}M" for v in tot) +
           "   | per iteration " + " ".join(f"{v / 1e3:.0f}k" for v in tot / it))
+
+
+ONE_WAVE = "--one-wave" in sys.argv
+if ONE_WAVE:
+    sys.argv.remove("--one-wave")
 
 
 def lpv(name):
@@ -62,11 +74,19 @@ def lpv(name):
         t0 = time.perf_counter()
         res = bp.solve(*args)
         ms = (time.perf_counter() - t0) * 1e3
-        bp.opts = L.opts(flags=L.CMPC_FLAG_RICCATI, stamps=st.data_ptr())
+        flags = L.CMPC_FLAG_RICCATI | (L.CMPC_FLAG_ONE_WAVE if ONE_WAVE else 0)
+        if ONE_WAVE:
+            bp.opts = L.opts(flags=flags)
+            bp.solve(*args)
+            t0 = time.perf_counter()
+            res = bp.solve(*args)
+            ms = (time.perf_counter() - t0) * 1e3
+        bp.opts = L.opts(flags=flags, stamps=st.data_ptr())
         res = bp.solve(*args)
         torch.cuda.synchronize()
-        report(st.cpu().numpy(), res["iters"], f"{name} rows {rows} ({len(cs)} agents, status {res['status'].tolist()})",
-               ms)
+        mode = "one wave per agent" if ONE_WAVE else "latency mode, four waves per agent (slot 0: residuals | factor)"
+        report(st.cpu().numpy(), res["iters"], f"{name} rows {rows} ({len(cs)} agents, status {res['status'].tolist()}; "
+               f"{mode})", ms)
 
 
 def cfg5(agents):
