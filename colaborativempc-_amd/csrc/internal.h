@@ -23,7 +23,8 @@ struct MpcConst {
     int ldk;    // leading dimension of the LDS Hessian (odd)
     int max_iter;
     int riccati;  // 1: stage-wise Riccati kernel (fp64, N*nu > 64 or CMPC_FLAG_RICCATI)
-    int rescue;   // 1: CMPC_FLAG_RESCUE on a condensed solve (Riccati re-solve of broken-down agents)
+    int rescue;   // 1: CMPC_FLAG_RESCUE on a condensed solve (Riccati re-solve of broken-down agents); 2: its
+                  // cold second pass; 3: the fp32 path's fp64 pass over the agents short of tol (mpc_launch)
     int lpv;      // 1: data made by lpv_build.hip with Q diagonal (the v3 kernel's LS layout applies); 2: and Q zero
                   // on states 1, 2, 5, 6 (the LS kernel's L5 contraction, the reference's config_LPV.py:7)
     int finish;   // 1: CMPC_FLAG_FINISH (rescue also continues breakdowns at the rounding floor)

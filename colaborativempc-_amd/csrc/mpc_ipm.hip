@@ -818,7 +818,18 @@ hipError_t mpc_launch(const MpcConst& c_in, const MpcPtrs& p, int batch, hipStre
     MpcConst c = c_in;
     c.ws_stride = p.ws ? mpc_ws_doubles(c) : 0;
     if (c.lane) return mpc_lane_launch(c, p, batch, s);
-    if (c.riccati) return mpc_riccati_launch(c, p, batch, s);
+    if (c.riccati) {
+        hipError_t er = mpc_riccati_launch(c, p, batch, s);
+        if (er != hipSuccess || !c.f32 || !p.status || !p.ws) return er;
+        // the fp32 path (Cfg::F32): an agent still short of tol after its in-launch fp64 restart gets the
+        // fp64 kernel of the fp64 path at tol * 1e-3 (its floor the requested tol); every other workgroup
+        // returns at once (rescue 3)
+        MpcConst c64 = c;
+        c64.f32 = 0;
+        c64.tol = c.tol * 1e-3;
+        c64.rescue = 3;
+        return mpc_riccati_launch(c64, p, batch, s);
+    }
     hipError_t e;
     if (flags & CMPC_FLAG_GENERIC || !mpc3_try_launch(c, p, batch, s, &e)) {
         switch (c.npad / 16) {

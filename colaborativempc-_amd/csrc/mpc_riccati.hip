@@ -58,6 +58,11 @@ constexpr int kDdStall = 2;
 // Cfg::F32: an agent leaves fp32 for good after this many iterations without a new best iterate
 // (or at an fp32 factorisation breakdown) — the lane kernel's kF32Stall (lane_body.h)
 constexpr int kRicF32Stall = 2;
+// rescue 3 (the fp32 path's last pass, mpc_launch): th capped here — on the one BASELINE cfg5 QP where every
+// fp64 variant broke down at ~27 iterations with th ~ 1e25 (tools/f32_capture.py, round 6), the capped
+// solve reaches KKT 6.9e-9 in 40 iterations without a breakdown (oracle RIC_F32 lab: 1e16 4.5e-8, 1e15
+// 4.3e-7) — and it stops at the KKT bar (kkt < the requested tol: status 2 when the merit is not below it)
+constexpr double kThCapLast = 1e17;
 #ifndef RIC_P1
 #define RIC_P1 1
 #endif
@@ -1607,17 +1612,19 @@ __device__ __forceinline__ bool riccati_back_piped(const MpcConst& c, const doub
     if (l < NA) pv[l] = (l < NX) ? ybC[N * NX + l] : 0.0;
     wsync();
     bool okw = true;
-    for (int k = N - 1; k >= 0; --k) {
-        // A_k, B_k: kernel inputs, never written — loaded before the waits
+    // A_k, B_k (kernel inputs, never written) prefetched one stage ahead into two register sets (a stage
+    // that waited on its own loads ran at ~3 k clk, slower than the factorisation it follows)
+    auto load = [&](int k, double (&bm)[NX][NU], double (&ac)[NX]) __attribute__((always_inline)) {
         const double* Ak = A + (size_t)k * NX * NX;
         const double* Bk = B + (size_t)k * NX * NU;
-        double bm[NX][NU], ac[NX];
 #pragma unroll
         for (int s2 = 0; s2 < NX; ++s2) {
 #pragma unroll
             for (int a = 0; a < NU; ++a) bm[s2][a] = Bk[s2 * NU + a];
             ac[s2] = Ak[s2 * NX + lx];
         }
+    };
+    auto stage = [&](int k, const double (&bm)[NX][NU], const double (&ac)[NX]) __attribute__((always_inline)) {
         okw = spin_until(prog_a, (double)(N - k)) && okw;
         okw = spin_until(prog_f, (double)(N - k)) && okw;
         const double* Kg = ring + (k % kRing) * sF;
@@ -1661,6 +1668,15 @@ __device__ __forceinline__ bool riccati_back_piped(const MpcConst& c, const doub
         }
         wsync();
         if (l == 0) *cons = (double)(N - k);
+    };
+    double bm0[NX][NU], ac0[NX], bm1[NX][NU], ac1[NX];
+    load(N - 1, bm0, ac0);
+    for (int k = N - 1; k >= 0; k -= 2) {
+        if (k >= 1) load(k - 1, bm1, ac1);
+        stage(k, bm0, ac0);
+        if (k < 1) break;
+        if (k >= 2) load(k - 2, bm0, ac0);
+        stage(k - 1, bm1, ac1);
     }
     return okw;
 }
@@ -1810,11 +1826,16 @@ __global__ __launch_bounds__(kWave) void mpc_riccati_kernel(const MpcConst c_arg
     extern __shared__ __attribute__((aligned(16))) double sm[];
     // launch order (cmpc_opts.order): clamped into range, so a bad entry cannot address outside the batch
     const int b = P.order ? min(max(P.order[blockIdx.x], 0), (int)gridDim.x - 1) : (int)blockIdx.x;
-    if (c_arg.rescue) {  // rescue pass: agents handed over at a breakdown, or left CMPC_UNSOLVED, only
+    if (c_arg.rescue == 3) {  // the fp32 path's fp64 pass (mpc_launch): the agents it left short of tol only
+        if (P.status[b] == CMPC_SOLVED) return;
+    } else if (c_arg.rescue) {  // rescue pass: agents handed over at a breakdown, or left CMPC_UNSOLVED, only
         const RGlb g0 = r_glb(c_arg);
         if (P.ws[(size_t)b * g0.total + g0.hand] != 1.0 && P.status[b] != CMPC_UNSOLVED) return;
     }
     const int l = threadIdx.x;
+    // rescue 3 runs at tol * 1e-3 of the fp32 solve's tol: its rounding floor is the requested tol
+    const double tol_req = c_arg.rescue == 3 ? 1e3 * c_arg.tol : c_arg.tol;
+    const int it_prev = (c_arg.rescue == 3 && P.iters) ? P.iters[b] : 0;
     const RLds L = r_layout(c_arg);
     // the weights are indexed by lane-dependent expressions: read them from an LDS copy (a
     // kernel-argument struct indexed that way is materialised in scratch)
@@ -1879,10 +1900,12 @@ __global__ __launch_bounds__(kWave) void mpc_riccati_kernel(const MpcConst c_arg
     // (hand_doubles, internal.h), or start cold; the flag is consumed here, so a second rescue
     // pass over an agent this one leaves CMPC_UNSOLVED starts cold
     double* hand = ws + gl.hand;
-    const bool warm = c_arg.rescue && hand[0] == 1.0;
+    const bool warm = (c_arg.rescue == 1 || c_arg.rescue == 2) && hand[0] == 1.0;
     // double-double near the solution: a continued (rescue) solve from the start, a cold one only
     // once the fp64 recursion stops making progress or breaks down (kDdStall)
-    bool dd_on = warm;
+    // (rescue 3, the fp32 path's last pass: double-double at every iteration above kDdTh from the start —
+    // the robust rule of round 2 — for the agents whose fp32 solve and its fp64 restart both stopped short)
+    bool dd_on = warm || c_arg.rescue == 3;
     bool f32_on = G::F32 && !warm;  // Cfg::F32: fp32 factorisation and recursions until kRicF32Stall
     const int it0 = warm ? (int)hand[1] : 0;
     if (warm) {
@@ -1912,6 +1935,7 @@ __global__ __launch_bounds__(kWave) void mpc_riccati_kernel(const MpcConst c_arg
     // oracle RIC_F32).  `tol` is the attempt's tolerance, it_done the iterations of the first attempt.
     double tol = c.tol;
     int it_done = 0;
+    bool kkt_stop = false;  // rescue 3 stopped at kkt < the requested tol (merit not below it)
     double best_m, best_kkt, kkt;
     int best_it, stop, it;
     for (int attempt = 0;; ++attempt) {
@@ -2062,6 +2086,11 @@ __global__ __launch_bounds__(kWave) void mpc_riccati_kernel(const MpcConst c_arg
             stop = kStopConverged;
             break;
         }
+        if (c_arg.rescue == 3 && kkt < tol_req) {  // the last pass stops at the KKT bar (status 2 below)
+            kkt_stop = true;
+            stop = kStopConverged;
+            break;
+        }
         if (best_m < 1e3 * tol && it - best_it >= kStallIters) {
             stop = kStopStalled;
             break;
@@ -2086,7 +2115,7 @@ __global__ __launch_bounds__(kWave) void mpc_riccati_kernel(const MpcConst c_arg
 #pragma unroll
             for (int i = 0; i < kRowChunk; ++i) {
                 const int r = r0 + i * kWave;
-                if (r < m) th[r] = isfinite(wv[i]) ? lv[i] / tv[i] : 0.0;
+                if (r < m) th[r] = isfinite(wv[i]) ? (c_arg.rescue == 3 ? fmin(lv[i] / tv[i], kThCapLast) : lv[i] / tv[i]) : 0.0;
             }
         }
         wsync();
@@ -2401,7 +2430,7 @@ __global__ __launch_bounds__(kWave) void mpc_riccati_kernel(const MpcConst c_arg
     }
     break;
     }
-    int status = CMPC_SOLVED;
+    int status = kkt_stop ? CMPC_SOLVED_INACCURATE : CMPC_SOLVED;
     // polish (CMPC_FLAG_POLISH): a rescue-pass solve that stops short of tol for the last time — status 2 or
     // -2, or anything on the second (cold) pass, rescue == 2 — leaves its last iterate in the rescue image
     // with flag 2 and its best merit (mpc_polish.hip)
@@ -2427,7 +2456,7 @@ __global__ __launch_bounds__(kWave) void mpc_riccati_kernel(const MpcConst c_arg
             kkt = best_kkt;
         }
         // (an fp64 restart that ends with its best merit below the requested tol has met it)
-        status = (it_done && best_m < c.tol) ? CMPC_SOLVED : stop_status(stop, best_m, c.tol);
+        status = ((it_done || c_arg.rescue == 3) && best_m < tol_req) ? CMPC_SOLVED : stop_status(stop, best_m, tol_req);
     }
     wsync();
 
@@ -2447,7 +2476,7 @@ __global__ __launch_bounds__(kWave) void mpc_riccati_kernel(const MpcConst c_arg
     }
     if (l == 0) {
         if (P.kkt) P.kkt[b] = kkt;
-        if (P.iters) P.iters[b] = it_done + it;
+        if (P.iters) P.iters[b] = it_prev + it_done + it;
         if (P.status) P.status[b] = status;
     }
     RSTAMP(14);
@@ -2491,6 +2520,260 @@ __host__ __device__ inline RLds r_layout_mw(const MpcConst& c) {
     L.ring = L.red + 16;
     L.total = L.ring + ((kRing * d.sF + 1) & ~1);
     return L;
+}
+
+// ---- latency mode: the solve passes in segments (parallel in time) ----
+// The Newton solve's two passes are linear recursions on y_k = [dX_k; dU_{k-1}] once the gains are known:
+//   forward  y_{k+1} = M_k y_k + [B_k kk_k; kk_k],   M_k = [[A_k + B_k Kx_k, B_k Ku_k]; [Kx_k, Ku_k]]
+//   backward p_k = M_k' p_{k+1} + [yb_k; 0] + K_k' r0_k   (kk_k = -Hinv_k g_k, g_k = p_u + r0_k + B_k' p_x)
+// With the horizon cut into kSeg segments [a_q, a_{q+1}) (one per wavefront), a pass runs every segment
+// from a zero boundary value at once (the first forward / last backward segment from its true one), carries
+// the boundary values across the segments through each segment's transition Phi_q = M_{b-1} ... M_a
+// (formed once per iteration, beside pass 0's forward run), and runs the segments again from their true
+// boundary values: 2 N / kSeg + kSeg stage steps instead of N.  The same arithmetic per stage as
+// riccati_solve; the boundary values round differently (the iterates are not bit-identical to one wave).
+constexpr int kSeg = 4;
+__device__ __forceinline__ int seg_a(int q, int N) { return (q * N) / kSeg; }
+
+template <class G>
+struct SegIO {
+    const double* A;
+    const double* B;
+    const double* F;  // gains K_k | Hinv_k (global, the factorisation's)
+    int sF;
+};
+
+// forward run over [a, b) from yin (NA values; null: zero), y ping-pong in ybuf (2 NA); wr: write
+// dX_{k+1} (and dX_a = yin's x when a == 0) and dU_k = v_k; yout (if set): the end state; phi (if set):
+// Phi built alongside in phi[0, 2 NA^2) with Z in phi[2 NA^2, + NU NA), the result copied to phi_out
+template <class G>
+__device__ __forceinline__ void seg_forward(const SegIO<G>& io, int a, int b, const double* yin, double* ybuf,
+                                            double* dX, double* dU, bool wr, double* yout, double* phi,
+                                            double* phi_out) {
+    constexpr int NX = G::NX, NU = G::NU, NA = NX + NU, NP = NA * NA;
+    const int l = lane_id(), lx = l < NX ? l : NX - 1;
+    if (l < NA) ybuf[l] = yin ? yin[l] : 0.0;
+    if (wr && a == 0 && l < NX) dX[l] = 0.0;
+    if (phi)
+        for (int e = l; e < NP; e += kWave) phi[e] = (e / NA == e % NA) ? 1.0 : 0.0;
+    wsync();
+    // phi rows of this lane's two entries
+    const int e0 = l, e1 = l + kWave < NP ? l + kWave : NP - 1;
+    const int i0 = e0 / NA, i1 = e1 / NA;
+    const int ri0 = i0 < NX ? i0 : 0, ri1 = i1 < NX ? i1 : 0;
+    // the stage's gains and A_k / B_k rows prefetched one stage ahead (two register sets, the loop unrolled by
+    // two): a step that waited on its own global loads cost ~1.4 k clk
+    struct SF {
+        double kg[NU][NA], ar[NX], br[NU];
+    };
+    auto load = [&](int k, SF& f) __attribute__((always_inline)) {
+        const double* Ak = io.A + (size_t)k * NX * NX;
+        const double* Bk = io.B + (size_t)k * NX * NU;
+        const double* Kg = io.F + (size_t)k * io.sF;
+#pragma unroll
+        for (int q = 0; q < NU; ++q) {
+#pragma unroll
+            for (int j = 0; j < NA; ++j) f.kg[q][j] = Kg[q * NA + j];
+            f.br[q] = Bk[lx * NU + q];
+        }
+#pragma unroll
+        for (int t = 0; t < NX; ++t) f.ar[t] = Ak[lx * NX + t];
+    };
+    auto step = [&](int k, const SF& f) __attribute__((always_inline)) {
+        const double* Ak = io.A + (size_t)k * NX * NX;
+        const double* Bk = io.B + (size_t)k * NX * NU;
+        const double* Kg = io.F + (size_t)k * io.sF;
+        const double* xc = ybuf + ((k - a) & 1) * NA;
+        double* xn = ybuf + ((k - a + 1) & 1) * NA;
+        double x[NX], up[NU], d0[NU];
+#pragma unroll
+        for (int q = 0; q < NU; ++q) {
+            d0[q] = dU[k * NU + q];
+            up[q] = xc[NX + q];
+        }
+#pragma unroll
+        for (int t = 0; t < NX; ++t) x[t] = xc[t];
+        __builtin_amdgcn_sched_barrier(0);
+        double vk[NU];
+#pragma unroll
+        for (int q = 0; q < NU; ++q) {
+            double v = d0[q];
+#pragma unroll
+            for (int j = 0; j < NX; ++j) v = fma(f.kg[q][j], x[j], v);
+            if (k > 0)
+#pragma unroll
+                for (int r = 0; r < NU; ++r) v = fma(f.kg[q][NX + r], up[r], v);
+            vk[q] = v;
+        }
+        double v = 0.0;
+#pragma unroll
+        for (int t = 0; t < NX; ++t) v = fma(f.ar[t], x[t], v);
+#pragma unroll
+        for (int q = 0; q < NU; ++q) v = fma(f.br[q], vk[q], v);
+        if (l < NX) {
+            xn[l] = v;
+            if (wr) dX[(k + 1) * NX + l] = v;
+        } else if (l < NA) {
+            xn[l] = vk[l - NX];
+        }
+#pragma unroll
+        for (int q = 0; q < NU; ++q)
+            if (wr && l == q) dU[k * NU + q] = vk[q];
+        if (phi) {  // Phi <- M_k Phi:  Z = K Phi;  Phi[i][j] = sum_t A[i][t] Phi[t][j] + sum_q B[i][q] Z[q][j] (i < nx), Z
+            const double* Pc = phi + ((k - a) & 1) * NP;
+            double* Pn = phi + ((k - a + 1) & 1) * NP;
+            double* Z = phi + 2 * NP;
+            if (l < NU * NA) {
+                const int q = l / NA, j = l - q * NA;
+                double z = 0.0;
+#pragma unroll
+                for (int s2 = 0; s2 < NA; ++s2) z = fma(Kg[q * NA + s2], Pc[s2 * NA + j], z);
+                Z[l] = z;
+            }
+            wsync();
+            double a0[NX], a1[NX], b0[NU], b1[NU];
+#pragma unroll
+            for (int t = 0; t < NX; ++t) {
+                a0[t] = Ak[ri0 * NX + t];
+                a1[t] = Ak[ri1 * NX + t];
+            }
+#pragma unroll
+            for (int q = 0; q < NU; ++q) {
+                b0[q] = Bk[ri0 * NU + q];
+                b1[q] = Bk[ri1 * NU + q];
+            }
+            const int j0 = e0 - i0 * NA, j1 = e1 - i1 * NA;
+            double w0 = 0.0, w1 = 0.0;
+            if (i0 < NX) {
+#pragma unroll
+                for (int t = 0; t < NX; ++t) w0 = fma(a0[t], Pc[t * NA + j0], w0);
+#pragma unroll
+                for (int q = 0; q < NU; ++q) w0 = fma(b0[q], Z[q * NA + j0], w0);
+            } else {
+                w0 = Z[(i0 - NX) * NA + j0];
+            }
+            if (i1 < NX) {
+#pragma unroll
+                for (int t = 0; t < NX; ++t) w1 = fma(a1[t], Pc[t * NA + j1], w1);
+#pragma unroll
+                for (int q = 0; q < NU; ++q) w1 = fma(b1[q], Z[q * NA + j1], w1);
+            } else {
+                w1 = Z[(i1 - NX) * NA + j1];
+            }
+            Pn[e0] = w0;
+            if (l + kWave < NP) Pn[e1] = w1;
+        }
+        wsync();
+    };
+    SF f0, f1;
+    if (a < b) load(a, f0);
+    for (int k = a; k < b; k += 2) {
+        if (k + 1 < b) load(k + 1, f1);
+        step(k, f0);
+        if (k + 1 >= b) break;
+        if (k + 2 < b) load(k + 2, f0);
+        step(k + 1, f1);
+    }
+    if (yout && l < NA) yout[l] = ybuf[((b - a) & 1) * NA + l];
+    if (phi && phi_out)
+        for (int e = l; e < NP; e += kWave) phi_out[e] = phi[((b - a) & 1) * NP + e];
+    wsync();
+}
+
+// backward run over [a, b) from pin (NA values at stage b; null: zero); p ping-pong in pbuf (2 NA); r0 from
+// (rd, rt) and the state term from yb (riccati_solve's pass-1 right-hand side); wr: write dU_k = kk_k;
+// pout (if set): p_a
+template <class G>
+__device__ __forceinline__ void seg_backward(const SegIO<G>& io, int a, int b, const double* pin, double* pbuf,
+                                             const double* yb, const double* rd, const double* rt, int ms,
+                                             double* dU, bool wr, double* pout) {
+    constexpr int NX = G::NX, NU = G::NU, NA = NX + NU;
+    const int l = lane_id();
+    const int lx = l < NX ? l : NX - 1, la = l < NA ? l : NA - 1, lu = l < NU ? l : NU - 1;
+    if (l < NA) pbuf[l] = pin ? pin[l] : 0.0;
+    wsync();
+    struct SB {
+        double bm[NX][NU], ac[NX], kg[NU], hg[NU];
+    };
+    auto load = [&](int k, SB& f) __attribute__((always_inline)) {
+        const double* Ak = io.A + (size_t)k * NX * NX;
+        const double* Bk = io.B + (size_t)k * NX * NU;
+        const double* Kg = io.F + (size_t)k * io.sF;
+        const double* Hg = Kg + NU * NA;
+#pragma unroll
+        for (int s2 = 0; s2 < NX; ++s2) {
+#pragma unroll
+            for (int q = 0; q < NU; ++q) f.bm[s2][q] = Bk[s2 * NU + q];
+            f.ac[s2] = Ak[s2 * NX + lx];
+        }
+#pragma unroll
+        for (int q = 0; q < NU; ++q) {
+            f.kg[q] = Kg[q * NA + la];
+            f.hg[q] = Hg[lu * NU + q];
+        }
+    };
+    auto step = [&](int k, const SB& f) __attribute__((always_inline)) {
+        const double* pc = pbuf + ((b - 1 - k) & 1) * NA;
+        double* pn = pbuf + ((b - k) & 1) * NA;
+        double p[NA], r0[NU];
+#pragma unroll
+        for (int q = 0; q < NU; ++q) {
+            const int ci = k * NU + q;
+            r0[q] = rd[ci] + (rt[ms + 2 * ci] - rt[ms + 2 * ci + 1]);
+        }
+        const double y0 = (l < NX) ? yb[k * NX + l] : 0.0;
+#pragma unroll
+        for (int s2 = 0; s2 < NA; ++s2) p[s2] = pc[s2];
+        __builtin_amdgcn_sched_barrier(0);
+        double g[NU];
+#pragma unroll
+        for (int q = 0; q < NU; ++q) {
+            double v = p[NX + q] + r0[q];
+#pragma unroll
+            for (int s2 = 0; s2 < NX; ++s2) v = fma(f.bm[s2][q], p[s2], v);
+            g[q] = v;
+        }
+        double v = y0;
+        if (l < NX) {
+#pragma unroll
+            for (int s2 = 0; s2 < NX; ++s2) v = fma(f.ac[s2], p[s2], v);
+        }
+#pragma unroll
+        for (int q = 0; q < NU; ++q) v = fma(f.kg[q], g[q], v);
+        if (l < NA) pn[l] = v;
+        if (wr && l < NU) {
+            double u = 0.0;
+#pragma unroll
+            for (int q = 0; q < NU; ++q) u = fma(-f.hg[q], g[q], u);
+            dU[k * NU + l] = u;
+        }
+        wsync();
+    };
+    SB f0, f1;
+    if (a < b) load(b - 1, f0);
+    for (int k = b - 1; k >= a; k -= 2) {
+        if (k - 1 >= a) load(k - 1, f1);
+        step(k, f0);
+        if (k - 1 < a) break;
+        if (k - 2 >= a) load(k - 2, f0);
+        step(k - 1, f1);
+    }
+    if (pout && l < NA) pout[l] = pbuf[((b - a) & 1) * NA + l];
+    wsync();
+}
+
+// out = base + Phi v (trans: Phi' v), NA lanes
+template <int NA>
+__device__ __forceinline__ void seg_carry(const double* Phi, const double* v, const double* base, double* out,
+                                          bool trans) {
+    const int l = lane_id();
+    if (l < NA) {
+        double s = base[l];
+#pragma unroll
+        for (int j = 0; j < NA; ++j) s = fma(trans ? Phi[j * NA + l] : Phi[l * NA + j], v[j], s);
+        out[l] = s;
+    }
+    wsync();
 }
 
 // rt of the rows (the slack groups' Schur form of rho; mpc_riccati_kernel's loop) over nt threads
@@ -2872,7 +3155,56 @@ __global__ __launch_bounds__(kMW * kWave) void mpc_riccati_mw_kernel(const MpcCo
             }
             const double* yrt = pass ? yb : ybC;
             MSTAMP(4);
-            if (wv == 0) {  // the Newton solve: serial in the stages
+#ifdef RIC_MW_NOSEG  // lab: the solve passes serial on wave 0
+            constexpr bool kSegOn = false;
+#else
+            constexpr bool kSegOn = true;
+#endif
+            if (kSegOn && !hp) {  // the passes in kSeg segments, one per wave (seg_forward / seg_backward above)
+                constexpr int NA = NX + G::NU, NP = NA * NA;
+                double* sg = GdU;                   // scratch (GdU is rebuilt after the solve): per-wave ping-pongs,
+                double* ybuf = sg + wv * 2 * NA;    // boundary values, Phi's build
+                double* yhat = sg + kSeg * 2 * NA;  // zero-start forward runs: end states of segments 0..2
+                double* ya = yhat + 3 * NA;         // true start states of segments 1..3
+                double* phat = ya + 3 * NA;         // zero-end backward runs: start values of segments 1..3
+                double* pb = phat + 3 * NA;         // true end values of segments 0..2
+                double* pN = pb + 3 * NA;
+                double* phb = pN + NA;              // Phi build (waves 1, 2), 2 NP + NU NA each
+                double* Phi = rh;                   // Phi_1, Phi_2 (rh: free in an fp64 iteration), pass 0 -> pass 1
+                const SegIO<G> io{A, B, F, d.sF};
+                const int aq = seg_a(wv, N), bq = seg_a(wv + 1, N);
+                if (pass) {  // the backward pass (pass 0's ran piped beside the factorisation)
+                    if (wv == kSeg - 1 && l < NA) pN[l] = l < NX ? yrt[N * NX + l] : 0.0;
+                    wsync();
+                    seg_backward<G>(io, aq, bq, wv == kSeg - 1 ? pN : nullptr, ybuf, yrt, rd, rt, ms, dU, wv == kSeg - 1,
+                                    wv >= 1 ? phat + (wv - 1) * NA : nullptr);
+                    __syncthreads();
+                    if (wv == 0) {
+                        if (l < NA) pb[2 * NA + l] = phat[2 * NA + l];  // p_{a_3}: segment 3 ran from the true p_N
+                        wsync();
+                        seg_carry<NA>(Phi + NP, pb + 2 * NA, phat + NA, pb + NA, true);
+                        seg_carry<NA>(Phi, pb + NA, phat, pb, true);
+                    }
+                    __syncthreads();
+                    if (wv < kSeg - 1) seg_backward<G>(io, aq, bq, pb + wv * NA, ybuf, yrt, rd, rt, ms, dU, true, nullptr);
+                    __syncthreads();
+                } else if (!piped) {
+                    if (wv == 0) riccati_solve<G>(c, d, L, sm, A, B, F, nullptr, dU, dX, yrt, rd, rt, 1);
+                    __syncthreads();
+                }
+                seg_forward<G>(io, aq, bq, nullptr, ybuf, dX, dU, wv == 0, wv < kSeg - 1 ? yhat + wv * NA : nullptr,
+                               (!pass && (wv == 1 || wv == 2)) ? phb + (wv - 1) * (2 * NP + G::NU * NA) : nullptr,
+                               Phi + (wv - 1) * NP);
+                __syncthreads();
+                if (wv == 0) {
+                    if (l < NA) ya[l] = yhat[l];  // y_{a_1}: segment 0 ran from the true y_0
+                    wsync();
+                    seg_carry<NA>(Phi, ya, yhat + NA, ya + NA, false);
+                    seg_carry<NA>(Phi + NP, ya + NA, yhat + 2 * NA, ya + 2 * NA, false);
+                }
+                __syncthreads();
+                if (wv >= 1) seg_forward<G>(io, aq, bq, ya + (wv - 1) * NA, ybuf, dX, dU, true, nullptr, nullptr, nullptr);
+            } else if (wv == 0) {  // the Newton solve: serial in the stages
                 if (!hp) {  // (pass 0 with wave 2's backward pass: the forward pass only)
                     riccati_solve<G>(c, d, L, sm, A, B, F, nullptr, dU, dX, yrt, rd, rt, (!pass && piped) ? 2 : 3);
                 } else {

@@ -1450,6 +1450,7 @@ done:
    tol; an end with the best merit below the requested tol (f32_req) counts as solved */
 static _Thread_local int f32_no = 0;
 static _Thread_local double f32_req = 0.0;
+static _Thread_local int f32_dd = 0;   /* the last pass (mpc_launch rescue 3): double-double from the start */
 long cmpc_f32_restarts = 0;
 #endif
 static int solve_one_base(const shared_t* S, const agent_t* a, double tol, int max_iter, work_t* wk,
@@ -1467,9 +1468,16 @@ static int solve_one(const shared_t* S, const agent_t* a, double tol, int max_it
         f32_no = 1;
         f32_req = tol;
         st = solve_one_base(S, a, tol * 1e-3, max_iter, wk, z, kkt_out, iters_out);
+        *iters_out += it1;
+        if (st != 1) {  /* ... and still short: the fp64 kernel's pass with double-double from the start */
+            const int it2 = *iters_out;
+            f32_dd = 1;
+            st = solve_one_base(S, a, tol * 1e-3, max_iter, wk, z, kkt_out, iters_out);
+            f32_dd = 0;
+            *iters_out += it2;
+        }
         f32_no = 0;
         f32_req = 0.0;
-        *iters_out += it1;
     }
 #endif
     return st;
@@ -1612,6 +1620,10 @@ static int solve_one_base(const shared_t* S, const agent_t* a, double tol, int m
 #define DD_STALL 2           /* kDdStall of mpc_riccati.hip */
 #endif
     int dd_on = 0;           /* newton 3: this solve has switched to double-double near the solution */
+    int kkt_stop = 0;        /* lab RIC_F32 last pass: stopped at kkt < the requested tol */
+#ifdef RIC_F32
+    dd_on = f32_dd;
+#endif
 #ifdef LAB_SIGMA2
     /* lab: a second corrector with another centring parameter per iteration (a second wavefront's
        work in a two-wave kernel); the longer step wins, ties to the first */
@@ -1730,6 +1742,9 @@ static int solve_one_base(const shared_t* S, const agent_t* a, double tol, int m
         }
 #endif
         if (merit < tol) { stop = 1; break; }
+#ifdef RIC_F32
+        if (f32_dd && kkt < f32_req) { stop = 1; kkt_stop = 1; break; }  /* the last pass: at the KKT bar */
+#endif
         /* near-converged but no progress for STALL_ITERS iterations: rounding floor reached */
         if (best_m < 1e3 * tol && it - best_it >= STALL_ITERS) {
             stop = 3;
@@ -1745,6 +1760,10 @@ static int solve_one_base(const shared_t* S, const agent_t* a, double tol, int m
         /* ---- Newton matrix ---- */
         int hp = 0; /* Riccati: this iteration factors in double-double (newton == 3) */
         for (int r = 0; r < m; ++r) wk->th[r] = wk->act[r] ? lam[r] / t[r] : 0.0;
+#ifdef RIC_F32
+        if (f32_dd)  /* the last pass: th capped (kThCapLast of mpc_riccati.hip) */
+            for (int r = 0; r < m; ++r) wk->th[r] = fmin(wk->th[r], 1e17);
+#endif
 #ifdef THMAX
         for (int r = 0; r < m; ++r) wk->th[r] = fmin(wk->th[r], THMAX);
 #endif
@@ -2337,7 +2356,7 @@ static int solve_one_base(const shared_t* S, const agent_t* a, double tol, int m
 #endif
     int status;
     if (stop == 1 && !(degen && pol_m < best_m)) {
-        status = 1;
+        status = kkt_stop ? 2 : 1;
     } else if (pol_m < best_m && pol_m < 1e3 * tol) { /* (mpc_polish.hip: never promotes past the floor) */
         memcpy(U, wk->dU, sizeof(double) * n);
         memcpy(sig, wk->dsig, sizeof(double) * N * ns);
