@@ -2522,260 +2522,6 @@ __host__ __device__ inline RLds r_layout_mw(const MpcConst& c) {
     return L;
 }
 
-// ---- latency mode: the solve passes in segments (parallel in time) ----
-// The Newton solve's two passes are linear recursions on y_k = [dX_k; dU_{k-1}] once the gains are known:
-//   forward  y_{k+1} = M_k y_k + [B_k kk_k; kk_k],   M_k = [[A_k + B_k Kx_k, B_k Ku_k]; [Kx_k, Ku_k]]
-//   backward p_k = M_k' p_{k+1} + [yb_k; 0] + K_k' r0_k   (kk_k = -Hinv_k g_k, g_k = p_u + r0_k + B_k' p_x)
-// With the horizon cut into kSeg segments [a_q, a_{q+1}) (one per wavefront), a pass runs every segment
-// from a zero boundary value at once (the first forward / last backward segment from its true one), carries
-// the boundary values across the segments through each segment's transition Phi_q = M_{b-1} ... M_a
-// (formed once per iteration, beside pass 0's forward run), and runs the segments again from their true
-// boundary values: 2 N / kSeg + kSeg stage steps instead of N.  The same arithmetic per stage as
-// riccati_solve; the boundary values round differently (the iterates are not bit-identical to one wave).
-constexpr int kSeg = 4;
-__device__ __forceinline__ int seg_a(int q, int N) { return (q * N) / kSeg; }
-
-template <class G>
-struct SegIO {
-    const double* A;
-    const double* B;
-    const double* F;  // gains K_k | Hinv_k (global, the factorisation's)
-    int sF;
-};
-
-// forward run over [a, b) from yin (NA values; null: zero), y ping-pong in ybuf (2 NA); wr: write
-// dX_{k+1} (and dX_a = yin's x when a == 0) and dU_k = v_k; yout (if set): the end state; phi (if set):
-// Phi built alongside in phi[0, 2 NA^2) with Z in phi[2 NA^2, + NU NA), the result copied to phi_out
-template <class G>
-__device__ __forceinline__ void seg_forward(const SegIO<G>& io, int a, int b, const double* yin, double* ybuf,
-                                            double* dX, double* dU, bool wr, double* yout, double* phi,
-                                            double* phi_out) {
-    constexpr int NX = G::NX, NU = G::NU, NA = NX + NU, NP = NA * NA;
-    const int l = lane_id(), lx = l < NX ? l : NX - 1;
-    if (l < NA) ybuf[l] = yin ? yin[l] : 0.0;
-    if (wr && a == 0 && l < NX) dX[l] = 0.0;
-    if (phi)
-        for (int e = l; e < NP; e += kWave) phi[e] = (e / NA == e % NA) ? 1.0 : 0.0;
-    wsync();
-    // phi rows of this lane's two entries
-    const int e0 = l, e1 = l + kWave < NP ? l + kWave : NP - 1;
-    const int i0 = e0 / NA, i1 = e1 / NA;
-    const int ri0 = i0 < NX ? i0 : 0, ri1 = i1 < NX ? i1 : 0;
-    // the stage's gains and A_k / B_k rows prefetched one stage ahead (two register sets, the loop unrolled by
-    // two): a step that waited on its own global loads cost ~1.4 k clk
-    struct SF {
-        double kg[NU][NA], ar[NX], br[NU];
-    };
-    auto load = [&](int k, SF& f) __attribute__((always_inline)) {
-        const double* Ak = io.A + (size_t)k * NX * NX;
-        const double* Bk = io.B + (size_t)k * NX * NU;
-        const double* Kg = io.F + (size_t)k * io.sF;
-#pragma unroll
-        for (int q = 0; q < NU; ++q) {
-#pragma unroll
-            for (int j = 0; j < NA; ++j) f.kg[q][j] = Kg[q * NA + j];
-            f.br[q] = Bk[lx * NU + q];
-        }
-#pragma unroll
-        for (int t = 0; t < NX; ++t) f.ar[t] = Ak[lx * NX + t];
-    };
-    auto step = [&](int k, const SF& f) __attribute__((always_inline)) {
-        const double* Ak = io.A + (size_t)k * NX * NX;
-        const double* Bk = io.B + (size_t)k * NX * NU;
-        const double* Kg = io.F + (size_t)k * io.sF;
-        const double* xc = ybuf + ((k - a) & 1) * NA;
-        double* xn = ybuf + ((k - a + 1) & 1) * NA;
-        double x[NX], up[NU], d0[NU];
-#pragma unroll
-        for (int q = 0; q < NU; ++q) {
-            d0[q] = dU[k * NU + q];
-            up[q] = xc[NX + q];
-        }
-#pragma unroll
-        for (int t = 0; t < NX; ++t) x[t] = xc[t];
-        __builtin_amdgcn_sched_barrier(0);
-        double vk[NU];
-#pragma unroll
-        for (int q = 0; q < NU; ++q) {
-            double v = d0[q];
-#pragma unroll
-            for (int j = 0; j < NX; ++j) v = fma(f.kg[q][j], x[j], v);
-            if (k > 0)
-#pragma unroll
-                for (int r = 0; r < NU; ++r) v = fma(f.kg[q][NX + r], up[r], v);
-            vk[q] = v;
-        }
-        double v = 0.0;
-#pragma unroll
-        for (int t = 0; t < NX; ++t) v = fma(f.ar[t], x[t], v);
-#pragma unroll
-        for (int q = 0; q < NU; ++q) v = fma(f.br[q], vk[q], v);
-        if (l < NX) {
-            xn[l] = v;
-            if (wr) dX[(k + 1) * NX + l] = v;
-        } else if (l < NA) {
-            xn[l] = vk[l - NX];
-        }
-#pragma unroll
-        for (int q = 0; q < NU; ++q)
-            if (wr && l == q) dU[k * NU + q] = vk[q];
-        if (phi) {  // Phi <- M_k Phi:  Z = K Phi;  Phi[i][j] = sum_t A[i][t] Phi[t][j] + sum_q B[i][q] Z[q][j] (i < nx), Z
-            const double* Pc = phi + ((k - a) & 1) * NP;
-            double* Pn = phi + ((k - a + 1) & 1) * NP;
-            double* Z = phi + 2 * NP;
-            if (l < NU * NA) {
-                const int q = l / NA, j = l - q * NA;
-                double z = 0.0;
-#pragma unroll
-                for (int s2 = 0; s2 < NA; ++s2) z = fma(Kg[q * NA + s2], Pc[s2 * NA + j], z);
-                Z[l] = z;
-            }
-            wsync();
-            double a0[NX], a1[NX], b0[NU], b1[NU];
-#pragma unroll
-            for (int t = 0; t < NX; ++t) {
-                a0[t] = Ak[ri0 * NX + t];
-                a1[t] = Ak[ri1 * NX + t];
-            }
-#pragma unroll
-            for (int q = 0; q < NU; ++q) {
-                b0[q] = Bk[ri0 * NU + q];
-                b1[q] = Bk[ri1 * NU + q];
-            }
-            const int j0 = e0 - i0 * NA, j1 = e1 - i1 * NA;
-            double w0 = 0.0, w1 = 0.0;
-            if (i0 < NX) {
-#pragma unroll
-                for (int t = 0; t < NX; ++t) w0 = fma(a0[t], Pc[t * NA + j0], w0);
-#pragma unroll
-                for (int q = 0; q < NU; ++q) w0 = fma(b0[q], Z[q * NA + j0], w0);
-            } else {
-                w0 = Z[(i0 - NX) * NA + j0];
-            }
-            if (i1 < NX) {
-#pragma unroll
-                for (int t = 0; t < NX; ++t) w1 = fma(a1[t], Pc[t * NA + j1], w1);
-#pragma unroll
-                for (int q = 0; q < NU; ++q) w1 = fma(b1[q], Z[q * NA + j1], w1);
-            } else {
-                w1 = Z[(i1 - NX) * NA + j1];
-            }
-            Pn[e0] = w0;
-            if (l + kWave < NP) Pn[e1] = w1;
-        }
-        wsync();
-    };
-    SF f0, f1;
-    if (a < b) load(a, f0);
-    for (int k = a; k < b; k += 2) {
-        if (k + 1 < b) load(k + 1, f1);
-        step(k, f0);
-        if (k + 1 >= b) break;
-        if (k + 2 < b) load(k + 2, f0);
-        step(k + 1, f1);
-    }
-    if (yout && l < NA) yout[l] = ybuf[((b - a) & 1) * NA + l];
-    if (phi && phi_out)
-        for (int e = l; e < NP; e += kWave) phi_out[e] = phi[((b - a) & 1) * NP + e];
-    wsync();
-}
-
-// backward run over [a, b) from pin (NA values at stage b; null: zero); p ping-pong in pbuf (2 NA); r0 from
-// (rd, rt) and the state term from yb (riccati_solve's pass-1 right-hand side); wr: write dU_k = kk_k;
-// pout (if set): p_a
-template <class G>
-__device__ __forceinline__ void seg_backward(const SegIO<G>& io, int a, int b, const double* pin, double* pbuf,
-                                             const double* yb, const double* rd, const double* rt, int ms,
-                                             double* dU, bool wr, double* pout) {
-    constexpr int NX = G::NX, NU = G::NU, NA = NX + NU;
-    const int l = lane_id();
-    const int lx = l < NX ? l : NX - 1, la = l < NA ? l : NA - 1, lu = l < NU ? l : NU - 1;
-    if (l < NA) pbuf[l] = pin ? pin[l] : 0.0;
-    wsync();
-    struct SB {
-        double bm[NX][NU], ac[NX], kg[NU], hg[NU];
-    };
-    auto load = [&](int k, SB& f) __attribute__((always_inline)) {
-        const double* Ak = io.A + (size_t)k * NX * NX;
-        const double* Bk = io.B + (size_t)k * NX * NU;
-        const double* Kg = io.F + (size_t)k * io.sF;
-        const double* Hg = Kg + NU * NA;
-#pragma unroll
-        for (int s2 = 0; s2 < NX; ++s2) {
-#pragma unroll
-            for (int q = 0; q < NU; ++q) f.bm[s2][q] = Bk[s2 * NU + q];
-            f.ac[s2] = Ak[s2 * NX + lx];
-        }
-#pragma unroll
-        for (int q = 0; q < NU; ++q) {
-            f.kg[q] = Kg[q * NA + la];
-            f.hg[q] = Hg[lu * NU + q];
-        }
-    };
-    auto step = [&](int k, const SB& f) __attribute__((always_inline)) {
-        const double* pc = pbuf + ((b - 1 - k) & 1) * NA;
-        double* pn = pbuf + ((b - k) & 1) * NA;
-        double p[NA], r0[NU];
-#pragma unroll
-        for (int q = 0; q < NU; ++q) {
-            const int ci = k * NU + q;
-            r0[q] = rd[ci] + (rt[ms + 2 * ci] - rt[ms + 2 * ci + 1]);
-        }
-        const double y0 = (l < NX) ? yb[k * NX + l] : 0.0;
-#pragma unroll
-        for (int s2 = 0; s2 < NA; ++s2) p[s2] = pc[s2];
-        __builtin_amdgcn_sched_barrier(0);
-        double g[NU];
-#pragma unroll
-        for (int q = 0; q < NU; ++q) {
-            double v = p[NX + q] + r0[q];
-#pragma unroll
-            for (int s2 = 0; s2 < NX; ++s2) v = fma(f.bm[s2][q], p[s2], v);
-            g[q] = v;
-        }
-        double v = y0;
-        if (l < NX) {
-#pragma unroll
-            for (int s2 = 0; s2 < NX; ++s2) v = fma(f.ac[s2], p[s2], v);
-        }
-#pragma unroll
-        for (int q = 0; q < NU; ++q) v = fma(f.kg[q], g[q], v);
-        if (l < NA) pn[l] = v;
-        if (wr && l < NU) {
-            double u = 0.0;
-#pragma unroll
-            for (int q = 0; q < NU; ++q) u = fma(-f.hg[q], g[q], u);
-            dU[k * NU + l] = u;
-        }
-        wsync();
-    };
-    SB f0, f1;
-    if (a < b) load(b - 1, f0);
-    for (int k = b - 1; k >= a; k -= 2) {
-        if (k - 1 >= a) load(k - 1, f1);
-        step(k, f0);
-        if (k - 1 < a) break;
-        if (k - 2 >= a) load(k - 2, f0);
-        step(k - 1, f1);
-    }
-    if (pout && l < NA) pout[l] = pbuf[((b - a) & 1) * NA + l];
-    wsync();
-}
-
-// out = base + Phi v (trans: Phi' v), NA lanes
-template <int NA>
-__device__ __forceinline__ void seg_carry(const double* Phi, const double* v, const double* base, double* out,
-                                          bool trans) {
-    const int l = lane_id();
-    if (l < NA) {
-        double s = base[l];
-#pragma unroll
-        for (int j = 0; j < NA; ++j) s = fma(trans ? Phi[j * NA + l] : Phi[l * NA + j], v[j], s);
-        out[l] = s;
-    }
-    wsync();
-}
-
 // rt of the rows (the slack groups' Schur form of rho; mpc_riccati_kernel's loop) over nt threads
 template <class G>
 __device__ __forceinline__ void mw_rt(const MpcConst& c, int tid, int nt, const double* rho, const double* th,
@@ -3155,56 +2901,7 @@ __global__ __launch_bounds__(kMW * kWave) void mpc_riccati_mw_kernel(const MpcCo
             }
             const double* yrt = pass ? yb : ybC;
             MSTAMP(4);
-#ifdef RIC_MW_NOSEG  // lab: the solve passes serial on wave 0
-            constexpr bool kSegOn = false;
-#else
-            constexpr bool kSegOn = true;
-#endif
-            if (kSegOn && !hp) {  // the passes in kSeg segments, one per wave (seg_forward / seg_backward above)
-                constexpr int NA = NX + G::NU, NP = NA * NA;
-                double* sg = GdU;                   // scratch (GdU is rebuilt after the solve): per-wave ping-pongs,
-                double* ybuf = sg + wv * 2 * NA;    // boundary values, Phi's build
-                double* yhat = sg + kSeg * 2 * NA;  // zero-start forward runs: end states of segments 0..2
-                double* ya = yhat + 3 * NA;         // true start states of segments 1..3
-                double* phat = ya + 3 * NA;         // zero-end backward runs: start values of segments 1..3
-                double* pb = phat + 3 * NA;         // true end values of segments 0..2
-                double* pN = pb + 3 * NA;
-                double* phb = pN + NA;              // Phi build (waves 1, 2), 2 NP + NU NA each
-                double* Phi = rh;                   // Phi_1, Phi_2 (rh: free in an fp64 iteration), pass 0 -> pass 1
-                const SegIO<G> io{A, B, F, d.sF};
-                const int aq = seg_a(wv, N), bq = seg_a(wv + 1, N);
-                if (pass) {  // the backward pass (pass 0's ran piped beside the factorisation)
-                    if (wv == kSeg - 1 && l < NA) pN[l] = l < NX ? yrt[N * NX + l] : 0.0;
-                    wsync();
-                    seg_backward<G>(io, aq, bq, wv == kSeg - 1 ? pN : nullptr, ybuf, yrt, rd, rt, ms, dU, wv == kSeg - 1,
-                                    wv >= 1 ? phat + (wv - 1) * NA : nullptr);
-                    __syncthreads();
-                    if (wv == 0) {
-                        if (l < NA) pb[2 * NA + l] = phat[2 * NA + l];  // p_{a_3}: segment 3 ran from the true p_N
-                        wsync();
-                        seg_carry<NA>(Phi + NP, pb + 2 * NA, phat + NA, pb + NA, true);
-                        seg_carry<NA>(Phi, pb + NA, phat, pb, true);
-                    }
-                    __syncthreads();
-                    if (wv < kSeg - 1) seg_backward<G>(io, aq, bq, pb + wv * NA, ybuf, yrt, rd, rt, ms, dU, true, nullptr);
-                    __syncthreads();
-                } else if (!piped) {
-                    if (wv == 0) riccati_solve<G>(c, d, L, sm, A, B, F, nullptr, dU, dX, yrt, rd, rt, 1);
-                    __syncthreads();
-                }
-                seg_forward<G>(io, aq, bq, nullptr, ybuf, dX, dU, wv == 0, wv < kSeg - 1 ? yhat + wv * NA : nullptr,
-                               (!pass && (wv == 1 || wv == 2)) ? phb + (wv - 1) * (2 * NP + G::NU * NA) : nullptr,
-                               Phi + (wv - 1) * NP);
-                __syncthreads();
-                if (wv == 0) {
-                    if (l < NA) ya[l] = yhat[l];  // y_{a_1}: segment 0 ran from the true y_0
-                    wsync();
-                    seg_carry<NA>(Phi, ya, yhat + NA, ya + NA, false);
-                    seg_carry<NA>(Phi + NP, ya + NA, yhat + 2 * NA, ya + 2 * NA, false);
-                }
-                __syncthreads();
-                if (wv >= 1) seg_forward<G>(io, aq, bq, ya + (wv - 1) * NA, ybuf, dX, dU, true, nullptr, nullptr, nullptr);
-            } else if (wv == 0) {  // the Newton solve: serial in the stages
+            if (wv == 0) {  // the Newton solve: serial in the stages
                 if (!hp) {  // (pass 0 with wave 2's backward pass: the forward pass only)
                     riccati_solve<G>(c, d, L, sm, A, B, F, nullptr, dU, dX, yrt, rd, rt, (!pass && piped) ? 2 : 3);
                 } else {
