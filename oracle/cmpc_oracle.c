@@ -95,6 +95,11 @@ long lab_pol_tried = 0, lab_pol_ok = 0; /* lab: polish attempts at iteration POL
 #ifdef GONDZIO
 long cmpc_gz_solves = 0; /* lab: corrector solves performed */
 #endif
+#ifdef LAB_DEGEN_COUNT
+/* lab: converged solves flagged for the polish by the degenerate-row test, and those whose polished point
+   replaced the endpoint (tools/degen_lab.py: the threshold's reach at a loose tol) */
+long cmpc_degen_flagged = 0, cmpc_degen_taken = 0;
+#endif
 /* after a step shorter than SHORT_STEP the next corrector centres with sigma >= SIGMA_MIN
    (kernels: kShortStep, kSigmaMin in internal.h) */
 #ifndef SHORT_STEP
@@ -2351,6 +2356,16 @@ static int solve_one_base(const shared_t* S, const agent_t* a, double tol, int m
     }
     if (S->polish && ((stop != 1 && stop != 4 && final_solve) || degen))
         pol_m = polish_one(S, a, wk, tol, U, sig, t, lam, wk->dU, wk->dsig, &pol_kkt);
+#ifdef LAB_DEGEN_COUNT
+    if (degen) {
+#pragma omp atomic
+        cmpc_degen_flagged += 1;
+        if (pol_m < best_m) {
+#pragma omp atomic
+            cmpc_degen_taken += 1;
+        }
+    }
+#endif
 #ifdef POLISH_DEBUG
     if (stop != 1) fprintf(stderr, "POL stop %d newton %d best_m %.2e pol_m %.2e\n", stop, S->newton, best_m, pol_m);
 #endif
