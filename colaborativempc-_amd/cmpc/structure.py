@@ -71,11 +71,11 @@ def _rows_of(X):
 def _dense_block(X, r0, r1, c0, c1):
     """X[r0:r1, c0:c1] as a dense array, read from the canonical csr arrays."""
     out = np.zeros((r1 - r0, c1 - c0))
-    for r in range(r0, r1):
-        s, e = X.indptr[r], X.indptr[r + 1]
-        c = X.indices[s:e]
-        m = (c >= c0) & (c < c1)
-        out[r - r0, c[m] - c0] = X.data[s:e][m]
+    s, e = X.indptr[r0], X.indptr[r1]
+    r = np.repeat(np.arange(r1 - r0), np.diff(X.indptr[r0:r1 + 1]))
+    c = X.indices[s:e]
+    m = (c >= c0) & (c < c1)
+    out[r[m], c[m] - c0] = X.data[s:e][m]
     return out
 
 
@@ -121,12 +121,96 @@ def reference_form(p, a=0):
     return _matrix(P), q, _matrix(G), h, _matrix(Aeq), beq
 
 
+_PATTERN_CACHE = {}
+
+
+def _sorted_pattern(rows, cols, shape):
+    """The canonical (row, then column) order of a list of entry slots: (order, rows, cols), read-only.
+    The slots of the reference form depend on the dimensions and the slack pattern only, so the sort
+    is done once per shape and a rebuild only drops the slots whose value is zero (_canon's result)."""
+    o = np.lexsort((cols, rows))
+    r, c = rows[o], cols[o]
+    if r.size > 1 and ((np.diff(r) == 0) & (np.diff(c) == 0)).any():
+        raise ValueError("duplicate entries")   # never for the reference form: one entry per slot
+    for a_ in (o, r, c):
+        a_.setflags(write=False)
+    return o, r, c, shape
+
+
+def _pattern(N, nx, ns, nu, mc, sl):
+    """Entry slots of G and Aeq of the reference form (LPV_Planner.py:251-380, :429-475) for these
+    dimensions and slack pattern ``sl`` (row_slack), in the order _reference_canon lists their values,
+    with their canonical order; plus the constant values of the input / input-rate slots."""
+    key = (N, nx, ns, nu, mc, sl.tobytes())
+    pat = _PATTERN_CACHE.get(key)
+    if pat is not None:
+        return pat
+    ne = nx + ns
+    nz = ne * (N + 1) + 2 * nu * N
+    cu, cd = ne * (N + 1), ne * (N + 1) + nu * N
+    # inequalities: stage rows C_{k,r} x_k (+ sign s_k[slack]), then per stage [u_i <= ub; -u_i <= -lb]
+    k = np.arange(1, N + 1)
+    r_st = (k - 1)[:, None, None] * mc + np.arange(mc)[None, :, None]          # (N, mc, 1)
+    c_st = k[:, None, None] * ne + np.arange(nx)[None, None, :]               # (N, 1, nx)
+    rows = [np.broadcast_to(r_st, (N, mc, nx)).ravel()]
+    cols = [np.broadcast_to(c_st, (N, mc, nx)).ravel()]
+    has = np.nonzero(sl >= 0)[0]
+    if has.size:
+        rows.append(((k - 1)[:, None] * mc + has[None, :]).ravel())
+        cols.append((k[:, None] * ne + nx + sl[has][None, :]).ravel())
+    ms = N * mc
+    ku = np.arange(N)[:, None]
+    iu = np.arange(nu)[None, :]
+    ru = ms + (ku * nu + iu) * 2
+    cu_i = cu + ku * nu + iu
+    rows += [ru.ravel(), (ru + 1).ravel()]
+    cols += [cu_i.ravel(), cu_i.ravel()]
+    G = _sorted_pattern(np.concatenate(rows), np.concatenate(cols), (ms + 2 * nu * N, nz))
+    g_const = np.concatenate([np.ones(N * nu), -np.ones(N * nu)])
+    # equalities: x_k - A_{k-1} x_{k-1} - B_{k-1} u_{k-1} = 0 (x_0 = x0), then the input-rate rows
+    ke = np.arange(N + 1)
+    rows = [(ke[:, None] * ne + np.arange(nx)).ravel()]
+    cols = [(ke[:, None] * ne + np.arange(nx)).ravel()]
+    kd = np.arange(1, N + 1)[:, None, None]
+    s_ = np.arange(nx)[None, :, None]
+    rows.append(np.broadcast_to(kd * ne + s_, (N, nx, nx)).ravel())
+    cols.append(np.broadcast_to((kd - 1) * ne + np.arange(nx)[None, None, :], (N, nx, nx)).ravel())
+    rows.append(np.broadcast_to(kd * ne + s_, (N, nx, nu)).ravel())
+    cols.append(np.broadcast_to(cu + (kd - 1) * nu + np.arange(nu)[None, None, :], (N, nx, nu)).ravel())
+    r0 = ne * (N + 1)
+    i = np.arange(N)[:, None]
+    j = np.arange(nu)[None, :]
+    rr = (r0 + i * nu + j).ravel()
+    first = (i == 0).repeat(nu, 1).ravel()
+    rows += [rr, rr, rr[~first]]
+    cols += [(cu + i * nu + j).ravel(), (cd + i * nu + j).ravel(), (cu + (i - 1) * nu + j).ravel()[~first]]
+    A = _sorted_pattern(np.concatenate(rows), np.concatenate(cols), (ne * (N + 1) + nu * N, nz))
+    a_const = np.concatenate([np.where(first, 1.0, -1.0), np.where(first, -1.0, 1.0), np.ones((~first).sum())])
+    for a_ in (g_const, a_const):
+        a_.setflags(write=False)
+    pat = dict(G=G, g_const=g_const, A=A, a_const=a_const, ones_x=np.ones((N + 1) * nx))
+    if len(_PATTERN_CACHE) > 64:
+        _PATTERN_CACHE.clear()
+    _PATTERN_CACHE[key] = pat
+    return pat
+
+
+def _fill(pat, vals):
+    """Canonical csr arrays of the slots ``pat`` holding ``vals`` (listed in slot order): the slots in
+    canonical order, those with a zero value dropped — equal to _canon of the same triples."""
+    o, r, c, shape = pat
+    v = vals[o]
+    keep = v != 0.0
+    indptr = np.zeros(shape[0] + 1, np.int64)
+    np.cumsum(np.bincount(r[keep], minlength=shape[0]), out=indptr[1:])
+    return indptr, c[keep], v[keep], shape
+
+
 def _reference_canon(p, a=0):
     """reference_form with the three matrices as canonical csr arrays (see _canon)."""
     nx, nu, N, ns, mc = (int(p[k]) for k in ("nx", "nu", "N", "ns", "mc"))
     ne = nx + ns
     nz = ne * (N + 1) + 2 * nu * N
-    cu, cd = ne * (N + 1), ne * (N + 1) + nu * N
     # cost
     Qt = np.zeros((ne, ne))
     Qt[:nx, :nx] = p["Q"]
@@ -135,57 +219,20 @@ def _reference_canon(p, a=0):
     P = _cost_matrix(N, Qt.shape[0], R_.shape[0], Qt.tobytes(), R_.tobytes(), dR_.tobytes())
     q = np.zeros(nz)
     q[: ne * (N + 1)].reshape(N + 1, ne)[:, :nx] = 2.0 * np.asarray(p["qlin"][a], float)
-    # inequalities: stage rows, then input rows
-    k = np.arange(1, N + 1)
-    r_st = (k - 1)[:, None, None] * mc + np.arange(mc)[None, :, None]          # (N, mc, 1)
-    c_st = k[:, None, None] * ne + np.arange(nx)[None, None, :]               # (N, 1, nx)
-    C = np.asarray(p["C"][a], float)
-    rows = [np.broadcast_to(r_st, C.shape).ravel()]
-    cols = [np.broadcast_to(c_st, C.shape).ravel()]
-    vals = [C.ravel()]
     sl = np.asarray(p["row_slack"])
-    sg = np.asarray(p["row_sign"], float)
+    pat = _pattern(N, nx, ns, nu, mc, sl)
+    # inequalities: stage rows, then input rows
     has = np.nonzero(sl >= 0)[0]
-    if has.size:
-        rows.append(((k - 1)[:, None] * mc + has[None, :]).ravel())
-        cols.append((k[:, None] * ne + nx + sl[has][None, :]).ravel())
-        vals.append(np.broadcast_to(sg[has], (N, has.size)).ravel())
-    ms = N * mc
-    ku = np.arange(N)[:, None]
-    iu = np.arange(nu)[None, :]
-    ru = ms + (ku * nu + iu) * 2
-    cu_i = cu + ku * nu + iu
-    rows += [ru.ravel(), (ru + 1).ravel()]
-    cols += [cu_i.ravel(), cu_i.ravel()]
-    vals += [np.ones(N * nu), -np.ones(N * nu)]
-    G = _canon(np.concatenate(rows), np.concatenate(cols), np.concatenate(vals).astype(np.float64),
-               (ms + 2 * nu * N, nz))
+    sg = np.asarray(p["row_sign"], float)
+    G = _fill(pat["G"], np.concatenate([np.asarray(p["C"][a], float).ravel(), np.tile(sg[has], N),
+                                        pat["g_const"]]))
     h = np.concatenate([np.asarray(p["h"][a], float).ravel(),
                         np.stack([np.broadcast_to(np.asarray(p["u_ub"], float), (N, nu)),
                                   np.broadcast_to(-np.asarray(p["u_lb"], float), (N, nu))], -1).ravel()])
     # equalities
-    ke = np.arange(N + 1)
-    rows = [(ke[:, None] * ne + np.arange(nx)).ravel()]
-    cols = [(ke[:, None] * ne + np.arange(nx)).ravel()]
-    vals = [np.ones((N + 1) * nx)]
-    kd = np.arange(1, N + 1)[:, None, None]
-    s_ = np.arange(nx)[None, :, None]
-    rows.append(np.broadcast_to(kd * ne + s_, (N, nx, nx)).ravel())
-    cols.append(np.broadcast_to((kd - 1) * ne + np.arange(nx)[None, None, :], (N, nx, nx)).ravel())
-    vals.append(-np.asarray(p["A"][a], float).ravel())
-    rows.append(np.broadcast_to(kd * ne + s_, (N, nx, nu)).ravel())
-    cols.append(np.broadcast_to(cu + (kd - 1) * nu + np.arange(nu)[None, None, :], (N, nx, nu)).ravel())
-    vals.append(-np.asarray(p["B"][a], float).ravel())
+    Aeq = _fill(pat["A"], np.concatenate([pat["ones_x"], -np.asarray(p["A"][a], float).ravel(),
+                                          -np.asarray(p["B"][a], float).ravel(), pat["a_const"]]))
     r0 = ne * (N + 1)
-    i = np.arange(N)[:, None]
-    j = np.arange(nu)[None, :]
-    rr = (r0 + i * nu + j).ravel()
-    first = (i == 0).repeat(nu, 1).ravel()
-    rows += [rr, rr, rr[~first]]
-    cols += [(cu + i * nu + j).ravel(), (cd + i * nu + j).ravel(), (cu + (i - 1) * nu + j).ravel()[~first]]
-    vals += [np.where(first, 1.0, -1.0), np.where(first, -1.0, 1.0), np.ones((~first).sum())]
-    Aeq = _canon(np.concatenate(rows), np.concatenate(cols), np.concatenate(vals).astype(np.float64),
-                 (ne * (N + 1) + nu * N, nz))
     beq = np.zeros(Aeq[3][0])
     beq[:nx] = p["x0"][a]
     beq[r0:r0 + nu] = p["u_prev"][a]

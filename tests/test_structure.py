@@ -93,3 +93,31 @@ def test_non_canonical_inputs_are_recognised_alike():
         assert p is not None
         for k, v in ref.items():
             np.testing.assert_array_equal(p[k], v)
+
+
+def test_zero_entries_drop_out_of_the_rebuilt_pattern():
+    """reference_form fills a per-shape cached slot pattern (cmpc.structure._pattern) and drops the
+    slots whose value is zero: a structured problem with zeros in C_k, A_k, B_k rebuilds into
+    canonical csr (sorted, no stored zeros) with exactly that many entries fewer, and is recognised
+    back into the same problem."""
+    _, c = next(iter(lpv_qps("lpv_n30_a3")))
+    p = St.recognize(*_args(c))
+    P0, q0, G0, h0, A0, b0 = St.reference_form(p)
+    p2 = {k: (v.copy() if isinstance(v, np.ndarray) else v) for k, v in p.items()}
+    rng = np.random.default_rng(3)
+    dropped = {}
+    for k, mat in (("C", G0), ("A", A0), ("B", A0)):
+        v = p2[k].reshape(-1)
+        nzi = np.flatnonzero(v)
+        pick = rng.choice(nzi, size=min(7, nzi.size), replace=False)
+        v[pick] = 0.0
+        dropped[k] = pick.size
+    P, q, G, h, A, b = St.reference_form(p2)
+    for M in (G, A):
+        assert M.has_canonical_format and (M.data != 0).all()
+    assert G.nnz == G0.nnz - dropped["C"]
+    assert A.nnz == A0.nnz - dropped["A"] - dropped["B"]
+    back = St.recognize(P, q, G, h, A, b)
+    assert back is not None
+    for k, v in p2.items():
+        np.testing.assert_array_equal(back[k], v)
