@@ -137,6 +137,15 @@ def _sorted_pattern(rows, cols, shape):
     return o, r, c, shape
 
 
+def _slot_keys(pat):
+    """(sorted row * ncols + col keys, slot of each) of a _sorted_pattern: the lookup that maps a
+    canonical csr entry to its slot (recognize)."""
+    o, r, c, shape = pat
+    keys = r.astype(np.int64) * shape[1] + c
+    keys.setflags(write=False)
+    return keys, o
+
+
 def _pattern(N, nx, ns, nu, mc, sl):
     """Entry slots of G and Aeq of the reference form (LPV_Planner.py:251-380, :429-475) for these
     dimensions and slack pattern ``sl`` (row_slack), in the order _reference_canon lists their values,
@@ -188,7 +197,8 @@ def _pattern(N, nx, ns, nu, mc, sl):
     a_const = np.concatenate([np.where(first, 1.0, -1.0), np.where(first, -1.0, 1.0), np.ones((~first).sum())])
     for a_ in (g_const, a_const):
         a_.setflags(write=False)
-    pat = dict(G=G, g_const=g_const, A=A, a_const=a_const, ones_x=np.ones((N + 1) * nx))
+    pat = dict(G=G, g_const=g_const, A=A, a_const=a_const, ones_x=np.ones((N + 1) * nx), G_keys=_slot_keys(G),
+               A_keys=_slot_keys(A), nC=N * mc * nx, nS=N * has.size, has=has, nA=N * nx * nx, nB=N * nx * nu)
     if len(_PATTERN_CACHE) > 64:
         _PATTERN_CACHE.clear()
     _PATTERN_CACHE[key] = pat
@@ -239,9 +249,109 @@ def _reference_canon(p, a=0):
     return P, q, G, h, Aeq, beq
 
 
+def _slots_of(X, keys_slots, nslots):
+    """Values of the canonical csr X in the slot order of a pattern (absent slots 0), or None when X
+    holds an entry outside the pattern."""
+    keys, slot = keys_slots
+    k = _rows_of(X).astype(np.int64) * X.shape[1] + X.indices
+    i = np.searchsorted(keys, k)
+    if k.size and (i[-1] >= keys.size or not np.array_equal(keys[np.minimum(i, keys.size - 1)], k)):
+        return None
+    vals = np.zeros(nslots)
+    vals[slot[i]] = X.data
+    return vals
+
+
 def recognize(P, q, G, h, A, b, layout=LPV_LAYOUT):
     """Structured single-agent problem dict (batch axis of 1) if (P, q, G, h, A, b) is exactly
-    a reference-form agent QP of the given layout, else None."""
+    a reference-form agent QP of the given layout, else None.
+
+    Every entry of G and Aeq is mapped to its slot of the reference form's pattern (cached per
+    shape and slack pattern, _pattern); the structured quantities are read from the slots and the
+    QP is accepted only when no entry lies outside the pattern and the fixed slots (identities, the
+    +-1 input rows, the slack signs of every stage), P, q, h and b are the reference form's — the
+    same QPs _recognize_rebuild accepts by rebuilding them (tests/test_structure.py compares the two)."""
+    if G is None or A is None or h is None or b is None:
+        return None
+    nx, ns, nu = layout
+    ne = nx + ns
+    P, G, A = _csr(P), _csr(G), _csr(A)
+    q, h, b = (np.asarray(v, dtype=np.float64).ravel() for v in (q, h, b))
+    nz = P.shape[1]
+    if P.shape != (nz, nz) or G.shape[1] != nz or A.shape[1] != nz or q.size != nz or \
+            h.size != G.shape[0] or b.size != A.shape[0]:
+        return None
+    d = dims_of(nz, G.shape[0], A.shape[0], layout)
+    if d is None:
+        return None
+    N, mc = d
+    cu, cd = ne * (N + 1), ne * (N + 1) + nu * N
+    if not (np.isfinite(q).all() and np.isfinite(b).all()) or np.isnan(h).any():
+        return None
+    # cost (P / 2 and q / 2 are exact in binary floating point)
+    Pd = _dense_block(P, 0, ne, 0, ne) / 2.0
+    Q, Qs = Pd[:nx, :nx], np.diag(Pd[nx:, nx:]).copy()
+    R = _dense_block(P, cu, cu + nu, cu, cu + nu) / 2.0
+    dR = _dense_block(P, cd, cd + nu, cd, cd + nu) / 2.0
+    if ns and not (Qs > 0).all():
+        return None
+    Qt = np.zeros((ne, ne))
+    Qt[:nx, :nx] = Q
+    Qt[nx:, nx:] = np.diag(Qs)
+    if not _same_canon(P, _cost_matrix(N, ne, nu, Qt.tobytes(), np.ascontiguousarray(R).tobytes(),
+                                       np.ascontiguousarray(dR).tobytes())):
+        return None
+    qlin = q[: ne * (N + 1)].reshape(N + 1, ne)[:, :nx] / 2.0
+    q2 = np.zeros(nz)
+    q2[: ne * (N + 1)].reshape(N + 1, ne)[:, :nx] = 2.0 * qlin
+    if not np.array_equal(q, q2):
+        return None
+    # slack pattern from the stage-1 rows (the slots check every stage)
+    row_slack = -np.ones(mc, np.int32)
+    row_sign = np.ones(mc, np.int32)
+    e1 = G.indptr[mc]
+    r1, c1, v1 = _rows_of(G)[:e1], G.indices[:e1], G.data[:e1]
+    ss = (c1 >= ne + nx) & (c1 < 2 * ne)
+    for rr_, cc_, vv_ in zip(r1[ss], c1[ss], v1[ss]):
+        if row_slack[rr_] >= 0 or vv_ not in (1.0, -1.0):
+            return None
+        row_slack[rr_] = cc_ - ne - nx
+        row_sign[rr_] = int(vv_)
+    pat = _pattern(N, nx, ns, nu, mc, row_slack)
+    nC, nS, has = pat["nC"], pat["nS"], pat["has"]
+    gv = _slots_of(G, pat["G_keys"], nC + nS + pat["g_const"].size)
+    if gv is None or not np.array_equal(gv[nC:nC + nS], np.tile(row_sign[has].astype(np.float64), N)) \
+            or not np.array_equal(gv[nC + nS:], pat["g_const"]):
+        return None
+    n1, nA, nB = pat["ones_x"].size, pat["nA"], pat["nB"]
+    av = _slots_of(A, pat["A_keys"], n1 + nA + nB + pat["a_const"].size)
+    if av is None or not np.array_equal(av[:n1], pat["ones_x"]) or \
+            not np.array_equal(av[n1 + nA + nB:], pat["a_const"]):
+        return None
+    Cm = gv[:nC].reshape(N, mc, nx)
+    Am = (0.0 - av[n1:n1 + nA]).reshape(N, nx, nx)          # 0.0 - v: an absent slot gives +0.0
+    Bm = (0.0 - av[n1 + nA:n1 + nA + nB]).reshape(N, nx, nu)
+    ms = N * mc
+    hu = h[ms:].reshape(N, nu, 2)
+    if not np.array_equal(hu, np.broadcast_to(hu[0], hu.shape)):
+        return None
+    x0 = b[:nx].copy()
+    u_prev = b[cu: cu + nu].copy()
+    b2 = np.zeros(b.size)
+    b2[:nx] = x0
+    b2[cu:cu + nu] = u_prev
+    if not np.array_equal(b, b2):
+        return None
+    hh = h[:ms].reshape(N, mc).copy()
+    u_ub, u_lb = hu[0, :, 0].copy(), -hu[0, :, 1]
+    return dict(nx=nx, nu=nu, N=N, ns=ns, mc=mc, Q=Q, R=R, dR=dR, Qs=Qs, u_ub=u_ub, u_lb=u_lb,
+                row_slack=row_slack, row_sign=row_sign, A=Am[None], B=Bm[None], x0=x0[None], u_prev=u_prev[None],
+                qlin=qlin[None], C=Cm[None], h=hh[None])
+
+
+def _recognize_rebuild(P, q, G, h, A, b, layout=LPV_LAYOUT):
+    """recognize by extraction and an exact rebuild (the round-5 form, kept as the tests' reference
+    for the slot-based recognize)."""
     if G is None or A is None or h is None or b is None:
         return None
     nx, ns, nu = layout

@@ -121,3 +121,50 @@ def test_zero_entries_drop_out_of_the_rebuilt_pattern():
     assert back is not None
     for k, v in p2.items():
         np.testing.assert_array_equal(back[k], v)
+
+
+def _same_result(p, p0):
+    if p is None or p0 is None:
+        return p is None and p0 is None
+    return p.keys() == p0.keys() and all(np.array_equal(np.asarray(p[k]), np.asarray(p0[k])) for k in p0)
+
+
+def test_slot_recogniser_agrees_with_the_rebuild_on_perturbed_qps():
+    """recognize reads the structured quantities from the slots of a cached pattern and checks the
+    fixed slots; _recognize_rebuild extracts and rebuilds the whole QP.  On every captured QP and on
+    seeded single-entry perturbations of them (values changed, entries added outside the pattern or
+    removed, a later stage's slack sign or input row flipped, bounds varying by stage, b or q
+    non-zero off the pattern) both accept the same QPs with the same result."""
+    rng = np.random.default_rng(11)
+    cases = [c for nm in ("lpv_n10_a2", "lpv_n30_a3") for _, c in list(lpv_qps(nm))[:3]]
+    n_acc = n_ref = 0
+    for c in cases:
+        base = _args(c)
+        assert _same_result(St.recognize(*base), St._recognize_rebuild(*base))
+        for trial in range(40):
+            P, q, G, h, A, b = (x.copy() for x in base)
+            which = trial % 8
+            if which in (0, 1):                        # a G entry: change, or add one anywhere
+                G = G.tolil()
+                r, k = rng.integers(G.shape[0]), rng.integers(G.shape[1])
+                G[r, k] = G[r, k] * -1.0 if (which == 0 and G[r, k] != 0) else rng.choice([1.0, -1.0, 0.5])
+                G = G.tocsr()
+            elif which in (2, 3):                      # an Aeq entry: change, add or remove
+                A = A.tolil()
+                r, k = rng.integers(A.shape[0]), rng.integers(A.shape[1])
+                A[r, k] = 0.0 if which == 2 else (A[r, k] + 1.0)
+                A = A.tocsr()
+            elif which == 4:                           # h anywhere
+                h[rng.integers(h.size)] += rng.choice([0.0, 1.0])
+            elif which == 5:                           # b anywhere
+                b[rng.integers(b.size)] += rng.choice([0.0, 1e-3])
+            elif which == 6:                           # q anywhere
+                q[rng.integers(q.size)] += rng.choice([0.0, 2.0])
+            else:                                      # an existing G entry's value scaled (slack signs, +-1 rows)
+                G = G.copy()
+                G.data[rng.integers(G.nnz)] *= rng.choice([-1.0, 2.0])
+            p, p0 = St.recognize(P, q, G, h, A, b), St._recognize_rebuild(P, q, G, h, A, b)
+            assert _same_result(p, p0), (which, trial)
+            n_acc += p is not None
+            n_ref += p is None
+    assert n_acc > 20 and n_ref > 100   # both outcomes exercised
